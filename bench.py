@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""Headline benchmark: k=19 k-mer counting of the E. coli-sized pair at ART 30x (BASELINE.json
+configs[1], "C2") on MI355X, plus the categorization SDK lookup of Nanosim-H-like 75x long
+reads against the C2 export at [10,25] (configs[2], "C3"), with the CPU oracle timed beside it.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-lookup]
+
+A step is one pass of the counting hot path over the resident reads: bin + per-file count +
+merge (hga_count_run), the specificity histogram (hga_count_spec_hist) and the sorted export
+selection at [10,25] (hga_count_select_device) — everything jf_occurrences does on the device.
+Inputs are resident in HBM before the timed region.  N > 1 (torchrun, one rank per GPU): every
+rank counts its own C2-sized shard of reads (weak scaling); barrier + max-over-ranks timing.
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "hybrid-genome-assembler_amd")]
+import hga  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+K = 19
+LA, LB = 4_641_652, 5_065_741  # MG1655, UTI89 lengths
+DIV = 0.021
+READ_LEN = 150
+COVERAGE = 30
+LOWER, UPPER = 10, 25
+THRESHOLDS = [70.0, 85.0, 90.0, 95.0, 99.0, 100.0, 100.01]
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_c2(rank):
+    ga = hga.gen_genome(LA, 1)
+    gb = hga.gen_haplotype(ga, DIV, LB - LA, 2)
+    na, nb = COVERAGE * LA // READ_LEN, COVERAGE * LB // READ_LEN
+    ra = hga.gen_art(ga, na, READ_LEN, 1000 + 2 * rank)
+    rb = hga.gen_art(gb, nb, READ_LEN, 1001 + 2 * rank)
+    return ga, gb, ra, rb
+
+
+def make_c3(ga, gb, rank):
+    na, nb = round(LA / 7777 * 75), round(LB / 7777 * 75)
+    ra = hga.gen_nanosim(ga, na, 3000 + 2 * rank)
+    rb = hga.gen_nanosim(gb, nb, 3001 + 2 * rank)
+    bases = ra.bases + rb.bases
+    offsets = np.concatenate([ra.offsets, rb.offsets[1:] + ra.offsets[-1]]).astype(np.uint64)
+    return bases, offsets
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch measured by a separate rocprofv3 --pmc pass (profiles/), if any."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+class Dist:
+    def __init__(self, n):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl")
+            self.torch, self.dist = torch, dist
+            self.pg = True
+        if n != self.world and self.world > 1:
+            log(f"warning: --gpus {n} but WORLD_SIZE={self.world}")
+
+    def barrier(self):
+        if self.pg:
+            self.torch.cuda.synchronize()
+            self.dist.barrier()
+
+    def max(self, v):
+        if not self.pg:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v):
+        if not self.pg:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.dist.destroy_process_group()
+
+
+def count_step(ctx):
+    ctx.count_run(2)
+    ctx.spec_hist(THRESHOLDS)
+    return ctx.select_device(LOWER, UPPER)
+
+
+KERNEL_BYTES = {
+    # algorithmic bytes per launch, from the per-unit figures in DESIGN.md §4
+    "kc_hist": lambda s: s["bytes"],                                    # 1 B/base read
+    "kc_bin": lambda s: s["bytes"] + 4 * s["instances"],                # 1 B/base + 4 B/instance written
+    "kc_count": lambda s: 4 * s["instances"] + (8 + 4 * s["files"]) * s["rows"],   # read binned, write rows
+}
+
+
+def cpu_baseline(ra, rb, threads):
+    """The oracle (C++ restatement, multi-threaded) over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    frac = 4   # a quarter of each file's reads
+    sa = ra.seq[: ra.seq.find(b"\n", len(ra.seq) // frac)]
+    sb = rb.seq[: rb.seq.find(b"\n", len(rb.seq) // frac)]
+    inst = oracle.count_instances(sa, K) + oracle.count_instances(sb, K)
+    t0 = time.perf_counter()
+    dumps = [oracle.count_stream(s, K, 2, threads=threads) for s in (sa, sb)]
+    keys, counts = oracle.merge(dumps)
+    oracle.specificity(counts, THRESHOLDS)
+    oracle.select(keys, counts, LOWER, UPPER)
+    dt = time.perf_counter() - t0
+    return {"value": inst / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+            "sample": f"first 1/{frac} of each C2 read file ({inst} 19-mer windows); oracle count "
+                      f"(std::unordered_map, {threads} threads) + merge + specificity + select",
+            "seconds": round(dt, 3)}
+
+
+def cpu_lookup_baseline(bases, offsets, sdk, threads):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n = min(len(offsets) - 1, 6000)
+    sub_off = offsets[: n + 1]
+    sub = bases[: int(sub_off[-1])]
+    t0 = time.perf_counter()
+    oracle.lookup_hits_mt(sub, sub_off, K, sdk, threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "reads/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} C3 reads, std::unordered_set lookup of every window, {threads} threads",
+            "seconds": round(dt, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-lookup", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("HGA_CPU_THREADS", "16")))
+    args = ap.parse_args()
+    D = Dist(args.gpus)
+    dev = D.local
+    t_gen = time.perf_counter()
+    ga, gb, ra, rb = make_c2(D.rank)
+    log(f"[rank {D.rank}] C2 generated in {time.perf_counter() - t_gen:.1f}s: {ra.n + rb.n} reads")
+
+    ctx = hga.Ctx(dev)
+    ctx.count_begin(K, 2)
+    ctx.count_add(0, ra.seq)
+    ctx.count_add(1, rb.seq)
+    for _ in range(args.warmup):
+        count_step(ctx)
+    st = ctx.count_stats()
+    stats = {"bytes": st.bytes, "instances": st.instances, "rows": st.distinct_rows, "files": 2}
+    ctx.profile(True)
+    ctx.profile_reset()
+    D.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n_sel, n_disc = count_step(ctx)
+    ctx.sync()
+    D.barrier()
+    dt = time.perf_counter() - t0
+    dt_max = D.max(dt)
+    ms_step = dt_max / args.steps * 1e3
+    inst_total = D.sum(float(st.instances))
+    value = inst_total / (dt_max / args.steps)
+
+    kernels = {}
+    for name in ("kc_hist", "kc_scan", "kc_bin", "kc_count", "kc_spec_hist", "kc_select", "radix_upsweep",
+                 "radix_downsweep", "scan"):
+        ms, n = ctx.profile_get(name)
+        if n:
+            kernels[name] = {"ms_total": ms, "launches": n, "ms_per_step": ms / args.steps}
+    ctx.profile(False)
+    dom = max(("kc_hist", "kc_bin", "kc_count"), key=lambda k: kernels.get(k, {}).get("ms_total", 0))
+    per_step_launches = kernels[dom]["launches"] / args.steps
+    avg_launch_ms = kernels[dom]["ms_total"] / kernels[dom]["launches"]
+    bytes_step = KERNEL_BYTES[dom](stats)
+    bytes_launch = bytes_step / per_step_launches
+    achieved = bytes_launch / (avg_launch_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(dom)
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_launch_ms, 4)}
+    # SURVEY.md §8(d) whole-counting model: 16.25 B per k-mer instance over the step time
+    pipe_gbs = 16.25 * st.instances / (ms_step * 1e-3) / 1e9
+    result = {
+        "metric": "k-mers/s counted + reads/s categorized, k=19 E.coli 30×; %HBM roofline",
+        "value": round(value, 1), "unit": "k-mers/s", "n_gpus": D.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": "C2: k=19 count of an E. coli-sized pair (4.64 + 5.07 Mb, d=0.021), ART-like 30x "
+                               "150 bp, 2 files; per step: count_run + spec_hist + select[10,25]",
+                   "k": K, "reads": ra.n + rb.n, "bases": st.bytes, "instances_per_gpu": st.instances,
+                   "distinct_rows": st.distinct_rows, "selected": n_sel, "discriminative": n_disc,
+                   "buckets": st.buckets, "parallelism": f"dp{D.world}",
+                   "exchange": "none: ranks count independent shards (replicas)" if D.world > 1 else None},
+        "roofline": roofline,
+        "pipeline_roofline": {"model": "16.25 B per k-mer instance (SURVEY.md §8(d))",
+                              "achieved": round(pipe_gbs, 1), "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)},
+        "kernels_ms_per_step": {k: round(v["ms_per_step"], 4) for k, v in kernels.items()},
+    }
+
+    if not args.no_lookup:
+        t_gen = time.perf_counter()
+        bases, offsets = make_c3(ga, gb, D.rank)
+        log(f"[rank {D.rank}] C3 generated in {time.perf_counter() - t_gen:.1f}s: {len(offsets) - 1} reads")
+        ctx2 = hga.Ctx(dev)
+        ctx.count_run(2)
+        sdk, _, _ = ctx.select(LOWER, UPPER)
+        ctx2.lookup_load(K, sdk)
+        ctx2.lookup_set_reads(bases, offsets, 1)
+        ctx2.lookup_run()
+        ctx2.profile(True)
+        ctx2.profile_reset()
+        D.barrier()
+        t0 = time.perf_counter()
+        reps = max(1, min(args.steps, 3))
+        for _ in range(reps):
+            ctx2.lookup_run()
+        ctx2.sync()
+        D.barrier()
+        dtl = D.max((time.perf_counter() - t0) / reps)
+        s = ctx2.lookup_sizes()
+        lk = {}
+        for name in ("lk_count", "lk_emit", "lk_post", "radix_upsweep", "radix_downsweep", "scan"):
+            ms, n = ctx2.profile_get(name)
+            if n:
+                lk[name] = round(ms / reps, 4)
+        lk_ms = lk.get("lk_count", 0) + lk.get("lk_emit", 0)
+        lk_bytes = s.windows * 2 * 12.25 + 12 * s.hits    # two walks: 0.25 B input + 12 B slot read per window
+        result["categorize"] = {
+            "workload": "C3: Nanosim-H-like 75x long reads of the C2 pair vs the C2 [10,25] export (k=19)",
+            "reads": int(s.n_reads), "bases": int(len(bases)), "windows": int(s.windows), "hits": int(s.hits),
+            "sdk": int(s.n_sdk), "ms": round(dtl * 1e3, 3), "reads_per_s": round(D.sum(s.n_reads) / dtl, 1),
+            "windows_per_s": round(D.sum(s.windows) / dtl, 1), "kernels_ms": lk,
+            "lookup_roofline": {"model": "12.25 B per window per walk + 12 B per hit (SURVEY.md §8(d))",
+                                "achieved": round(lk_bytes / (lk_ms * 1e-3) / 1e9, 1) if lk_ms else None},
+        }
+        ctx2.close()
+        if not args.no_cpu and D.rank == 0:
+            result["categorize"]["cpu_baseline"] = cpu_lookup_baseline(bases, offsets, sdk, args.cpu_threads)
+
+    if not args.no_cpu and D.rank == 0:
+        result["cpu_baseline"] = cpu_baseline(ra, rb, args.cpu_threads)
+    ctx.close()
+    D.close()
+    if D.rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

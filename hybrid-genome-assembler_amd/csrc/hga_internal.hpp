@@ -1,0 +1,184 @@
+// Internal host-side state of libhga: the context, device buffers, error plumbing and
+// the per-kernel event profiler.  Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/hga.h"
+
+namespace hga {
+
+// Exceptions never cross the ABI: api.hip catches them and maps them to a status.
+struct Error : std::runtime_error {
+    hga_status code;
+    Error(hga_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HGA_HIP(call)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            throw ::hga::Error(e_ == hipErrorOutOfMemory ? HGA_ERR_OOM : HGA_ERR_HIP,     \
+                               std::string(#call) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+#define HGA_REQUIRE(cond, code, msg)                           \
+    do {                                                       \
+        if (!(cond)) throw ::hga::Error((code), (msg));        \
+    } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    void* ensure(size_t bytes) {
+        if (bytes <= cap && p) return p;
+        release();
+        size_t b = bytes ? bytes : 16;
+        HGA_HIP(hipMalloc(&p, b));
+        cap = b;
+        return p;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+// Per-kernel event timing on the ctx stream (hga_profile_*).
+struct Profiler {
+    bool on = false;
+    struct Rec { std::string name; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    std::map<std::string, std::pair<double, uint64_t>> acc;
+
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e;
+        HGA_HIP(hipEventCreate(&e));
+        return e;
+    }
+    void drain() {
+        for (auto& r : pending) {
+            float ms = 0.f;
+            HGA_HIP(hipEventSynchronize(r.b));
+            HGA_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+            auto& s = acc[r.name];
+            s.first += ms;
+            s.second += 1;
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+        pending.clear();
+    }
+    ~Profiler() {
+        for (auto& r : pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+struct CountState {
+    bool begun = false, ran = false;
+    int k = 0;
+    uint32_t n_files = 0;
+    uint32_t min_per_file = 2;
+    // per-file resident sequence bytes
+    std::vector<DevBuf*> seq;
+    std::vector<uint64_t> seq_len;
+    // pipeline scratch
+    DevBuf st_hist, st_off, bucket_base, bucket_tot, file_start, binned, rows_key, rows_cnt,
+        cursor, scratch, sel_keys, sel_tmp, hist_dense, hist_over, misc;
+    uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
+    uint32_t buckets = 0, fb = 0, max_split = 1;
+    ~CountState() {
+        for (auto* b : seq) delete b;
+    }
+};
+
+struct LookupState {
+    bool loaded = false, have_reads = false, ran = false;
+    int k = 0;
+    uint32_t n_sdk = 0;
+    uint64_t slots = 0;
+    DevBuf tab_key, tab_id;
+    uint64_t n_reads = 0, n_bases = 0;
+    uint32_t first_read_id = 1;
+    DevBuf bases, offsets;
+    // results
+    DevBuf tile_cnt, hit_read, hit_kid, hit_pos, hit_ptr, s_key, s_val, s_key2, s_val2,
+        first_flag, first_kid, first_pos, first_read, first_ptr, kci_key, kci_val, kci_ptr, scratch,
+        scratch2;
+    std::vector<uint64_t> h_offsets;
+    uint64_t windows = 0, hits = 0, firsts = 0, reads_hit = 0;
+};
+
+}  // namespace hga
+
+struct hga_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int num_cu = 256;
+    hga::Profiler prof;
+    hga::CountState count;
+    hga::LookupState lookup;
+    hga::DevBuf pinned_dummy;
+
+    // Launch helper: records events around the launch when profiling is on.
+    template <class F>
+    void launch(const char* name, F&& f) {
+        if (!prof.on) { f(); return; }
+        hipEvent_t a = prof.get(), b = prof.get();
+        HGA_HIP(hipEventRecord(a, stream));
+        f();
+        HGA_HIP(hipEventRecord(b, stream));
+        prof.pending.push_back({name, a, b});
+        if (prof.pending.size() > 4096) prof.drain();
+    }
+    void check_launch(const char* name) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) throw hga::Error(HGA_ERR_HIP, std::string(name) + ": " + hipGetErrorString(e));
+    }
+    void sync() { HGA_HIP(hipStreamSynchronize(stream)); }
+};
+
+// Entry points implemented in count.hip / lookup.hip (called from api.hip).
+namespace hga {
+void count_begin(hga_ctx* c, int k, uint32_t n_files);
+void count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n);
+void count_run(hga_ctx* c, uint32_t min_per_file);
+void count_spec_hist(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out);
+void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* n_discr);
+void count_fetch_selected(hga_ctx* c, uint64_t* dst, uint8_t* flags);
+void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);
+
+void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n);
+void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, uint64_t n,
+                      uint32_t first_id);
+void lookup_run(hga_ctx* c);
+void lookup_sizes(hga_ctx* c, hga_lookup_sizes* out);
+void lookup_fetch(hga_ctx* c, const hga_lookup_result* out);
+
+// radix sort (sort.hip): stable LSD sort of `n` keys by their low `bits` bits, with an
+// optional u32 payload.  Result ends in keys/vals (scratch used as ping-pong).
+void radix_sort_u64(hga_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n, int bits,
+                    DevBuf& scratch);
+void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int bits,
+                    DevBuf& scratch);
+// exclusive scan of u64 in place (sort.hip)
+void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
+}  // namespace hga

@@ -1,0 +1,276 @@
+// sort.hip — stable LSD radix sort and exclusive scans (gfx950, wave64).
+//
+// Used for everything that needs the reference's orders: the exported k-mers
+// ascending (== LC_ALL=C order, run_jellyfish.sh:6), per-read sorted KmerID lists
+// (ReadClusteringEngine.cpp:272) and kmer_component_index (:282-284).
+//
+// Per 8-bit digit pass: upsweep (per-tile digit histogram, digit-major so one
+// linear exclusive scan gives every (digit, tile) output offset), scan, downsweep
+// (stable in-tile rank via 64-lane ballot matching, staged through LDS so the global
+// writes leave in digit runs).
+#include "hga_internal.hpp"
+#include "kmer_dev.hpp"
+
+namespace hga {
+namespace {
+
+constexpr int RS_T = 256;              // threads per tile
+constexpr int RS_I = 16;               // items per thread
+constexpr int RS_TILE = RS_T * RS_I;   // 4096 keys per tile
+constexpr int SC_T = 1024, SC_I = 4, SC_TILE = SC_T * SC_I;
+
+template <class K>
+__global__ void __launch_bounds__(RS_T) rs_upsweep(const K* __restrict__ keys, uint64_t n,
+                                                   int shift, uint32_t* __restrict__ counts,
+                                                   uint32_t n_tiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        uint64_t i = base + (uint64_t)j * RS_T + threadIdx.x;
+        if (i < n) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    counts[(uint64_t)threadIdx.x * n_tiles + blockIdx.x] = h[threadIdx.x];
+}
+
+template <class K, bool HAS_V>
+__global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
+                                                     const uint32_t* __restrict__ vin,
+                                                     K* __restrict__ kout,
+                                                     uint32_t* __restrict__ vout, uint64_t n,
+                                                     int shift,
+                                                     const uint32_t* __restrict__ offs,
+                                                     uint32_t n_tiles) {
+    __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint32_t ws[8];
+    __shared__ K sk[RS_TILE];
+    __shared__ uint32_t sv[HAS_V ? RS_TILE : 1];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < 4 * 256; i += RS_T) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    K key[RS_I];
+    uint32_t val[RS_I];
+    uint32_t dig[RS_I];
+    uint32_t rank[RS_I];
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        const uint64_t i = base + (uint64_t)wave * 1024 + (uint64_t)j * 64 + lane;
+        const bool ok = i < n;
+        key[j] = ok ? kin[i] : K(0);
+        if (HAS_V) val[j] = ok ? vin[i] : 0u;
+        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & 255u) : 256u;
+    }
+    // Stable rank inside the wave: items in (j, lane) order.
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        const uint32_t d = dig[j];
+        const bool ok = d < 256u;
+        uint64_t m = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        uint32_t before = 0;
+        if (ok) before = wcnt[wave][d];
+        rank[j] = before + (uint32_t)__popcll(m & lt);
+        if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // digit starts inside the tile, then per-wave starts
+    {
+        const int d = tid;
+        const uint32_t c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<RS_T>(c0 + c1 + c2 + c3, ws, &tot);
+        dstart[d] = ex;
+        wcnt[0][d] = ex;
+        wcnt[1][d] = ex + c0;
+        wcnt[2][d] = ex + c0 + c1;
+        wcnt[3][d] = ex + c0 + c1 + c2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        if (dig[j] < 256u) {
+            const uint32_t lp = wcnt[wave][dig[j]] + rank[j];
+            sk[lp] = key[j];
+            if (HAS_V) sv[lp] = val[j];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
+    for (uint32_t i = tid; i < cnt; i += RS_T) {
+        const K kk = sk[i];
+        const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+        const uint64_t g = (uint64_t)offs[(uint64_t)d * n_tiles + blockIdx.x] + (i - dstart[d]);
+        kout[g] = kk;
+        if (HAS_V) vout[g] = sv[i];
+    }
+}
+
+// ---- exclusive scans --------------------------------------------------------------
+template <class T>
+__global__ void __launch_bounds__(SC_T) sc_reduce(const T* __restrict__ in, uint64_t n,
+                                                  uint64_t* __restrict__ sums) {
+    __shared__ uint64_t ws[SC_T / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_I;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_I; ++j)
+        if (base + j < n) s += (uint64_t)in[base + j];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    s = wave_incl_scan64(s, lane);
+    if (lane == 63) ws[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < SC_T / 64; ++w) t += ws[w];
+        sums[blockIdx.x] = t;
+    }
+}
+
+// Exclusive scan of one tile with a carried-in block offset; in -> out (may alias).
+template <class T>
+__global__ void __launch_bounds__(SC_T) sc_scan(const T* in, T* out, uint64_t n,
+                                                const uint64_t* __restrict__ block_off) {
+    __shared__ uint64_t ws[SC_T / 64 + 1];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_I;
+    uint64_t v[SC_I];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_I; ++j) {
+        v[j] = base + j < n ? (uint64_t)in[base + j] : 0ull;
+        s += v[j];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl_scan64(s, lane);
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < SC_T / 64; ++w) { uint64_t x = ws[w]; ws[w] = t; t += x; }
+    }
+    __syncthreads();
+    uint64_t run = (block_off ? block_off[blockIdx.x] : 0ull) + ws[wave] + inc - s;
+#pragma unroll
+    for (int j = 0; j < SC_I; ++j) {
+        if (base + j < n) out[base + j] = (T)run;
+        run += v[j];
+    }
+}
+
+template <class T>
+uint64_t excl_scan_impl(hga_ctx* c, T* data, uint64_t n, DevBuf& scratch, size_t scratch_off) {
+    if (n == 0) return 0;
+    const uint64_t nb = (n + SC_TILE - 1) / SC_TILE;
+    // scratch layout: [sums(nb)] [recursive scratch...]
+    uint64_t* sums = reinterpret_cast<uint64_t*>(static_cast<char*>(scratch.p) + scratch_off);
+    uint64_t total = 0;
+    if (nb == 1) {
+        c->launch("scan", [&] {
+            hipLaunchKernelGGL(sc_scan<T>, dim3(1), dim3(SC_T), 0, c->stream, data, data, n,
+                               (const uint64_t*)nullptr);
+        });
+        c->check_launch("sc_scan");
+        // total = last exclusive + last input is lost in place; recompute via reduce
+    } else {
+        c->launch("scan", [&] {
+            hipLaunchKernelGGL(sc_reduce<T>, dim3((unsigned)nb), dim3(SC_T), 0, c->stream, data,
+                               n, sums);
+        });
+        c->check_launch("sc_reduce");
+        excl_scan_impl<uint64_t>(c, sums, nb, scratch, scratch_off + ((nb * 8 + 255) & ~255ull));
+        c->launch("scan", [&] {
+            hipLaunchKernelGGL(sc_scan<T>, dim3((unsigned)nb), dim3(SC_T), 0, c->stream, data,
+                               data, n, (const uint64_t*)sums);
+        });
+        c->check_launch("sc_scan");
+    }
+    (void)total;
+    return 0;
+}
+
+size_t scan_scratch_bytes(uint64_t n) {
+    size_t b = 0;
+    while (n > (uint64_t)SC_TILE) {
+        n = (n + SC_TILE - 1) / SC_TILE;
+        b += ((n * 8 + 255) & ~255ull);
+    }
+    return b + 256;
+}
+
+template <class K>
+void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, DevBuf& scratch) {
+    if (n <= 1 || bits <= 0) return;
+    HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "radix sort: n >= 2^32");
+    const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    const uint64_t n_cnt = (uint64_t)256 * n_tiles;
+    const size_t kb = ((n * sizeof(K) + 255) & ~255ull);
+    const size_t vb = vals ? ((n * 4 + 255) & ~255ull) : 0;
+    const size_t cb = ((n_cnt * 4 + 255) & ~255ull);
+    const size_t sb = scan_scratch_bytes(n_cnt);
+    char* base = static_cast<char*>(scratch.ensure(kb + vb + cb + sb));
+    K* k2 = reinterpret_cast<K*>(base);
+    uint32_t* v2 = vals ? reinterpret_cast<uint32_t*>(base + kb) : nullptr;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kb + vb);
+    K* ka = keys;
+    K* kbuf = k2;
+    uint32_t* va = vals;
+    uint32_t* vbuf = v2;
+    int passes = 0;
+    for (int shift = 0; shift < bits; shift += 8, ++passes) {
+        c->launch("radix_upsweep", [&] {
+            hipLaunchKernelGGL(rs_upsweep<K>, dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n,
+                               shift, cnt, n_tiles);
+        });
+        c->check_launch("rs_upsweep");
+        excl_scan_impl<uint32_t>(c, cnt, n_cnt, scratch, kb + vb + cb);
+        if (vals) {
+            c->launch("radix_downsweep", [&] {
+                hipLaunchKernelGGL((rs_downsweep<K, true>), dim3(n_tiles), dim3(RS_T), 0, c->stream,
+                                   ka, va, kbuf, vbuf, n, shift, cnt, n_tiles);
+            });
+        } else {
+            c->launch("radix_downsweep", [&] {
+                hipLaunchKernelGGL((rs_downsweep<K, false>), dim3(n_tiles), dim3(RS_T), 0,
+                                   c->stream, ka, (const uint32_t*)nullptr, kbuf,
+                                   (uint32_t*)nullptr, n, shift, cnt, n_tiles);
+            });
+        }
+        c->check_launch("rs_downsweep");
+        std::swap(ka, kbuf);
+        std::swap(va, vbuf);
+    }
+    if (passes & 1) {
+        HGA_HIP(hipMemcpyAsync(keys, ka, n * sizeof(K), hipMemcpyDeviceToDevice, c->stream));
+        if (vals) HGA_HIP(hipMemcpyAsync(vals, va, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+}
+
+}  // namespace
+
+void radix_sort_u64(hga_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n, int bits,
+                    DevBuf& scratch) {
+    radix_sort_impl<uint64_t>(c, keys, vals, n, bits, scratch);
+}
+void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int bits,
+                    DevBuf& scratch) {
+    radix_sort_impl<uint32_t>(c, keys, vals, n, bits > 32 ? 32 : bits, scratch);
+}
+void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch) {
+    scratch.ensure(scan_scratch_bytes(n));
+    excl_scan_impl<uint64_t>(c, data, n, scratch, 0);
+}
+
+}  // namespace hga

@@ -1,0 +1,387 @@
+"""ctypes binding of the native libraries (test / bench plumbing, not the product).
+
+The product is the C ABI of ``include/hga.h`` (``lib/libhga.so``, HIP for gfx950) and the
+C++ CLIs in ``bin/``.  This module only marshals numpy buffers through that ABI and through
+``lib/libhga_host.so`` (host readers and seeded generators).  There is no fallback: if the
+HIP library is missing or a call fails, an ``HgaError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "lib")
+BIN_DIR = os.path.join(HERE, "bin")
+
+
+class HgaError(RuntimeError):
+    pass
+
+
+_u8p = C.POINTER(C.c_uint8)
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_vp = C.c_void_p
+
+
+class CountStats(C.Structure):
+    _fields_ = [("instances", C.c_uint64), ("distinct_rows", C.c_uint64), ("bytes", C.c_uint64),
+                ("buckets", C.c_uint32), ("max_split", C.c_uint32)]
+
+
+class LookupSizes(C.Structure):
+    _fields_ = [("n_reads", C.c_uint64), ("windows", C.c_uint64), ("hits", C.c_uint64),
+                ("firsts", C.c_uint64), ("reads_hit", C.c_uint64), ("n_sdk", C.c_uint32)]
+
+
+class LookupResult(C.Structure):
+    _fields_ = [("hit_ptr", _u64p), ("hit_kid", _u32p), ("hit_pos", _u32p), ("sorted_kid", _u32p),
+                ("first_ptr", _u64p), ("first_kid", _u32p), ("first_pos", _u32p),
+                ("kci_ptr", _u64p), ("kci_read", _u32p)]
+
+
+_lib = None
+_host = None
+
+# name -> (restype, argtypes) for every symbol include/hga.h declares
+HGA_SYMBOLS = {
+    "hga_last_error": (C.c_char_p, []),
+    "hga_free": (None, [_vp]),
+    "hga_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "hga_version": (C.c_char_p, []),
+    "hga_ctx_create": (C.c_int, [C.POINTER(_vp), C.c_int]),
+    "hga_ctx_destroy": (C.c_int, [_vp]),
+    "hga_count_begin": (C.c_int, [_vp, C.c_int, C.c_uint32]),
+    "hga_count_add": (C.c_int, [_vp, C.c_uint32, C.c_char_p, C.c_uint64]),
+    "hga_count_run": (C.c_int, [_vp, C.c_uint32]),
+    "hga_count_get_stats": (C.c_int, [_vp, C.POINTER(CountStats)]),
+    "hga_count_spec_hist": (C.c_int, [_vp, C.POINTER(C.c_double), C.c_uint32, C.POINTER(_i64p), _u64p]),
+    "hga_count_select": (C.c_int, [_vp, C.c_int64, C.c_int64, C.POINTER(_u64p), _u64p, _u64p]),
+    "hga_count_select_ex": (C.c_int, [_vp, C.c_int64, C.c_int64, C.POINTER(_u64p), C.POINTER(_u8p), _u64p,
+                                      _u64p]),
+    "hga_count_select_device": (C.c_int, [_vp, C.c_int64, C.c_int64, _u64p, _u64p]),
+    "hga_count_rows": (C.c_int, [_vp, C.POINTER(_u64p), C.POINTER(_u32p), _u64p]),
+    "hga_count_dump": (C.c_int, [_vp, C.c_uint32, C.POINTER(_u64p), C.POINTER(_u32p), _u64p]),
+    "hga_lookup_load": (C.c_int, [_vp, C.c_int, _u64p, C.c_uint32]),
+    "hga_lookup_set_reads": (C.c_int, [_vp, C.c_char_p, _u64p, C.c_uint64, C.c_uint32]),
+    "hga_lookup_run": (C.c_int, [_vp]),
+    "hga_lookup_get_sizes": (C.c_int, [_vp, C.POINTER(LookupSizes)]),
+    "hga_lookup_fetch": (C.c_int, [_vp, C.POINTER(LookupResult)]),
+    "hga_profile_enable": (C.c_int, [_vp, C.c_int]),
+    "hga_profile_reset": (C.c_int, [_vp]),
+    "hga_profile_get": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_double), _u64p]),
+    "hga_sync": (C.c_int, [_vp]),
+}
+
+HOST_SYMBOLS = {
+    "hgh_last_error": (C.c_char_p, []),
+    "hgh_free": (None, [_vp]),
+    "hgh_gen_genome": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(_vp)]),
+    "hgh_gen_haplotype": (C.c_int, [C.c_char_p, C.c_uint64, C.c_double, C.c_uint64, C.c_uint64,
+                                    C.POINTER(_vp), _u64p]),
+    "hgh_gen_art": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.POINTER(_vp), _u64p,
+                              C.POINTER(_vp), C.POINTER(_u64p), _u64p]),
+    "hgh_gen_nanosim": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(_vp), _u64p,
+                                  C.POINTER(_vp), C.POINTER(_u64p), _u64p]),
+    "hgh_write_art_fastq": (C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int, C.c_uint64,
+                                      C.c_char_p]),
+    "hgh_write_nanosim_fasta": (C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_uint64,
+                                          C.c_char_p]),
+    "hgh_load_records": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.POINTER(_vp), C.POINTER(_u64p),
+                                   C.POINTER(_i32p), C.POINTER(_u32p), C.POINTER(_u32p), _u64p,
+                                   C.POINTER(_u64p), C.POINTER(_vp)]),
+    "hgh_jf_stream": (C.c_int, [C.c_char_p, C.POINTER(_vp), _u64p, _u64p]),
+    "hgh_fmt_double": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
+}
+
+
+def _bind(lib, table):
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """The HIP library (lib/libhga.so).  Raises if it was not built."""
+    global _lib
+    if _lib is None:
+        path = os.path.join(LIB_DIR, "libhga.so")
+        if not os.path.exists(path):
+            raise HgaError(f"{path} missing: build it with `make -C hybrid-genome-assembler_amd`")
+        _lib = C.CDLL(path)
+        _bind(_lib, HGA_SYMBOLS)
+    return _lib
+
+
+def host():
+    global _host
+    if _host is None:
+        path = os.path.join(LIB_DIR, "libhga_host.so")
+        if not os.path.exists(path):
+            raise HgaError(f"{path} missing: build it with `make -C hybrid-genome-assembler_amd`")
+        _host = C.CDLL(path)
+        _bind(_host, HOST_SYMBOLS)
+    return _host
+
+
+def _ck(status):
+    if status != 0:
+        raise HgaError(f"hga status {status}: {lib().hga_last_error().decode()}")
+
+
+def _hck(status):
+    if status != 0:
+        raise HgaError(f"host: {host().hgh_last_error().decode()}")
+
+
+def _take(ptr, n, dtype, free):
+    """Copy n items of dtype from a library-allocated pointer into numpy, then free it."""
+    try:
+        if n == 0:
+            return np.zeros(0, dtype=dtype)
+        addr = ptr if isinstance(ptr, int) else C.cast(ptr, C.c_void_p).value
+        buf = (C.c_char * (n * np.dtype(dtype).itemsize)).from_address(addr)
+        return np.frombuffer(buf, dtype=dtype).copy()
+    finally:
+        free(ptr)
+
+
+def _p(arr, ct):
+    return arr.ctypes.data_as(C.POINTER(ct))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _ck(lib().hga_device_count(C.byref(n)))
+    return n.value
+
+
+class Ctx:
+    """One hga_ctx (one HIP stream on one device)."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        _ck(lib().hga_ctx_create(C.byref(self._h), device))
+        self.n_files = 0
+
+    def close(self):
+        if self._h:
+            lib().hga_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- counting
+    def count_begin(self, k: int, n_files: int):
+        _ck(lib().hga_count_begin(self._h, k, n_files))
+        self.n_files = n_files
+
+    def count_add(self, file: int, seq: bytes):
+        _ck(lib().hga_count_add(self._h, file, seq, len(seq)))
+
+    def count_run(self, min_per_file: int = 2):
+        _ck(lib().hga_count_run(self._h, min_per_file))
+
+    def count_stats(self) -> CountStats:
+        s = CountStats()
+        _ck(lib().hga_count_get_stats(self._h, C.byref(s)))
+        return s
+
+    def spec_hist(self, thresholds):
+        thr = np.ascontiguousarray(thresholds, dtype=np.float64)
+        p = _i64p()
+        n = C.c_uint64()
+        _ck(lib().hga_count_spec_hist(self._h, _p(thr, C.c_double), len(thr), C.byref(p), C.byref(n)))
+        return _take(p, 3 * n.value, np.int64, lib().hga_free).reshape(-1, 3)
+
+    def select(self, lower: int, upper: int):
+        k = _u64p()
+        f = _u8p()
+        n = C.c_uint64()
+        d = C.c_uint64()
+        _ck(lib().hga_count_select_ex(self._h, lower, upper, C.byref(k), C.byref(f), C.byref(n), C.byref(d)))
+        keys = _take(k, n.value, np.uint64, lib().hga_free)
+        flags = _take(f, n.value, np.uint8, lib().hga_free)
+        return keys, flags, d.value
+
+    def select_device(self, lower: int, upper: int):
+        n = C.c_uint64()
+        d = C.c_uint64()
+        _ck(lib().hga_count_select_device(self._h, lower, upper, C.byref(n), C.byref(d)))
+        return n.value, d.value
+
+    def rows(self):
+        k = _u64p()
+        c = _u32p()
+        n = C.c_uint64()
+        _ck(lib().hga_count_rows(self._h, C.byref(k), C.byref(c), C.byref(n)))
+        keys = _take(k, n.value, np.uint64, lib().hga_free)
+        cnts = _take(c, n.value * self.n_files, np.uint32, lib().hga_free).reshape(-1, self.n_files)
+        return keys, cnts
+
+    def dump(self, file: int):
+        k = _u64p()
+        c = _u32p()
+        n = C.c_uint64()
+        _ck(lib().hga_count_dump(self._h, file, C.byref(k), C.byref(c), C.byref(n)))
+        return _take(k, n.value, np.uint64, lib().hga_free), _take(c, n.value, np.uint32, lib().hga_free)
+
+    # ---- lookup
+    def lookup_load(self, k: int, keys_in_id_order):
+        keys = np.ascontiguousarray(keys_in_id_order, dtype=np.uint64)
+        _ck(lib().hga_lookup_load(self._h, k, _p(keys, C.c_uint64), len(keys)))
+
+    def lookup_set_reads(self, bases: bytes, offsets, first_read_id: int = 1):
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        _ck(lib().hga_lookup_set_reads(self._h, bases, _p(off, C.c_uint64), len(off) - 1, first_read_id))
+
+    def lookup_run(self):
+        _ck(lib().hga_lookup_run(self._h))
+
+    def lookup_sizes(self) -> LookupSizes:
+        s = LookupSizes()
+        _ck(lib().hga_lookup_get_sizes(self._h, C.byref(s)))
+        return s
+
+    def lookup_fetch(self) -> dict:
+        s = self.lookup_sizes()
+        n, H, U, K = s.n_reads, s.hits, s.firsts, s.n_sdk
+        out = {
+            "hit_ptr": np.zeros(n + 1, np.uint64), "hit_kid": np.zeros(H, np.uint32),
+            "hit_pos": np.zeros(H, np.uint32), "sorted_kid": np.zeros(H, np.uint32),
+            "first_ptr": np.zeros(n + 1, np.uint64), "first_kid": np.zeros(U, np.uint32),
+            "first_pos": np.zeros(U, np.uint32), "kci_ptr": np.zeros(K + 1, np.uint64),
+            "kci_read": np.zeros(H, np.uint32),
+        }
+        r = LookupResult()
+        for name, arr in out.items():
+            setattr(r, name, _p(arr, C.c_uint64 if arr.dtype == np.uint64 else C.c_uint32))
+        _ck(lib().hga_lookup_fetch(self._h, C.byref(r)))
+        return out
+
+    # ---- measurement
+    def profile(self, on: bool = True):
+        _ck(lib().hga_profile_enable(self._h, 1 if on else 0))
+
+    def profile_reset(self):
+        _ck(lib().hga_profile_reset(self._h))
+
+    def profile_get(self, name: str):
+        ms = C.c_double()
+        n = C.c_uint64()
+        _ck(lib().hga_profile_get(self._h, name.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def sync(self):
+        _ck(lib().hga_sync(self._h))
+
+
+# ---------------------------------------------------------------- host helpers
+def gen_genome(length: int, seed: int) -> bytes:
+    p = C.c_void_p()
+    _hck(host().hgh_gen_genome(length, seed, C.byref(p)))
+    return bytes(_take(p.value, length, np.uint8, host().hgh_free))
+
+
+def gen_haplotype(src: bytes, d: float, extra: int, seed: int) -> bytes:
+    p = C.c_void_p()
+    n = C.c_uint64()
+    _hck(host().hgh_gen_haplotype(src, len(src), d, extra, seed, C.byref(p), C.byref(n)))
+    return bytes(_take(p.value, n.value, np.uint8, host().hgh_free))
+
+
+@dataclass
+class Reads:
+    seq: bytes               # '\n'-joined stream (counting input)
+    bases: bytes             # concatenated sequences (lookup input)
+    offsets: np.ndarray      # CSR, n+1
+
+    @property
+    def n(self):
+        return len(self.offsets) - 1
+
+
+def _reads_from(fn, *args) -> Reads:
+    sp, bp = C.c_void_p(), C.c_void_p()
+    sl = C.c_uint64()
+    op = _u64p()
+    nr = C.c_uint64()
+    _hck(fn(*args, C.byref(sp), C.byref(sl), C.byref(bp), C.byref(op), C.byref(nr)))
+    offsets = _take(op, nr.value + 1, np.uint64, host().hgh_free)
+    seq = bytes(_take(sp.value, sl.value, np.uint8, host().hgh_free))
+    bases = bytes(_take(bp.value, int(offsets[-1]), np.uint8, host().hgh_free)) if offsets[-1] else (
+        host().hgh_free(bp.value) or b"")
+    return Reads(seq, bases, offsets)
+
+
+def gen_art(genome: bytes, n_reads: int, read_len: int, seed: int) -> Reads:
+    return _reads_from(host().hgh_gen_art, genome, len(genome), n_reads, read_len, seed)
+
+
+def gen_nanosim(genome: bytes, n_reads: int, seed: int) -> Reads:
+    return _reads_from(host().hgh_gen_nanosim, genome, len(genome), n_reads, seed)
+
+
+def write_art_fastq(genome: bytes, name: str, n_reads: int, read_len: int, seed: int, path: str):
+    _hck(host().hgh_write_art_fastq(genome, len(genome), name.encode(), n_reads, read_len, seed, path.encode()))
+
+
+def write_nanosim_fasta(genome: bytes, name: str, n_reads: int, seed: int, path: str):
+    _hck(host().hgh_write_nanosim_fasta(genome, len(genome), name.encode(), n_reads, seed, path.encode()))
+
+
+def load_records(paths, annotate: bool):
+    arr = (C.c_char_p * len(paths))(*[p.encode() for p in paths])
+    bp = C.c_void_p()
+    op, sp, ep = _u64p(), _u32p(), _u32p()
+    cp = _i32p()
+    n = C.c_uint64()
+    mp = _u64p()
+    fp = C.c_void_p()
+    _hck(host().hgh_load_records(arr, len(paths), 1 if annotate else 0, C.byref(bp), C.byref(op), C.byref(cp),
+                                 C.byref(sp), C.byref(ep), C.byref(n), C.byref(mp), C.byref(fp)))
+    nr = n.value
+    offsets = _take(op, nr + 1, np.uint64, host().hgh_free)
+    bases = bytes(_take(bp.value, int(offsets[-1]), np.uint8, host().hgh_free))
+    meta = _take(mp, (len(paths) + 1) * 5, np.uint64, host().hgh_free).reshape(-1, 5)
+    fname = C.string_at(fp.value).decode()
+    host().hgh_free(fp.value)
+    return {
+        "bases": bases, "offsets": offsets,
+        "category": _take(cp, nr, np.int32, host().hgh_free),
+        "start": _take(sp, nr, np.uint32, host().hgh_free),
+        "end": _take(ep, nr, np.uint32, host().hgh_free),
+        "meta": meta, "filename": fname,
+    }
+
+
+def jf_stream(path: str) -> bytes:
+    p = C.c_void_p()
+    n = C.c_uint64()
+    r = C.c_uint64()
+    _hck(host().hgh_jf_stream(path.encode(), C.byref(p), C.byref(n), C.byref(r)))
+    return bytes(_take(p.value, n.value, np.uint8, host().hgh_free)) if n.value else (
+        host().hgh_free(p.value) or b"")
+
+
+def fmt_double(v: float) -> str:
+    buf = C.create_string_buffer(64)
+    n = host().hgh_fmt_double(v, buf, 64)
+    return buf.value.decode() if n >= 0 else ""

@@ -1,0 +1,157 @@
+// categorization — drop-in for the reference's `categorization` CLI
+// (src/read_clustering.cpp:35-84) up to and including index construction, whose
+// per-read SDK lookup (ReadClusteringEngine::construct_indices,
+// src/clustering/ReadClusteringEngine.cpp:234-299) runs on the MI355X through libhga.
+//
+// Kept from the reference: argv (positional reads, -k/--kmers <path>, -o/--output,
+// the clustering knobs, -s/--spectral, -d/--debug, -t/--threads), SDK loading with
+// KmerIDs in std::unordered_set iteration order (read_clustering.cpp:18-33,
+// ReadClusteringEngine.cpp:237-241), the SequenceRecordIterator metadata print,
+// the default output folder "./<f1>__<f2>_clusters/" (read_clustering.cpp:78), the
+// "Index construction took <ms>ms" timing line and, when every file is a category
+// (ReadClusteringEngine.cpp:229), "X out of Y kmers are discriminative" (:285-297).
+//
+// The stages after index construction (connections, union-find, tails, spectral
+// clustering, export; ReadClusteringEngine.cpp:301-826) are out of this build's
+// scope; with --index-out <path> the constructed index is written
+// as a binary file for a downstream consumer.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "args.h"
+#include "hga.h"
+#include "seqio.h"
+
+namespace {
+void check(hga_status s, const char* what) {
+    if (s != HGA_OK) throw std::runtime_error(std::string(what) + ": " + hga_last_error());
+}
+
+// load_text_file_kmers (src/read_clustering.cpp:18-33)
+std::pair<std::vector<uint64_t>, int> load_text_file_kmers(const std::string& path) {
+    std::ifstream in(path);
+    std::string line;
+    int k = 0;
+    std::unordered_set<uint64_t> s;
+    while (std::getline(in, line)) {
+        k = (int)line.length();
+        s.insert(hgah::line_canonical(line.data(), line.size()));
+    }
+    return {std::vector<uint64_t>(s.begin(), s.end()), k};   // KmerID = iteration order
+}
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    std::vector<std::string> read_paths;
+    std::string kmer_path, output_folder_path, index_out;
+    bool debug = false, force_spectral = false;
+    int threads = 1, sc_min = 30, sc_max = -1, dims = 16;
+    double sc_fraction = 0.15;
+    uint64_t sc_score = 0, tail = 40, enrich = 20;
+    hgah::ArgParser ap;
+    ap.add("help", 'h', true, "Help screen", nullptr);
+    ap.add("read_paths", 0, false, "Path to file with reads (FASTA or FASTQ)",
+           [&](const std::string& v) { read_paths.push_back(v); });
+    ap.add("kmers", 'k', false, "Path to text file with kmers", [&](const std::string& v) { kmer_path = v; });
+    ap.add("output", 'o', false, "Path to folder with exported clusters",
+           [&](const std::string& v) { output_folder_path = v; });
+    ap.add("sc_max_size", 0, false, "Maximum size for a scaffold component", [&](const std::string& v) { sc_max = std::stoi(v); });
+    ap.add("sc_min_size", 0, false, "Minimum size for a scaffold component", [&](const std::string& v) { sc_min = std::stoi(v); });
+    ap.add("sc_fraction", 0, false, "Minimum score for a scaffold component forming connection",
+           [&](const std::string& v) { sc_fraction = std::stod(v); });
+    ap.add("sc_score", 0, false, "Minimum score for a scaffold component forming connection",
+           [&](const std::string& v) { sc_score = std::stoull(v); });
+    ap.add("tail_amplification", 0, false, "Minimal score for tail amplifying connections",
+           [&](const std::string& v) { tail = std::stoull(v); });
+    ap.add("core_enrichment", 0, false, "Minimal score for connections enriching core components",
+           [&](const std::string& v) { enrich = std::stoull(v); });
+    ap.add("spectral_dims", 0, false, "Number of dimensions for spectral embedding",
+           [&](const std::string& v) { dims = std::stoi(v); });
+    ap.add("spectral", 's', true, "Forces the usage of spectral clustering on the entire dataset",
+           [&](const std::string&) { force_spectral = true; });
+    ap.add("debug", 'd', true, "Debug flag. Treat read files as separate haplotype reads.",
+           [&](const std::string&) { debug = true; });
+    ap.add("threads", 't', false, "Number of threads to use", [&](const std::string& v) { threads = std::stoi(v); });
+    ap.add("index-out", 0, false, "Write the constructed index (binary) to this path",
+           [&](const std::string& v) { index_out = v; });
+    ap.parse(argc, argv);
+    for (auto& p : ap.positional) read_paths.push_back(p);
+    (void)threads; (void)sc_min; (void)sc_max; (void)dims; (void)sc_fraction; (void)sc_score; (void)tail;
+    (void)enrich; (void)force_spectral;
+    if (ap.has("help")) {
+        std::cout << ap.describe();
+        return 0;
+    }
+    if (read_paths.empty()) throw std::invalid_argument("You need to specify paths to read files");
+    if (kmer_path.empty()) throw std::invalid_argument("You need to specify path to kmers");
+    auto kk = load_text_file_kmers(kmer_path);
+    const int k = kk.second;
+    if (k < 1 || k > 32) throw std::invalid_argument("Kmer size must be in [1, 32]");
+
+    hgah::RecordSet rs = hgah::load_records(read_paths, debug, !index_out.empty());
+    for (auto& m : rs.file_meta) std::cout << m.repr();
+    if (output_folder_path.empty()) output_folder_path = "./" + rs.meta.filename + "_clusters/";
+    const bool engine_debug = rs.file_meta.size() == rs.categories;   // ReadClusteringEngine.cpp:229
+
+    const char* dev_env = std::getenv("HGA_DEVICE");
+    hga_ctx* ctx = nullptr;
+    check(hga_ctx_create(&ctx, dev_env ? std::atoi(dev_env) : 0), "hga_ctx_create");
+    const auto t0 = std::chrono::steady_clock::now();
+    check(hga_lookup_load(ctx, k, kk.first.data(), (uint32_t)kk.first.size()), "hga_lookup_load");
+    check(hga_lookup_set_reads(ctx, rs.bases.data(), rs.offsets.data(), rs.size(), 1), "hga_lookup_set_reads");
+    check(hga_lookup_run(ctx), "hga_lookup_run");
+    hga_lookup_sizes sz;
+    check(hga_lookup_get_sizes(ctx, &sz), "hga_lookup_get_sizes");
+    std::vector<uint64_t> hit_ptr(sz.n_reads + 1), first_ptr(sz.n_reads + 1), kci_ptr((size_t)sz.n_sdk + 1);
+    std::vector<uint32_t> sorted_kid(sz.hits), first_kid(sz.firsts), first_pos(sz.firsts), kci_read(sz.hits);
+    hga_lookup_result res{};
+    res.hit_ptr = hit_ptr.data();
+    res.sorted_kid = sorted_kid.data();
+    res.first_ptr = first_ptr.data();
+    res.first_kid = first_kid.data();
+    res.first_pos = first_pos.data();
+    res.kci_ptr = kci_ptr.data();
+    res.kci_read = kci_read.data();
+    check(hga_lookup_fetch(ctx, &res), "hga_lookup_fetch");
+    const auto t1 = std::chrono::steady_clock::now();
+    std::cout << "Index construction took "
+              << std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count() << "ms\n";
+
+    if (engine_debug) {   // ReadClusteringEngine.cpp:285-297
+        uint32_t discriminative = 0, total = 0;
+        for (uint64_t id = 0; id < sz.n_sdk; ++id) {
+            std::set<int32_t> cats;
+            for (uint64_t j = kci_ptr[id]; j < kci_ptr[id + 1]; ++j) cats.insert(rs.category[kci_read[j] - 1]);
+            if (cats.size() == 1) ++discriminative;
+            if (!cats.empty()) ++total;
+        }
+        std::cout << discriminative << " out of " << total << " kmers are discriminative \n";
+    }
+    if (!index_out.empty()) {
+        std::FILE* f = std::fopen(index_out.c_str(), "wb");
+        if (!f) throw std::runtime_error("cannot write " + index_out);
+        const uint64_t hdr[5] = {sz.n_reads, sz.hits, sz.firsts, sz.n_sdk, (uint64_t)k};
+        std::fwrite(hdr, 8, 5, f);
+        std::fwrite(hit_ptr.data(), 8, hit_ptr.size(), f);
+        std::fwrite(sorted_kid.data(), 4, sorted_kid.size(), f);
+        std::fwrite(first_ptr.data(), 8, first_ptr.size(), f);
+        std::fwrite(first_kid.data(), 4, first_kid.size(), f);
+        std::fwrite(first_pos.data(), 4, first_pos.size(), f);
+        std::fwrite(kci_ptr.data(), 8, kci_ptr.size(), f);
+        std::fwrite(kci_read.data(), 4, kci_read.size(), f);
+        std::fclose(f);
+    }
+    std::cerr << "categorization: " << sz.reads_hit << " of " << sz.n_reads << " reads carry SDKs (" << sz.hits
+              << " hits); the clustering stages after index construction are not part of this build "
+                 "(output folder " << output_folder_path << " not written)\n";
+    hga_ctx_destroy(ctx);
+    return 0;
+}

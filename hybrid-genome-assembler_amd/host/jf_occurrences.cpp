@@ -1,0 +1,167 @@
+// jf_occurrences — drop-in for the reference's `jf_occurrences` CLI
+// (src/jellyfish_occurrences.cpp:14-59), with the jellyfish count + dump + sort
+// (src/occurrences/run_jellyfish.sh) and both string k-way merge passes of
+// JellyfishOccurrenceReader (src/occurrences/JellyfishOccurrenceReader.cpp:63-135)
+// replaced by the MI355X pipeline of libhga (include/hga.h).
+//
+// Kept from the reference: argv (positional read files, -k/--k-size, -o/--output,
+// -h/--help), the specificity thresholds {70,85,90,95,99,100,100.01} (:47), the
+// plot pipe to `python scripts/plotting.py --plot kmer_histogram_with_spec` with the
+// Python-literal wire format (src/common/Plotting.cpp:20-37) and its "0" echo, the
+// stdin prompt (:54-55), the default export name "{k}-mers_{lower}_{upper}_{p*100}%.txt"
+// (:57), one k-mer per line in ascending order, and the final
+// "{d} out of {e} exported kmers are discriminative" line without newline (:133).
+//
+// HGA_DEVICE selects the GPU (default 0); HGA_PLOT_CMD overrides the plot command.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <map>
+#include <random>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "args.h"
+#include "hga.h"
+#include "seqio.h"
+
+namespace {
+
+void check(hga_status s, const char* what) {
+    if (s != HGA_OK) throw std::runtime_error(std::string(what) + ": " + hga_last_error());
+}
+
+// run_command_with_input (src/common/Utils.cpp:24-45): popen(cmd, "w"), write, pclose.
+int run_command_with_input(const std::string& cmd, const std::string& in) {
+    std::FILE* p = popen(cmd.c_str(), "w");
+    if (!p) {
+        std::fprintf(stderr, "incorrect parameters or too many files.\n");
+        return EXIT_FAILURE;
+    }
+    std::fprintf(p, "%s", in.c_str());
+    if (std::ferror(p)) {
+        std::fprintf(stderr, "Output to stream failed.\n");
+        std::exit(EXIT_FAILURE);
+    }
+    if (pclose(p) != 0) std::fprintf(stderr, "Could not run more or other error.\n");
+    return EXIT_SUCCESS;
+}
+
+using KmerSpecificity = std::map<double, std::map<int, int>>;
+
+// plot_kmer_specificity (src/common/Plotting.cpp:20-37)
+std::string plot_wire(const std::map<int, KmerSpecificity>& specs, int max_coverage) {
+    std::string ks;
+    bool first_k = true;
+    for (const auto& k_specs : specs) {
+        std::string bounds;
+        bool first_b = true;
+        for (const auto& bound : k_specs.second) {
+            std::string counts;
+            bool first_c = true;
+            for (const auto& cc : bound.second) {
+                if (cc.second < 50) continue;
+                counts += (first_c ? "" : ", ") + std::string("(") + std::to_string(cc.first) + ", " +
+                          std::to_string(cc.second) + ")";
+                first_c = false;
+            }
+            bounds += (first_b ? "" : ", ") + std::string("(") + hgah::fmt_double(bound.first) + ", [" + counts + "])";
+            first_b = false;
+        }
+        ks += (first_k ? "" : "\n") + std::string("(") + std::to_string(k_specs.first) + ", [" + bounds + "])";
+        first_k = false;
+    }
+    return std::to_string(specs.size()) + " " + std::to_string(max_coverage) + "\n" + ks;
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    std::vector<std::string> read_paths;
+    std::string output_path;
+    int k = 11;
+    hgah::ArgParser ap;
+    ap.add("help", 'h', true, "Help screen", nullptr);
+    ap.add("read_paths", 0, false, "Path to file with reads (FASTA or FASTQ)",
+           [&](const std::string& v) { read_paths.push_back(v); });
+    ap.add("k-size", 'k', false, "Size of kmer to analyze & select", [&](const std::string& v) { k = std::stoi(v); });
+    ap.add("output", 'o', false, "Output path for the counting bloom filter",
+           [&](const std::string& v) { output_path = v; });
+    ap.parse(argc, argv);
+    for (auto& p : ap.positional) read_paths.push_back(p);
+    if (ap.has("help")) {
+        std::cout << ap.describe();
+        return 0;
+    }
+    if (read_paths.empty()) throw std::invalid_argument("You need to specify paths to read files");
+    if (!ap.has("k-size"))
+        throw std::invalid_argument(
+            "automatic k selection (HyperLogLog, src/occurrences/KmerAnalysis.cpp) is not part of this build; pass -k");
+
+    const char* dev_env = std::getenv("HGA_DEVICE");
+    hga_ctx* ctx = nullptr;
+    check(hga_ctx_create(&ctx, dev_env ? std::atoi(dev_env) : 0), "hga_ctx_create");
+    check(hga_count_begin(ctx, k, (uint32_t)read_paths.size()), "hga_count_begin");
+    for (uint32_t f = 0; f < read_paths.size(); ++f) {
+        const std::string s = hgah::jf_stream(read_paths[f]);
+        check(hga_count_add(ctx, f, s.data(), s.size()), "hga_count_add");
+    }
+    check(hga_count_run(ctx, 2), "hga_count_run");   // jellyfish --bc: per-file singletons dropped
+
+    const std::set<double> thresholds = {70, 85, 90, 95, 99, 100, 100.01};
+    const std::vector<double> thr(thresholds.begin(), thresholds.end());
+    int64_t* tri = nullptr;
+    uint64_t n_tri = 0;
+    check(hga_count_spec_hist(ctx, thr.data(), (uint32_t)thr.size(), &tri, &n_tri), "hga_count_spec_hist");
+    KmerSpecificity spec;
+    for (double t : thr) spec.insert({t, {}});
+    for (uint64_t i = 0; i < n_tri; ++i)
+        spec[thr[(size_t)tri[3 * i]]][(int)tri[3 * i + 1]] += (int)tri[3 * i + 2];
+    hga_free(tri);
+    std::map<int, KmerSpecificity> spec_map = {{k, spec}};
+    const char* plot_env = std::getenv("HGA_PLOT_CMD");
+    const std::string plot_cmd = plot_env ? plot_env : "python scripts/plotting.py --plot kmer_histogram_with_spec";
+    std::cout << run_command_with_input(plot_cmd, plot_wire(spec_map, 200)) << std::endl;
+
+    int lower = 0, upper = 0;
+    double percent = 0;
+    std::cout << "Enter lower and upper bounds for exported kmers as well as percentage\n";
+    std::cin >> lower >> upper >> percent;
+    if (output_path.empty())
+        output_path = std::to_string(k) + "-mers_" + std::to_string(lower) + "_" + std::to_string(upper) + "_" +
+                      hgah::fmt_double(percent * 100) + "%.txt";
+
+    // export_kmers (JellyfishOccurrenceReader.cpp:110-135)
+    uint64_t* keys = nullptr;
+    uint8_t* disc = nullptr;
+    uint64_t n = 0, n_disc_all = 0;
+    check(hga_count_select_ex(ctx, lower, upper, &keys, &disc, &n, &n_disc_all), "hga_count_select_ex");
+    std::random_device dev;
+    std::mt19937 rng(dev());
+    std::uniform_real_distribution<> dis(0.0, 1.0);
+    std::FILE* out = std::fopen(output_path.c_str(), "wb");
+    if (!out) throw std::runtime_error("cannot open " + output_path);
+    std::vector<char> buf;
+    buf.reserve(1 << 20);
+    uint32_t exported = 0, discriminative = 0;
+    std::vector<char> line((size_t)k + 1, '\n');
+    for (uint64_t i = 0; i < n; ++i) {
+        if (!(dis(rng) < percent)) continue;
+        hgah::kmer_to_chars(keys[i], k, line.data());
+        buf.insert(buf.end(), line.begin(), line.end());
+        if (buf.size() > (1u << 20)) { std::fwrite(buf.data(), 1, buf.size(), out); buf.clear(); }
+        ++exported;
+        discriminative += disc[i] ? 1u : 0u;
+    }
+    std::fwrite(buf.data(), 1, buf.size(), out);
+    std::fclose(out);
+    hga_free(keys);
+    hga_free(disc);
+    std::cout << discriminative << " out of " << exported << " exported kmers are discriminative";
+    std::cout.flush();
+    hga_ctx_destroy(ctx);
+    return 0;
+}

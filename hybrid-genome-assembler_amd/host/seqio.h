@@ -1,0 +1,62 @@
+// seqio.h — host-side sequence input for the two drop-in CLIs.
+//
+//  * RecordSet / load_records: SequenceRecordIterator semantics
+//    (src/common/SequenceRecordIterator.cpp:16-205) for `categorization`: one line
+//    stream across all files (std::getline, no CR stripping), FASTQ = 4 lines,
+//    FASTA = exactly 2 lines, format sniffed per file, ReadIDs 1-based and
+//    continuing across files, category = file index when annotating, simulator
+//    header regexes, the metadata pass.
+//  * jf_stream: the sequence stream jellyfish reads for the counting path
+//    (run_jellyfish.sh:3-4): multi-line FASTA/FASTQ records, sequences joined by
+//    '\n' (a non-base byte, so no k-mer window spans two reads).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace hgah {
+
+struct FileMeta {               // MetaData / ReadFileMetaData, SequenceRecordIterator.h:52-68
+    std::string filename;
+    uint64_t records = 0;
+    uint64_t min_read_length = UINT64_MAX;
+    uint64_t max_read_length = 0;
+    uint64_t avg_read_length = 0;
+    uint64_t total_bases = 0;
+    int file_type = 2;          // 0 FASTA, 1 FASTQ, 2 UNKNOWN
+    std::string repr() const;   // MetaData::repr, SequenceRecordIterator.h:60-63
+};
+
+struct RecordSet {
+    // CSR of sequences in reader order; read i has ReadID i + 1.
+    std::vector<char> bases;
+    std::vector<uint64_t> offsets{0};
+    std::vector<int32_t> category;      // GenomeReadData::category_id
+    std::vector<uint32_t> start, end;   // simulator-header coordinates (0 when unknown)
+    std::vector<std::string> headers;   // without the leading '@' / '>'
+    std::vector<std::string> qualities; // empty for FASTA
+    std::vector<FileMeta> file_meta;
+    FileMeta meta;                      // all files ("__"-joined names)
+    uint32_t categories = 1;
+    uint64_t size() const { return offsets.size() - 1; }
+};
+
+// Throws std::invalid_argument / std::logic_error with the reference's messages.
+// keep_text=false skips headers/qualities (the lookup needs sequences only).
+RecordSet load_records(const std::vector<std::string>& paths, bool annotate, bool keep_text = true);
+
+// Whole-file read of the sequences jellyfish would count, '\n'-separated.
+std::string jf_stream(const std::string& path, uint64_t* n_records = nullptr);
+
+// fmt "{}" formatting of a double (shortest round trip, fmt's fixed/exponent switch).
+std::string fmt_double(double v);
+
+// KmerIterator::number_to_sequence (src/common/KmerIterator.cpp:44-52).
+std::string kmer_to_string(uint64_t code, int k);
+void kmer_to_chars(uint64_t code, int k, char* out);
+
+// KmerIterator canonical code of a whole line (load_text_file_kmers, read_clustering.cpp:18-33).
+uint64_t line_canonical(const char* s, size_t len);
+
+}  // namespace hgah

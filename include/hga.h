@@ -1,0 +1,180 @@
+/* hga.h — C ABI of the MI355X k-mer hot path (libhga.so).
+ *
+ * The reference has no FFI; its seams are a process boundary and an in-process C++
+ * API.  Every entry point below names the reference interface it replaces
+ * (paths relative to the reference tree).  Plain pointers and sizes only; no
+ * exception crosses the ABI; every call returns an hga_status and
+ * hga_last_error() returns a thread-local message for the last failure.
+ *
+ * Threading: one hga_ctx owns one HIP stream on one device.  A ctx is not
+ * thread-safe; several ctx per device are allowed.  Host buffers passed in are
+ * caller-owned and may be freed as soon as the call returns.  Buffers the library
+ * allocates for the caller are released with hga_free().
+ */
+#ifndef HGA_H
+#define HGA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hga_ctx hga_ctx;
+
+typedef enum hga_status {
+    HGA_OK = 0,
+    HGA_ERR_INVALID = 1, /* bad argument (k out of range, unknown file index, ...)  */
+    HGA_ERR_HIP = 2,     /* a HIP runtime call failed                                */
+    HGA_ERR_OOM = 3,     /* device or host allocation failed                         */
+    HGA_ERR_STATE = 4,   /* call out of order (e.g. select before count_run)         */
+    HGA_ERR_COMM = 5     /* RCCL failure                                             */
+} hga_status;
+
+/* Thread-local text of the last error ("" if none). */
+const char* hga_last_error(void);
+/* Frees any buffer the library returned through an out-pointer. */
+void hga_free(void* p);
+/* Number of visible HIP devices. */
+hga_status hga_device_count(int* n);
+/* Library/kernel build identification string (static). */
+const char* hga_version(void);
+
+hga_status hga_ctx_create(hga_ctx** out, int device);
+hga_status hga_ctx_destroy(hga_ctx* ctx);
+
+/* ------------------------------------------------------------------------------
+ * Counting — replaces reference seam #1 (the per-file
+ *   popen("./occurrences/run_jellyfish.sh <reads> <k> <sorted>")  of
+ *   src/occurrences/JellyfishOccurrenceReader.cpp:19-24, i.e. `jellyfish bc/count -C
+ *   --bc`, `dump -c` and `LC_ALL=C sort`, src/occurrences/run_jellyfish.sh:3-6)
+ * and both k-way merge passes of seam #2 (JellyfishOccurrenceReader::get_next_kmer,
+ *   get_specificity, export_kmers; src/occurrences/JellyfishOccurrenceReader.cpp:63-135).
+ * ------------------------------------------------------------------------------ */
+
+/* Starts a counting session: k in [1,32], n_files >= 1 (one file = one haplotype,
+ * README.md:36).  Replaces JellyfishOccurrenceReader(paths, k)
+ * (src/occurrences/JellyfishOccurrenceReader.h:32). */
+hga_status hga_count_begin(hga_ctx* ctx, int k, uint32_t n_files);
+
+/* Appends sequence bytes of file `file` (copied to HBM).  `seq` holds whole reads
+ * separated by any byte that is not A/C/G/T (either case), e.g. '\n'; windows
+ * containing such a byte are not counted (jellyfish semantics).  May be called
+ * several times per file; a read must not straddle two calls. */
+hga_status hga_count_add(hga_ctx* ctx, uint32_t file, const char* seq, uint64_t n_bytes);
+
+/* Runs the device pipeline on everything added: canonical k-mers, per-file exact
+ * counts, per-file drop of k-mers whose count is < min_per_file (2 = jellyfish
+ * `--bc`), merge across files.  May be re-run (bench). */
+hga_status hga_count_run(hga_ctx* ctx, uint32_t min_per_file);
+
+typedef struct hga_count_stats {
+    uint64_t instances;      /* k-mer windows counted (all files)                  */
+    uint64_t distinct_rows;  /* merged rows present after the per-file drop       */
+    uint64_t bytes;          /* sequence bytes resident on the device              */
+    uint32_t buckets;        /* hash buckets used by the binning pass              */
+    uint32_t max_split;      /* largest sub-pass split any bucket needed           */
+} hga_count_stats;
+hga_status hga_count_get_stats(hga_ctx* ctx, hga_count_stats* out);
+
+/* Specificity histogram — JellyfishOccurrenceReader::get_specificity
+ * (src/occurrences/JellyfishOccurrenceReader.cpp:88-108): for every merged row,
+ * spec = first threshold > ((double)max_f c_f / (double)Σ c_f) * 100 and
+ * result[spec][Σc] += 1.  thr must be ascending; every row must fall below the last
+ * threshold.  Output: *triples = malloc'ed int64 [3 * *n]: (threshold index, total,
+ * unique k-mer count), ordered by threshold then total (std::map order);
+ * thresholds with no rows produce no triple. */
+hga_status hga_count_spec_hist(hga_ctx* ctx, const double* thr, uint32_t n_thr,
+                               int64_t** triples, uint64_t* n);
+
+/* Export selection — JellyfishOccurrenceReader::export_kmers
+ * (src/occurrences/JellyfishOccurrenceReader.cpp:110-135) with percent >= 1: the
+ * canonical codes of all merged rows with lower <= Σc <= upper, ascending
+ * (== the reference's LC_ALL=C string order for fixed k), and the number of them
+ * present in exactly one file (:128-130).  *keys malloc'ed (hga_free).
+ * Sampling for percent < 1 is host work on this output (see host/jf_occurrences). */
+hga_status hga_count_select(hga_ctx* ctx, int64_t lower, int64_t upper, uint64_t** keys,
+                            uint64_t* n, uint64_t* n_discriminative);
+/* Same, plus one byte per key: 1 if that k-mer is present in exactly one file.  The
+ * host needs the flags when it samples with percent < 1 (:128-130).  *keys and
+ * *discriminative are malloc'ed (hga_free). */
+hga_status hga_count_select_ex(hga_ctx* ctx, int64_t lower, int64_t upper, uint64_t** keys,
+                               uint8_t** discriminative, uint64_t* n, uint64_t* n_discriminative);
+/* Same, leaving the sorted keys on the device (bench / chained use). */
+hga_status hga_count_select_device(hga_ctx* ctx, int64_t lower, int64_t upper,
+                                   uint64_t* n, uint64_t* n_discriminative);
+
+/* All merged rows, ascending by code: keys[rows], counts[rows * n_files] row-major.
+ * This is the stream JellyfishOccurrenceReader::get_next_kmer yields. */
+hga_status hga_count_rows(hga_ctx* ctx, uint64_t** keys, uint32_t** counts, uint64_t* rows);
+
+/* One file's dump: rows with count >= min_per_file in that file, ascending — the
+ * content of "<reads>_<k>-mers_sorted" (run_jellyfish.sh:5-6). */
+hga_status hga_count_dump(hga_ctx* ctx, uint32_t file, uint64_t** keys, uint32_t** counts,
+                          uint64_t* rows);
+
+/* ------------------------------------------------------------------------------
+ * SDK lookup — replaces the per-read loop of ReadClusteringEngine::construct_indices
+ * (src/clustering/ReadClusteringEngine.cpp:234-299).  The host keeps SDK loading
+ * (src/read_clustering.cpp:18-33) and the KmerID assignment (iteration order of the
+ * std::unordered_set, ReadClusteringEngine.cpp:237-241).
+ * ------------------------------------------------------------------------------ */
+
+/* Uploads the SDK set: keys_in_id_order[i] is the canonical code of KmerID i. */
+hga_status hga_lookup_load(hga_ctx* ctx, int k, const uint64_t* keys_in_id_order, uint32_t n);
+
+/* Uploads reads in reader order as a CSR: read i = bases[offsets[i], offsets[i+1]).
+ * Read i has ReadID first_read_id + i (SequenceRecordIterator IDs are consecutive,
+ * 1-based, src/common/SequenceRecordIterator.cpp:27,168). */
+hga_status hga_lookup_set_reads(hga_ctx* ctx, const char* bases, const uint64_t* offsets,
+                                uint64_t n_reads, uint32_t first_read_id);
+
+/* Runs the lookup and builds every index on the device. */
+hga_status hga_lookup_run(hga_ctx* ctx);
+
+typedef struct hga_lookup_sizes {
+    uint64_t n_reads;
+    uint64_t windows;   /* k-mer windows scanned                                       */
+    uint64_t hits;      /* H: windows whose canonical code is an SDK                   */
+    uint64_t firsts;    /* U: distinct (read, KmerID) pairs                            */
+    uint64_t reads_hit; /* reads with >= 1 hit (the ReadComponents created)            */
+    uint32_t n_sdk;     /* K                                                           */
+} hga_lookup_sizes;
+hga_status hga_lookup_get_sizes(hga_ctx* ctx, hga_lookup_sizes* out);
+
+/* Caller-allocated output arrays (any may be NULL to skip):
+ *  hit_ptr[n+1], hit_kid[H], hit_pos[H]: per read, hits in window order with the
+ *      end-exclusive position (KmerIterator::position_in_sequence);
+ *  sorted_kid[H]: per read, KmerIDs ascending with duplicates
+ *      (ReadComponent::discriminative_kmer_ids, ReadClusteringEngine.cpp:262-272);
+ *  first_ptr[n+1], first_kid[U], first_pos[U]: ReadMetaData::kmer_positions
+ *      (first occurrence wins, :267) listed by ascending KmerID;
+ *  kci_ptr[K+1], kci_read[H]: kmer_component_index, per KmerID the ReadIDs, one per
+ *      occurrence, ascending (:262-263, 282-284). */
+typedef struct hga_lookup_result {
+    uint64_t* hit_ptr;
+    uint32_t* hit_kid;
+    uint32_t* hit_pos;
+    uint32_t* sorted_kid;
+    uint64_t* first_ptr;
+    uint32_t* first_kid;
+    uint32_t* first_pos;
+    uint64_t* kci_ptr;
+    uint32_t* kci_read;
+} hga_lookup_result;
+hga_status hga_lookup_fetch(hga_ctx* ctx, const hga_lookup_result* out);
+
+/* ------------------------------------------------------------------------------
+ * Measurement: per-kernel device time, recorded with HIP events on the ctx stream.
+ * ------------------------------------------------------------------------------ */
+hga_status hga_profile_enable(hga_ctx* ctx, int on);
+hga_status hga_profile_reset(hga_ctx* ctx);
+/* Total milliseconds and launch count recorded for kernel `name` since the reset. */
+hga_status hga_profile_get(hga_ctx* ctx, const char* name, double* ms, uint64_t* launches);
+/* Blocks until the ctx stream is idle. */
+hga_status hga_sync(hga_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGA_H */

@@ -1,0 +1,446 @@
+// oracle/oracle.cpp — CPU restatement of the reference hot path.
+//
+// TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load this library, and only as the checker / the timed CPU
+// baseline.  The product (libhga.so, the CLIs) never links or calls it.
+//
+// PARITY STATUS: "parity unpinned" in the strict sense of the task rules.  The
+// reference has no tests, fixtures or golden vectors for this path,
+// and it cannot be compiled here without stand-ins: every translation unit on the
+// path includes Boost headers (common/KmerIterator.h:3 <boost/optional.hpp>,
+// occurrences/JellyfishOccurrenceReader.h:7 <boost/function.hpp>,
+// common/SequenceRecordIterator.h:9 <boost/regex.hpp>) and Boost is not installed.
+// The counting stage itself is the external `jellyfish` binary, which is absent.
+// Each function below cites the reference lines it restates; hand-derived
+// known-answer tests (tests/test_oracle_kat.py) check the restatement.
+//
+// Written as plain, obviously-correct code (std::unordered_map, std::map,
+// std::sort).  The multi-threaded *_mt variants exist for bench.py's cpu_baseline
+// and are checked against the plain ones in tests/test_oracle.py.
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+// src/common/KmerIterator.cpp:7-19.  BASE_TO_NUM / COMPLEMENT are
+// std::unordered_map<char,Kmer> read with operator[]: any byte that is not one of
+// the four upper-case bases default-inserts 0, so it contributes code 0 to BOTH the
+// forward and the reverse-complement register.
+inline uint64_t ref_fwd_code(char c) {
+    switch (c) {
+        case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3;
+        default: return 0;
+    }
+}
+inline uint64_t ref_rc_code(char c) {
+    switch (c) {
+        case 'A': return 3; case 'C': return 2; case 'G': return 1; case 'T': return 0;
+        default: return 0;
+    }
+}
+
+// Jellyfish counting semantics (src/occurrences/run_jellyfish.sh:3-6, `-C`):
+// bases are ACGT case-insensitively; any other byte ends the current k-mer run.
+inline int jf_code(unsigned char c) {
+    switch (c) {
+        case 'A': case 'a': return 0;
+        case 'C': case 'c': return 1;
+        case 'G': case 'g': return 2;
+        case 'T': case 't': return 3;
+        default: return -1;
+    }
+}
+
+inline uint64_t kmask(int k) { return k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1); }
+
+// Canonical k-mers of every window of every ACGT run of a byte stream, in order.
+template <class F>
+void for_each_jf_kmer(const char* s, uint64_t n, int k, F&& f) {
+    const uint64_t mask = kmask(k);
+    const int sh = 2 * (k - 1);
+    uint64_t fwd = 0, rc = 0;
+    int run = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        int c = jf_code((unsigned char)s[i]);
+        if (c < 0) { run = 0; fwd = rc = 0; continue; }
+        fwd = ((fwd << 2) | (uint64_t)c) & mask;
+        rc = (rc >> 2) | ((uint64_t)(3 - c) << sh);
+        if (++run >= k) f(fwd < rc ? fwd : rc, i);
+    }
+}
+
+struct Buf { void* p; };
+
+template <class T>
+T* dup_vec(const std::vector<T>& v) {
+    T* p = (T*)std::malloc(std::max<size_t>(1, v.size() * sizeof(T)));
+    if (!v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(T));
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+void or_free(void* p) { std::free(p); }
+
+// --- A1/A2: KmerIterator (src/common/KmerIterator.cpp:23-76) ------------------------
+// Writes the canonical k-mer and the end-exclusive position_in_sequence of every
+// window of `seq`.  Returns the number of windows: 0 when len < k
+// (KmerIterator.cpp:33-34), len-k+1 otherwise; -1 when k > 32 (KmerIterator.cpp:24-26)
+// or k < 1.  Output pointers may be null (count only).
+int64_t or_kmer_windows(const char* seq, uint64_t len, int k, uint64_t* out_kmer,
+                        uint32_t* out_pos) {
+    if (k > 32 || k < 1) return -1;
+    if (len < (uint64_t)k) return 0;
+    const uint64_t mask = kmask(k);             // KmerIterator.cpp:30 clearing_mask
+    const int sh = 2 * (k - 1);                 // KmerIterator.cpp:31 complement_shift_by
+    uint64_t fwd = 0, rc = 0;
+    int64_t w = 0;
+    for (uint64_t i = 0; i < len; ++i) {
+        fwd = ((fwd << 2) | ref_fwd_code(seq[i])) & mask;   // roll_forward_strand :54-58
+        rc = (rc >> 2) | (ref_rc_code(seq[i]) << sh);       // roll_complementary_strand :60-63
+        if (i + 1 >= (uint64_t)k) {                         // next_kmer :65-76
+            if (out_kmer) out_kmer[w] = fwd < rc ? fwd : rc;
+            if (out_pos) out_pos[w] = (uint32_t)(i + 1);
+            ++w;
+        }
+    }
+    return w;
+}
+
+// --- A3: jellyfish count of one read file (run_jellyfish.sh:3-6) -------------------
+// `s` is the file's sequences joined by any non-ACGT separator byte.  Exact count of
+// canonical k-mers, k-mers with count < min_count dropped (`--bc` drops singletons),
+// output ascending by 2-bit code == LC_ALL=C order of the dump (run_jellyfish.sh:6).
+// Returns the number of (key,count) rows; *keys/*counts are malloc'ed (or_free).
+int64_t or_count_stream(const char* s, uint64_t n, int k, uint32_t min_count,
+                        uint64_t** keys, uint32_t** counts) {
+    if (k > 32 || k < 1) return -1;
+    std::unordered_map<uint64_t, uint32_t> m;
+    for_each_jf_kmer(s, n, k, [&](uint64_t c, uint64_t) { ++m[c]; });
+    std::vector<std::pair<uint64_t, uint32_t>> v;
+    v.reserve(m.size());
+    for (auto& kv : m)
+        if (kv.second >= min_count) v.push_back(kv);
+    std::sort(v.begin(), v.end());
+    std::vector<uint64_t> ks(v.size());
+    std::vector<uint32_t> cs(v.size());
+    for (size_t i = 0; i < v.size(); ++i) { ks[i] = v[i].first; cs[i] = v[i].second; }
+    *keys = dup_vec(ks);
+    *counts = dup_vec(cs);
+    return (int64_t)v.size();
+}
+
+// Number of k-mer windows the jellyfish semantics count in a stream.
+uint64_t or_count_instances(const char* s, uint64_t n, int k) {
+    uint64_t c = 0;
+    for_each_jf_kmer(s, n, k, [&](uint64_t, uint64_t) { ++c; });
+    return c;
+}
+
+// Multi-threaded exact count (cpu_baseline leg).  Threads take contiguous slices of
+// the stream (cut at separator bytes so no window is split), count into private
+// hash maps partitioned by key hash, then each partition is merged by one thread.
+int64_t or_count_stream_mt(const char* s, uint64_t n, int k, uint32_t min_count,
+                           int threads, uint64_t** keys, uint32_t** counts) {
+    if (k > 32 || k < 1) return -1;
+    if (threads < 1) threads = 1;
+    const int P = threads;
+    std::vector<uint64_t> cut(threads + 1, 0);
+    cut[threads] = n;
+    for (int t = 1; t < threads; ++t) {
+        uint64_t c = n * (uint64_t)t / threads;
+        if (c < cut[t - 1]) c = cut[t - 1];
+        while (c < n && jf_code((unsigned char)s[c]) >= 0) ++c;
+        cut[t] = c;
+    }
+    auto part_of = [P](uint64_t key) {
+        uint64_t h = key * 0x9E3779B97F4A7C15ull;
+        return (int)((h >> 40) % (uint64_t)P);
+    };
+    std::vector<std::vector<std::unordered_map<uint64_t, uint32_t>>> local(
+        threads, std::vector<std::unordered_map<uint64_t, uint32_t>>(P));
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                auto& L = local[t];
+                for_each_jf_kmer(s + cut[t], cut[t + 1] - cut[t], k,
+                                 [&](uint64_t c, uint64_t) { ++L[part_of(c)][c]; });
+            });
+        for (auto& x : th) x.join();
+    }
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> out(P);
+    {
+        std::vector<std::thread> th;
+        for (int p = 0; p < P; ++p)
+            th.emplace_back([&, p] {
+                std::unordered_map<uint64_t, uint32_t> m;
+                for (int t = 0; t < threads; ++t)
+                    for (auto& kv : local[t][p]) m[kv.first] += kv.second;
+                for (int t = 0; t < threads; ++t) std::unordered_map<uint64_t, uint32_t>().swap(local[t][p]);
+                auto& o = out[p];
+                for (auto& kv : m)
+                    if (kv.second >= min_count) o.push_back(kv);
+                std::sort(o.begin(), o.end());
+            });
+        for (auto& x : th) x.join();
+    }
+    // k-way merge of the P sorted partitions
+    size_t total = 0;
+    for (auto& o : out) total += o.size();
+    std::vector<uint64_t> ks;
+    std::vector<uint32_t> cs;
+    ks.reserve(total);
+    cs.reserve(total);
+    std::vector<size_t> idx(P, 0);
+    using QE = std::pair<uint64_t, int>;
+    std::vector<QE> heap;
+    for (int p = 0; p < P; ++p)
+        if (!out[p].empty()) heap.push_back({out[p][0].first, p});
+    auto cmp = [](const QE& a, const QE& b) { return a.first > b.first; };
+    std::make_heap(heap.begin(), heap.end(), cmp);
+    while (!heap.empty()) {
+        std::pop_heap(heap.begin(), heap.end(), cmp);
+        int p = heap.back().second;
+        heap.pop_back();
+        ks.push_back(out[p][idx[p]].first);
+        cs.push_back(out[p][idx[p]].second);
+        if (++idx[p] < out[p].size()) {
+            heap.push_back({out[p][idx[p]].first, p});
+            std::push_heap(heap.begin(), heap.end(), cmp);
+        }
+    }
+    *keys = dup_vec(ks);
+    *counts = dup_vec(cs);
+    return (int64_t)ks.size();
+}
+
+// --- A4: k-way merge of the per-file sorted dumps -------------------------------------
+// JellyfishOccurrenceReader::get_next_kmer (JellyfishOccurrenceReader.cpp:63-86): one
+// merged row per distinct k-mer, counts[f] = 0 where file f's dump lacks it.
+// For a fixed k the string order of the dump lines equals ascending 2-bit code.
+// Inputs: F sorted key arrays with counts.  Output: merged keys (ascending) and a
+// row-major [rows][F] count matrix.  Returns rows.
+int64_t or_merge(int F, const uint64_t* const* keys, const uint32_t* const* counts,
+                 const uint64_t* lens, uint64_t** out_keys, uint32_t** out_counts) {
+    std::map<uint64_t, std::vector<uint32_t>> m;
+    for (int f = 0; f < F; ++f)
+        for (uint64_t i = 0; i < lens[f]; ++i) {
+            auto it = m.find(keys[f][i]);
+            if (it == m.end()) it = m.emplace(keys[f][i], std::vector<uint32_t>(F, 0)).first;
+            it->second[f] = counts[f][i];
+        }
+    std::vector<uint64_t> ks;
+    std::vector<uint32_t> cs;
+    ks.reserve(m.size());
+    cs.reserve(m.size() * F);
+    for (auto& kv : m) {
+        ks.push_back(kv.first);
+        for (int f = 0; f < F; ++f) cs.push_back(kv.second[f]);
+    }
+    *out_keys = dup_vec(ks);
+    *out_counts = dup_vec(cs);
+    return (int64_t)ks.size();
+}
+
+// --- A5: get_specificity (JellyfishOccurrenceReader.cpp:88-108) ----------------------
+// For every merged row: total = Σcounts, prevalent = max counts,
+// spec = *thresholds.upper_bound(((double)prevalent / (double)total) * 100)
+// and result[spec][total] += 1.  Output: flattened (threshold_index, total, n) triples
+// in std::map order (threshold ascending, total ascending).  Returns the triple count;
+// *out is malloc'ed [3*count] int64.  (upper_bound past the largest threshold is
+// undefined in the reference; it cannot happen with the CLI's 100.01 sentinel.)
+int64_t or_specificity(int F, uint64_t rows, const uint32_t* counts, const double* thr,
+                       int n_thr, int64_t** out) {
+    std::set<double> T(thr, thr + n_thr);
+    std::vector<double> tv(T.begin(), T.end());
+    std::map<double, std::map<int, int>> result;
+    for (double t : tv) result.insert({t, {}});
+    for (uint64_t r = 0; r < rows; ++r) {
+        int prevalent = 0, total = 0;
+        for (int f = 0; f < F; ++f) {
+            int c = (int)counts[r * F + f];
+            prevalent = std::max(c, prevalent);
+            total += c;
+        }
+        auto it = T.upper_bound(((double)prevalent / (double)total) * 100);
+        if (it == T.end()) return -1;
+        result[*it].insert(std::pair<int, int>(total, 0)).first->second += 1;
+    }
+    std::vector<int64_t> v;
+    for (auto& tk : result) {
+        int ti = (int)(std::lower_bound(tv.begin(), tv.end(), tk.first) - tv.begin());
+        for (auto& oc : tk.second) {
+            v.push_back(ti);
+            v.push_back(oc.first);
+            v.push_back(oc.second);
+        }
+    }
+    *out = dup_vec(v);
+    return (int64_t)(v.size() / 3);
+}
+
+// --- A7: export_kmers selection (JellyfishOccurrenceReader.cpp:110-135) -------------
+// Deterministic part (percent >= 1): every merged row with lower <= total <= upper is
+// exported in merge order; `discriminative` counts exported rows with exactly one
+// nonzero file count (:128-130).  Returns the number exported; keys malloc'ed.
+int64_t or_select(int F, uint64_t rows, const uint64_t* keys, const uint32_t* counts,
+                  int64_t lower, int64_t upper, uint64_t** out_keys, uint64_t* n_discr) {
+    std::vector<uint64_t> ks;
+    uint64_t d = 0;
+    for (uint64_t r = 0; r < rows; ++r) {
+        int64_t total = 0;
+        int nz = 0;
+        for (int f = 0; f < F; ++f) {
+            total += counts[r * F + f];
+            nz += counts[r * F + f] > 0;
+        }
+        if (lower <= total && total <= upper) {
+            ks.push_back(keys[r]);
+            if (nz == 1) ++d;
+        }
+    }
+    *n_discr = d;
+    *out_keys = dup_vec(ks);
+    return (int64_t)ks.size();
+}
+
+// --- A8: load_text_file_kmers (src/read_clustering.cpp:18-33) ------------------------
+// Per line (std::getline, so no trailing-newline line): k = line length, the line's
+// canonical code via KmerIterator, inserted into a std::unordered_set<uint64_t>.
+// KmerIDs are the set's iteration order (ReadClusteringEngine.cpp:237-241), so the
+// output is the keys in that order.  *k_out = the last line's length.  Returns the
+// number of keys, -1 if a line is longer than 32 (KmerIterator throws).
+int64_t or_load_sdk_text(const char* text, uint64_t n, uint64_t** keys_in_id_order,
+                         int* k_out) {
+    std::unordered_set<uint64_t> s;
+    int k = 0;
+    uint64_t i = 0;
+    while (i < n) {
+        uint64_t j = i;
+        while (j < n && text[j] != '\n') ++j;
+        const char* line = text + i;
+        uint64_t len = j - i;
+        k = (int)len;
+        if (k > 32) return -1;
+        uint64_t code = 0;  // current_kmer stays 0 when next_kmer() returns false
+        if (k >= 1) or_kmer_windows(line, len, k, &code, nullptr);
+        s.insert(code);
+        i = j + 1;
+    }
+    std::vector<uint64_t> v(s.begin(), s.end());
+    *keys_in_id_order = dup_vec(v);
+    *k_out = k;
+    return (int64_t)v.size();
+}
+
+// --- A9: construct_indices (src/clustering/ReadClusteringEngine.cpp:234-299) ---------
+// Reads are given as a CSR (bases, offsets[n+1]) in reader order; read_ids[i] is the
+// reader's 1-based ReadID.  SDK keys are given in KmerID order.
+// Outputs (all malloc'ed, or_free):
+//  hit_ptr[n+1], hit_kid[H], hit_pos[H]  - per read, every window whose canonical code
+//        is in the set, in window order (:248-254), with the end-exclusive position;
+//  sorted_kid[H]                         - per read, the KmerIDs sorted ascending with
+//        duplicates (ReadComponent::discriminative_kmer_ids, :262-272);
+//  first_ptr[n+1], first_kid[U], first_pos[U] - per read, kmer_positions (:267):
+//        the FIRST position of each distinct KmerID, listed by ascending KmerID;
+//  kci_ptr[K+1], kci_read[H]             - kmer_component_index: per KmerID the
+//        ReadIDs (one per occurrence) sorted ascending (:262-263, 282-284).
+// Returns H.
+int64_t or_construct_indices(const char* bases, const uint64_t* offsets, uint64_t n,
+                             const uint32_t* read_ids, int k, const uint64_t* sdk_keys,
+                             uint32_t n_sdk, uint64_t** hit_ptr, uint32_t** hit_kid,
+                             uint32_t** hit_pos, uint32_t** sorted_kid, uint64_t** first_ptr,
+                             uint32_t** first_kid, uint32_t** first_pos, uint64_t** kci_ptr,
+                             uint32_t** kci_read, uint64_t* n_first) {
+    if (k > 32 || k < 1) return -1;
+    std::unordered_map<uint64_t, uint32_t> kmer_index;  // KmerIndex, :237-241
+    for (uint32_t i = 0; i < n_sdk; ++i) kmer_index[sdk_keys[i]] = i;
+    std::vector<std::vector<uint32_t>> kci(n_sdk);
+    std::vector<uint64_t> hp(n + 1, 0), fp(n + 1, 0);
+    std::vector<uint32_t> hk, hpos, sk, fk, fpos;
+    std::vector<uint64_t> wk;
+    std::vector<uint32_t> wp;
+    for (uint64_t r = 0; r < n; ++r) {
+        uint64_t len = offsets[r + 1] - offsets[r];
+        wk.resize(len + 1);
+        wp.resize(len + 1);
+        int64_t w = or_kmer_windows(bases + offsets[r], len, k, wk.data(), wp.data());
+        std::vector<uint32_t> ids;
+        std::map<uint32_t, uint32_t> firstpos;  // robin_map insert: first wins
+        for (int64_t i = 0; i < w; ++i) {
+            auto it = kmer_index.find(wk[i]);
+            if (it == kmer_index.end()) continue;
+            hk.push_back(it->second);
+            hpos.push_back(wp[i]);
+            ids.push_back(it->second);
+            kci[it->second].push_back(read_ids[r]);
+            firstpos.insert({it->second, wp[i]});
+        }
+        std::sort(ids.begin(), ids.end());
+        sk.insert(sk.end(), ids.begin(), ids.end());
+        for (auto& kv : firstpos) {
+            fk.push_back(kv.first);
+            fpos.push_back(kv.second);
+        }
+        hp[r + 1] = hk.size();
+        fp[r + 1] = fk.size();
+    }
+    std::vector<uint64_t> kp(n_sdk + 1, 0);
+    std::vector<uint32_t> kr;
+    for (uint32_t i = 0; i < n_sdk; ++i) {
+        std::sort(kci[i].begin(), kci[i].end());
+        kr.insert(kr.end(), kci[i].begin(), kci[i].end());
+        kp[i + 1] = kr.size();
+    }
+    *hit_ptr = dup_vec(hp);
+    *hit_kid = dup_vec(hk);
+    *hit_pos = dup_vec(hpos);
+    *sorted_kid = dup_vec(sk);
+    *first_ptr = dup_vec(fp);
+    *first_kid = dup_vec(fk);
+    *first_pos = dup_vec(fpos);
+    *kci_ptr = dup_vec(kp);
+    *kci_read = dup_vec(kr);
+    *n_first = fk.size();
+    return (int64_t)hk.size();
+}
+
+// Multi-threaded lookup-only timing kernel for the cpu_baseline leg: counts SDK hits
+// over all windows of all reads with a std::unordered_set, reads split over threads.
+uint64_t or_lookup_hits_mt(const char* bases, const uint64_t* offsets, uint64_t n, int k,
+                           const uint64_t* sdk_keys, uint32_t n_sdk, int threads) {
+    std::unordered_set<uint64_t> s(sdk_keys, sdk_keys + n_sdk);
+    if (threads < 1) threads = 1;
+    std::atomic<uint64_t> hits{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            uint64_t h = 0;
+            std::vector<uint64_t> wk;
+            for (uint64_t r = (uint64_t)t; r < n; r += threads) {
+                uint64_t len = offsets[r + 1] - offsets[r];
+                wk.resize(len + 1);
+                int64_t w = or_kmer_windows(bases + offsets[r], len, k, wk.data(), nullptr);
+                for (int64_t i = 0; i < w; ++i) h += s.count(wk[i]);
+            }
+            hits += h;
+        });
+    for (auto& x : th) x.join();
+    return hits.load();
+}
+
+}  // extern "C"

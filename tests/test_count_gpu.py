@@ -1,0 +1,159 @@
+"""Counting path on the MI355X (through the C ABI) against the oracle and the golden fixtures.
+Bit-exact: per-file dumps, merged rows, specificity histogram, export selection."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def run_gpu(ctx, streams, k, lower, upper, min_count=2, thr=oracle.THRESHOLDS):
+    ctx.count_begin(k, len(streams))
+    for f, s in enumerate(streams):
+        ctx.count_add(f, s)
+    ctx.count_run(min_count)
+    keys, counts = ctx.rows()
+    hist = ctx.spec_hist(thr) if len(keys) else np.zeros((0, 3), np.int64)
+    sel, flags, nd = ctx.select(lower, upper)
+    dumps = [ctx.dump(f) for f in range(len(streams))]
+    return {"keys": keys, "counts": counts, "hist": hist, "selected": sel, "flags": flags, "n_discr": nd,
+            "dumps": dumps, "stats": ctx.count_stats()}
+
+
+def assert_same(g, o):
+    assert np.array_equal(g["keys"], o["keys"])
+    assert np.array_equal(g["counts"], o["counts"])
+    assert np.array_equal(g["hist"], o["hist"])
+    assert np.array_equal(g["selected"], o["selected"])
+    assert g["n_discr"] == o["n_discr"]
+    for (gk, gc), (ok, oc) in zip(g["dumps"], o["dumps"]):
+        assert np.array_equal(gk, ok) and np.array_equal(gc, oc)
+
+
+def golden_streams(hga_mod):
+    return [hga_mod.jf_stream(os.path.join(GOLD, p)) for p in ("reads_a.fq", "reads_b.fq")]
+
+
+@pytest.mark.parametrize("k", [5, 15, 19, 21, 31, 32])
+def test_count_golden(gpu_ctx, hga_mod, k):
+    g = np.load(os.path.join(GOLD, "count_golden.npz"))
+    r = run_gpu(gpu_ctx, golden_streams(hga_mod), k, 3, 12)
+    assert np.array_equal(r["keys"], g[f"k{k}_rows_keys"])
+    assert np.array_equal(r["counts"], g[f"k{k}_rows_counts"])
+    assert np.array_equal(r["hist"], g[f"k{k}_hist"])
+    assert np.array_equal(r["selected"], g[f"k{k}_selected"])
+    assert r["n_discr"] == int(g[f"k{k}_n_discr"][0])
+    for f in range(2):
+        assert np.array_equal(r["dumps"][f][0], g[f"k{k}_dump{f}_keys"])
+        assert np.array_equal(r["dumps"][f][1], g[f"k{k}_dump{f}_counts"])
+    assert r["stats"].instances == int(g[f"k{k}_instances"][0])
+    # discriminative flags agree with the row counts
+    nz = (r["counts"] > 0).sum(1)
+    idx = np.searchsorted(r["keys"], r["selected"])
+    assert np.array_equal(r["flags"].astype(bool), nz[idx] == 1)
+
+
+def random_streams(seed, n_files, n_reads, rlen, alphabet="ACGT", dup=0.5):
+    rng = random.Random(seed)
+    out = []
+    base = ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, rlen))) for _ in range(n_reads)]
+    for f in range(n_files):
+        rs = [r for r in base if rng.random() < 0.7] + \
+             ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, rlen))) for _ in range(n_reads // 3)]
+        rs += rs[: int(len(rs) * dup)]
+        rng.shuffle(rs)
+        out.append("\n".join(rs).encode())
+    return out
+
+
+@pytest.mark.parametrize("k", [1, 2, 7, 12, 16, 19, 21, 22, 27, 31, 32])
+def test_count_random_vs_oracle(gpu_ctx, k):
+    streams = random_streams(k, 2, 400, 120, "ACGTACGTACGTNacgt")
+    o = oracle.count_pipeline(streams, k, 2, 6)
+    assert_same(run_gpu(gpu_ctx, streams, k, 2, 6), o)
+
+
+@pytest.mark.parametrize("n_files", [1, 3, 5])
+@pytest.mark.parametrize("min_count", [1, 2, 3])
+def test_count_files_and_min(gpu_ctx, n_files, min_count):
+    streams = random_streams(100 + n_files, n_files, 300, 100)
+    o = oracle.count_pipeline(streams, 19, 2, 9, min_count=min_count)
+    assert_same(run_gpu(gpu_ctx, streams, 19, 2, 9, min_count=min_count), o)
+
+
+def test_count_edge_inputs(gpu_ctx):
+    cases = [
+        [b"", b""],                                  # empty files
+        [b"\n\n\n", b"NNNN"],                        # no bases at all
+        [b"ACG", b"AC"],                             # reads shorter than k
+        [b"A" * 5000 + b"\n" + b"T" * 5000, b"A" * 10],   # one heavy k-mer (poly-A)
+        [b"ACGTN" * 2000, b"acgtn" * 2000],
+    ]
+    for streams in cases:
+        o = oracle.count_pipeline(streams, 4, 1, 10 ** 9, min_count=1)
+        assert_same(run_gpu(gpu_ctx, streams, 4, 1, 10 ** 9, min_count=1), o)
+
+
+def test_count_split_buckets_all_distinct(gpu_ctx, hga_mod):
+    # coverage-1 random reads: every k-mer distinct -> buckets exceed the LDS table and
+    # must be split into sub-ranges
+    g = hga_mod.gen_genome(3_000_000, 77)
+    streams = [g[:1_500_000], g[1_500_000:]]
+    o = oracle.count_pipeline(streams, 25, 1, 5, min_count=1)
+    r = run_gpu(gpu_ctx, streams, 25, 1, 5, min_count=1)
+    assert_same(r, o)
+    assert r["stats"].max_split > 1
+
+
+def test_count_rerun_and_chunked_add(gpu_ctx):
+    streams = random_streams(9, 2, 500, 150)
+    a = run_gpu(gpu_ctx, streams, 19, 2, 8)
+    gpu_ctx.count_run(2)
+    b_keys, b_counts = gpu_ctx.rows()
+    assert np.array_equal(a["keys"], b_keys) and np.array_equal(a["counts"], b_counts)
+    # adding a file in several chunks (split at read boundaries) gives the same result
+    gpu_ctx.count_begin(19, 2)
+    for f, s in enumerate(streams):
+        parts = s.split(b"\n")
+        h = len(parts) // 2
+        gpu_ctx.count_add(f, b"\n".join(parts[:h]))
+        gpu_ctx.count_add(f, b"\n".join(parts[h:]))
+    gpu_ctx.count_run(2)
+    c_keys, c_counts = gpu_ctx.rows()
+    assert np.array_equal(a["keys"], c_keys) and np.array_equal(a["counts"], c_counts)
+
+
+def test_count_c1_scale_vs_oracle(gpu_ctx, hga_mod):
+    # BASELINE config 1 shape: 500 kb random pair, 3 % divergence, ART-like 30x, k=19
+    ga = hga_mod.gen_genome(500_000, 1)
+    gb = hga_mod.gen_haplotype(ga, 0.03, 0, 2)
+    ra = hga_mod.gen_art(ga, 100_000, 150, 3)
+    rb = hga_mod.gen_art(gb, 100_000, 150, 4)
+    streams = [ra.seq, rb.seq]
+    o = {"dumps": [oracle.count_stream(s, 19, 2, threads=8) for s in streams]}
+    o["keys"], o["counts"] = oracle.merge(o["dumps"])
+    o["hist"] = oracle.specificity(o["counts"], oracle.THRESHOLDS)
+    o["selected"], o["n_discr"] = oracle.select(o["keys"], o["counts"], 10, 25)
+    r = run_gpu(gpu_ctx, streams, 19, 10, 25)
+    assert_same(r, o)
+    assert r["stats"].instances == 2 * 100_000 * 132
+
+
+def test_count_conservation_large(gpu_ctx, hga_mod):
+    # size-independent property at a C2-like size: with min_count=1 every window is counted
+    # exactly once, so the merged counts sum to the number of windows
+    g = hga_mod.gen_genome(4_641_652, 11)
+    r = hga_mod.gen_art(g, 900_000, 150, 12)
+    gpu_ctx.count_begin(19, 1)
+    gpu_ctx.count_add(0, r.seq)
+    gpu_ctx.count_run(1)
+    st = gpu_ctx.count_stats()
+    assert st.instances == 900_000 * 132
+    keys, counts = gpu_ctx.rows()
+    assert int(counts.sum()) == st.instances
+    assert np.all(np.diff(keys.astype(np.int64)) > 0)

@@ -1,0 +1,116 @@
+"""Host-side C++ (libhga_host.so, the CLIs' argv handling) — no GPU needed."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import pyref_reader
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "hybrid-genome-assembler_amd", "bin")
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def write(path, text):
+    with open(path, "wb") as f:
+        f.write(text.encode() if isinstance(text, str) else text)
+    return str(path)
+
+
+def check_reader(hga_mod, paths, annotate):
+    got = hga_mod.load_records(paths, annotate)
+    want = pyref_reader.read_records(paths, annotate)
+    assert len(got["offsets"]) - 1 == len(want)
+    for i, r in enumerate(want):
+        a, b = int(got["offsets"][i]), int(got["offsets"][i + 1])
+        assert got["bases"][a:b].decode("latin-1") == r["seq"]
+        assert int(got["category"][i]) == r["cat"]
+        assert (int(got["start"][i]), int(got["end"][i])) == (r["start"], r["end"])
+    return got, want
+
+
+def test_reader_fastq_fasta_mix(tmp_path, hga_mod):
+    a = write(tmp_path / "a.fq", "@r1\nACGTN\n+\nIIIII\n@r2\nacgtACGT\n+\nIIIIIIII\n")
+    b = write(tmp_path / "b.fa", ">s1\nTTTT\n>s2\nGATTACA\n")
+    got, want = check_reader(hga_mod, [a, b], True)
+    # FASTQ -> FASTA: the first record of the FASTA file is read with the FASTQ layout
+    # (the reader switches layout only when it opens the next file) — reference quirk.
+    assert [r["seq"] for r in want] == ["ACGTN", "acgtACGT", "TTTT"]
+    assert got["filename"] == "a.fq__b.fa"
+    meta = got["meta"]
+    assert meta[0].tolist() == [2, 13, 5, 8, 6]
+    # all-files meta never updates max_read_length (SequenceRecordIterator.cpp:45-48)
+    assert meta[2][3] == 0
+
+
+def test_reader_crlf_and_ids(tmp_path, hga_mod):
+    a = write(tmp_path / "c.fq", "@x\r\nACGT\r\n+\r\nIIII\r\n@y\r\nGG\r\n+\r\nII\r\n")
+    b = write(tmp_path / "d.fq", "@z\nCCCC\n+\nIIII\n")
+    got, want = check_reader(hga_mod, [a, b], False)
+    assert [r["seq"] for r in want] == ["ACGT\r", "GG\r", "CCCC"]   # no CR stripping
+    assert got["category"].tolist() == [0, 0, 0]
+
+
+def test_reader_nanosim_and_simlord_headers(tmp_path, hga_mod):
+    a = write(tmp_path / "n.fa", ">hapA_1200_aligned_0_F_0_350_0\nACGT\n>hapA_77_aligned_1_R_0_90_0\nAC\n")
+    b = write(tmp_path / "s.fq", "@read;length=120bp;startpos=5;x\nAAAA\n+\nIIII\n")
+    got, want = check_reader(hga_mod, [a], True)
+    assert (got["start"].tolist(), got["end"].tolist()) == ([1200, 77], [1550, 167])
+    got, want = check_reader(hga_mod, [b], True)
+    assert (got["start"].tolist(), got["end"].tolist()) == ([5], [125])
+
+
+def test_reader_errors(tmp_path, hga_mod):
+    bad = write(tmp_path / "bad.txt", "hello\nworld\n")
+    with pytest.raises(hga_mod.HgaError, match="Unrecognized file format"):
+        hga_mod.load_records([bad], True)
+    with pytest.raises(hga_mod.HgaError, match="does not exist"):
+        hga_mod.load_records([str(tmp_path / "nope.fq")], True)
+
+
+def test_jf_stream_multiline(tmp_path, hga_mod):
+    p = write(tmp_path / "m.fa", ">a\nACGT\nTTGA\n>b\nCC\n\n>c\nG\n")
+    assert hga_mod.jf_stream(p) == b"ACGTTTGA\nCC\nG"
+    q = write(tmp_path / "m.fq", "@a\nACGT\nAC\n+\nIIII\nII\n@b\nGG\n+a\n@I\n")
+    assert hga_mod.jf_stream(q) == b"ACGTAC\nGG"
+
+
+@pytest.mark.parametrize("v,s", [(100.0, "100"), (70.0, "70"), (100.01, "100.01"), (12.5, "12.5"),
+                                 (0.07 * 100, "7.000000000000001"), (0.57 * 100, "56.99999999999999"), (40.0, "40"), (1e-5, "1e-05"),
+                                 (1e16, "1e+16"), (1e15, "1000000000000000"), (0.0001, "0.0001"),
+                                 (0.0, "0"), (99.5, "99.5")])
+def test_fmt_double(hga_mod, v, s):
+    assert hga_mod.fmt_double(v) == s
+
+
+def test_generators_deterministic(hga_mod):
+    g = hga_mod.gen_genome(10000, 5)
+    assert len(g) == 10000 and set(g) <= set(b"ACGT")
+    assert g == hga_mod.gen_genome(10000, 5)
+    h = hga_mod.gen_haplotype(g, 0.03, 500, 9)
+    assert len(h) == 10500
+    r1 = hga_mod.gen_art(g, 5000, 150, 1)
+    r2 = hga_mod.gen_art(g, 5000, 150, 1)
+    assert r1.seq == r2.seq and r1.n == 5000
+    assert r1.seq.count(b"\n") == 4999 and len(r1.bases) == 5000 * 150
+    ns = hga_mod.gen_nanosim(g, 50, 3)
+    lens = np.diff(ns.offsets)
+    assert ns.n == 50 and lens.min() >= 1
+
+
+def test_cli_help_needs_no_gpu():
+    for tool in ("jf_occurrences", "categorization"):
+        out = subprocess.run([os.path.join(BIN, tool), "--help"], capture_output=True, text=True, timeout=60)
+        assert out.returncode == 0
+        assert "Options" in out.stdout
+
+
+def test_cli_argument_errors():
+    out = subprocess.run([os.path.join(BIN, "jf_occurrences")], capture_output=True, text=True, timeout=60)
+    assert out.returncode != 0 and "You need to specify paths to read files" in out.stderr
+    out = subprocess.run([os.path.join(BIN, "categorization"), "x.fq"], capture_output=True, text=True, timeout=60)
+    assert out.returncode != 0 and "You need to specify path to kmers" in out.stderr
+    out = subprocess.run([os.path.join(BIN, "jf_occurrences"), "--bogus", "x"], capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode != 0 and "unrecognised option" in out.stderr

@@ -1,0 +1,100 @@
+"""SDK lookup / index construction on the MI355X against the oracle and golden fixtures."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NAMES = ["hit_ptr", "hit_kid", "hit_pos", "sorted_kid", "first_ptr", "first_kid", "first_pos", "kci_ptr",
+         "kci_read"]
+
+
+def run_gpu(ctx, bases, offsets, k, sdk, first_id=1):
+    ctx.lookup_load(k, sdk)
+    ctx.lookup_set_reads(bases, offsets, first_id)
+    ctx.lookup_run()
+    return ctx.lookup_fetch()
+
+
+def assert_same(g, o):
+    for n in NAMES:
+        assert np.array_equal(g[n], o[n]), n
+
+
+def test_lookup_golden(gpu_ctx, hga_mod):
+    g = np.load(os.path.join(GOLD, "lookup_golden.npz"))
+    paths = [os.path.join(GOLD, p) for p in ("reads_a.fq", "reads_b.fq", "reads_c.fa")]
+    rec = hga_mod.load_records(paths, True)
+    r = run_gpu(gpu_ctx, rec["bases"], rec["offsets"], 19, g["sdk_keys_id_order"])
+    assert_same(r, g)
+    s = gpu_ctx.lookup_sizes()
+    assert s.reads_hit == int((np.diff(g["hit_ptr"]) > 0).sum())
+
+
+def random_case(seed, n_reads, maxlen, k, alphabet, n_sdk):
+    rng = random.Random(seed)
+    reads = [("".join(rng.choice(alphabet) for _ in range(rng.randint(0, maxlen)))).encode() for _ in range(n_reads)]
+    pool = set()
+    for r in reads[: max(1, n_reads // 3)]:
+        c, _ = oracle.kmer_windows(r, k)
+        pool.update(c.tolist())
+    sdk = rng.sample(sorted(pool), min(n_sdk, len(pool))) if pool else []
+    sdk += [rng.getrandbits(min(2 * k, 62)) for _ in range(20)]
+    sdk = np.array(list(dict.fromkeys(sdk)), np.uint64)
+    bases = b"".join(reads)
+    offsets = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    return bases, offsets, sdk
+
+
+@pytest.mark.parametrize("k", [1, 3, 11, 19, 21, 31, 32])
+def test_lookup_random_vs_oracle(gpu_ctx, k):
+    bases, offsets, sdk = random_case(k, 700, 200, k, "ACGTACGTACGTNa", 3000)
+    assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 7), oracle.construct_indices(bases, offsets, k, sdk, 7))
+
+
+def test_lookup_long_reads(gpu_ctx, hga_mod):
+    g = hga_mod.gen_genome(200_000, 3)
+    r = hga_mod.gen_nanosim(g, 120, 4)
+    c, _ = oracle.kmer_windows(g[:50_000], 19)
+    sdk = np.unique(c)[::7]
+    assert_same(run_gpu(gpu_ctx, r.bases, r.offsets, 19, sdk), oracle.construct_indices(r.bases, r.offsets, 19, sdk))
+
+
+def test_lookup_edges(gpu_ctx):
+    cases = [
+        ([b"", b"", b"ACGT"], [0, 1, 5]),
+        ([b"A" * 100, b"", b"T" * 50], [0]),          # every window hits one id
+        ([b"AC", b"G", b"T"], [1, 2, 3]),              # all shorter than k
+        ([b"NNNNNNNN", b"acgtacgt"], [0, 27]),
+    ]
+    for reads, sdk in cases:
+        bases = b"".join(reads)
+        offsets = np.cumsum([0] + [len(x) for x in reads]).astype(np.uint64)
+        sdk = np.array(sdk, np.uint64)
+        assert_same(run_gpu(gpu_ctx, bases, offsets, 4, sdk), oracle.construct_indices(bases, offsets, 4, sdk))
+    # empty SDK set
+    bases, offsets = b"ACGTACGT", np.array([0, 8], np.uint64)
+    assert_same(run_gpu(gpu_ctx, bases, offsets, 4, np.zeros(0, np.uint64)),
+                oracle.construct_indices(bases, offsets, 4, np.zeros(0, np.uint64)))
+
+
+def test_lookup_c3_shape_property(gpu_ctx, hga_mod):
+    # C3-shaped (Nanosim-like long reads): the hit lists are consistent with each other
+    g = hga_mod.gen_genome(1_000_000, 5)
+    r = hga_mod.gen_nanosim(g, 2_000, 6)
+    c, _ = oracle.kmer_windows(g, 19)
+    sdk = np.unique(c)[::40]
+    res = run_gpu(gpu_ctx, r.bases, r.offsets, 19, sdk)
+    s = gpu_ctx.lookup_sizes()
+    assert res["hit_ptr"][-1] == s.hits == res["kci_ptr"][-1]
+    assert np.array_equal(np.bincount(res["hit_kid"], minlength=len(sdk)), np.diff(res["kci_ptr"]))
+    assert np.array_equal(np.sort(res["kci_read"]), np.sort(np.repeat(
+        np.arange(1, r.n + 1, dtype=np.uint32), np.diff(res["hit_ptr"]).astype(np.int64))))
+    # spot-check 200 reads against the oracle
+    o = oracle.construct_indices(r.bases[: int(r.offsets[200])], r.offsets[:201], 19, sdk)
+    h = int(o["hit_ptr"][-1])
+    assert np.array_equal(res["hit_kid"][:h], o["hit_kid"]) and np.array_equal(res["hit_pos"][:h], o["hit_pos"])
