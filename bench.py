@@ -114,9 +114,9 @@ def count_step(ctx):
 
 
 KERNEL_BYTES = {
-    # algorithmic bytes per launch, from the per-unit figures in DESIGN.md §4
-    "kc_hist": lambda s: s["bytes"],                                    # 1 B/base read
-    "kc_bin": lambda s: s["bytes"] + 4 * s["instances"],                # 1 B/base + 4 B/instance written
+    # algorithmic bytes per step, from the per-unit figures in DESIGN.md §4
+    "kc_bin1": lambda s: 0.375 * s["bytes"] + 4 * s["instances"],   # packed codes+valid read, 4 B/instance written
+    "kc_rebin": lambda s: 8 * s["instances"],                          # 4 B/instance read + 4 B written
     "kc_count": lambda s: 4 * s["instances"] + (8 + 4 * s["files"]) * s["rows"],   # read binned, write rows
 }
 
@@ -194,13 +194,13 @@ def main():
     value = inst_total / (dt_max / args.steps)
 
     kernels = {}
-    for name in ("kc_hist", "kc_scan", "kc_bin", "kc_count", "kc_spec_hist", "kc_select", "radix_upsweep",
-                 "radix_downsweep", "scan"):
+    for name in ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
+                 "radix_upsweep", "radix_downsweep", "scan"):
         ms, n = ctx.profile_get(name)
         if n:
             kernels[name] = {"ms_total": ms, "launches": n, "ms_per_step": ms / args.steps}
     ctx.profile(False)
-    dom = max(("kc_hist", "kc_bin", "kc_count"), key=lambda k: kernels.get(k, {}).get("ms_total", 0))
+    dom = max(("kc_bin1", "kc_rebin", "kc_count"), key=lambda k: kernels.get(k, {}).get("ms_total", 0))
     per_step_launches = kernels[dom]["launches"] / args.steps
     avg_launch_ms = kernels[dom]["ms_total"] / kernels[dom]["launches"]
     bytes_step = KERNEL_BYTES[dom](stats)
@@ -221,7 +221,7 @@ def main():
                                "150 bp, 2 files; per step: count_run + spec_hist + select[10,25]",
                    "k": K, "reads": ra.n + rb.n, "bases": st.bytes, "instances_per_gpu": st.instances,
                    "distinct_rows": st.distinct_rows, "selected": n_sel, "discriminative": n_disc,
-                   "buckets": st.buckets, "parallelism": f"dp{D.world}",
+                   "buckets": st.buckets, "max_split": st.max_split, "parallelism": f"dp{D.world}",
                    "exchange": "none: ranks count independent shards (replicas)" if D.world > 1 else None},
         "roofline": roofline,
         "pipeline_roofline": {"model": "16.25 B per k-mer instance (SURVEY.md §8(d))",

@@ -3,15 +3,17 @@
 // k-way merge passes of JellyfishOccurrenceReader (JellyfishOccurrenceReader.cpp:63-135).
 //
 // Pipeline (all HBM-bound integer work, no MFMA):
-//   A  kc_hist   per super-tile: scan the resident sequence bytes, canonical k-mer of
-//                every valid window, bijective 2k-bit mix, LDS histogram of the top
-//                fb bits (bucket) -> one row of st_hist[super-tile][bucket].
-//   S  kc_scan_cols / kc_bucket_scan / kc_file_start: column prefix sums -> every
-//                (super-tile, bucket) output offset; bucket-major, file-minor layout.
-//   B  kc_bin    recompute the windows, rank them inside a tile by bucket through
-//                LDS, write each bucket's run contiguously (coalesced) as the mixed
-//                value's low bits (u32 when 2k - fb <= 31).
-//   C  kc_count  one workgroup per bucket: LDS open-addressing table keyed by the
+//   P  kc_pack   ASCII -> 2-bit codes (u32 per 16 bases) + base-valid bits (u16 per 16).
+//   B1 kc_bin1   per tile of 8K window ends: closed-form canonical k-mer of every valid
+//                window from packed frames, bijective 2k-bit mix; the top fb1 (<= 6) bits
+//                pick a level-1 region, ranked through LDS so every region's run leaves as
+//                one coalesced segment (>= 512 B); space reserved with one returning atomic
+//                per (tile, region); per-fine-bucket histogram kept in LDS, flushed once.
+//   L  kc_layout one workgroup: fine-bucket bases (bucket-major, file-minor) and the
+//                chunk table of the level-1 regions.
+//   B2 kc_rebin  per 8K-element chunk of a level-1 region: the next fb2 bits pick the fine
+//                bucket (again <= 64-way, coalesced); writes the remainder (u32 when <= 31 bits).
+//   C  kc_count  one workgroup per fine bucket: LDS open-addressing table keyed by the
 //                remainder with one u32 counter per file; adaptive sub-range splitting
 //                if a bucket holds more distinct k-mers than the table; per-file drop
 //                of counts < min (jellyfish --bc); emit merged rows (key, counts[F]).
@@ -19,6 +21,7 @@
 //   X  kc_select      rows with lower <= total <= upper, + radix sort ascending
 //                     (export_kmers, :110-135; numeric order == LC_ALL=C order).
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 
 #include "hga_internal.hpp"
@@ -27,198 +30,297 @@
 namespace hga {
 namespace {
 
-constexpr int NT_AB = 1024;   // threads of pass A / B workgroups
-constexpr int P_AB = 16;      // window ends per thread per tile (u32 elements)
-constexpr int NT_B64 = 512;   // pass B workgroup for u64 elements (LDS budget)
-constexpr uint64_t TILE_POS = (uint64_t)NT_AB * P_AB;  // 16384
+constexpr int NT_B = 512;     // level-1 binning workgroup
+constexpr int P_B = 16;       // window ends per thread
+constexpr int TP_B = NT_B * P_B;       // 8192 window ends per tile
+constexpr uint64_t ST_ALIGN = TP_B;    // super-tiles are whole tiles
 constexpr int MAX_FB = 12;
 constexpr int MAX_NB = 1 << MAX_FB;
-constexpr int NT_C = 512;     // threads of the per-bucket count workgroup
+constexpr int MAX_FB1 = 6;    // level-1 fan-out <= 64
+constexpr int NB1_MAX = 1 << MAX_FB1;
+constexpr int NT_R = 512;     // re-bin workgroup
+constexpr int CH_R = NT_R * 16;        // 8192 elements per re-bin chunk
+constexpr int NT_C = 1024;    // threads of the per-bucket count workgroup
+constexpr int PF_C = 8;       // binned elements each count thread has in flight
 constexpr uint32_t LDS_TAB = 128 * 1024;
 
 struct KP {
     int k, sh;
     uint64_t mask;
     Mix mix;
-    uint32_t fb, rbits, nb;
+    uint32_t fb, rbits, nb;      // fine buckets: top fb bits; remainder = low rbits bits
     uint64_t rmask;
+    uint32_t fb1, r1bits, nb1;   // level-1 regions: top fb1 bits; element = low r1bits bits
+    uint64_t r1mask;
+    uint32_t fb2, nb2;           // level-2 digit: the next fb2 bits
 };
 
 __device__ __forceinline__ uint32_t bucket_of(uint64_t h, const KP& kp) {
     return kp.fb ? (uint32_t)(h >> kp.rbits) : 0u;
 }
+__device__ __forceinline__ uint32_t region_of(uint64_t h, const KP& kp) {
+    return kp.fb1 ? (uint32_t)(h >> kp.r1bits) : 0u;
+}
 
-// ---------------------------------------------------------------- pass A
-__global__ void __launch_bounds__(NT_AB) kc_hist(const uint8_t* __restrict__ s, uint64_t n,
-                                                 uint64_t st_pos, uint32_t st0, KP kp,
-                                                 uint32_t* __restrict__ st_hist,
-                                                 unsigned long long* __restrict__ instances) {
-    __shared__ uint32_t hist[MAX_NB];
-    __shared__ uint32_t ws[NT_AB / 64 + 1];
+// ---------------------------------------------------------------- pass P
+// One thread per 16 bases: packed codes (first base in bits 31:30) and valid bits.
+template <bool REF>
+__global__ void kc_pack(const uint8_t* __restrict__ s, uint64_t n, uint32_t* __restrict__ pk,
+                        uint16_t* __restrict__ vd, uint64_t nw) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const uint4 v = load16(s, (int64_t)(w * 16), n);
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    uint32_t code = 0, valid = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (ws[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        const uint32_t u = REF ? b : (b & 0xDFu);
+        const uint32_t d = u - 0x41u;
+        const bool ok = d < 20u && ((kBaseBits >> d) & 1u);
+        const uint32_t c = ok ? (((u >> 1) ^ (u >> 2)) & 3u) : 0u;
+        code |= c << (30 - 2 * j);
+        valid |= (ok ? 1u : 0u) << j;
+    }
+    pk[PAD_WORDS + w] = code;
+    vd[PAD_WORDS + w] = (uint16_t)valid;
+}
+
+// Canonical code of the window ending at p0+j, from a loaded frame.
+template <int P>
+__device__ __forceinline__ uint64_t frame_canon(const Frame<P>& f, int j, uint64_t mask) {
+    constexpr int NW = Frame<P>::NW;
+    const uint64_t fwd = field64<NW>(f.x, 2 * (16 * NW - 33 - j)) & mask;
+    const uint64_t rc = field64<NW>(f.r, 2 * j) & mask;
+    return fwd < rc ? fwd : rc;
+}
+
+// ---------------------------------------------------------------- pass B1
+// gstat: [0] row cursor, [1] max split, [2] error bits (1 unsplittable, 2 row capacity,
+// 4 level-1 region overflow), [4] instances.
+template <class E1>
+__global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
+                                                const uint16_t* __restrict__ vd, uint64_t n,
+                                                uint64_t st_pos, uint32_t file, uint32_t F, KP kp,
+                                                unsigned long long* __restrict__ cursor1,
+                                                const uint64_t* __restrict__ end1,
+                                                E1* __restrict__ out1,
+                                                unsigned long long* __restrict__ fine_hist,
+                                                unsigned long long* __restrict__ gstat) {
+    __shared__ uint32_t cnt1[NB1_MAX];
+    __shared__ uint32_t off1[NB1_MAX + 1];
+    __shared__ unsigned long long base1[NB1_MAX];
+    __shared__ unsigned long long lim1[NB1_MAX];
+    __shared__ uint32_t fhist[MAX_NB];
+    __shared__ E1 stage[TP_B];
+    __shared__ uint8_t sd1[TP_B];
+    __shared__ uint32_t ws[NT_B / 64 + 1];
     const int tid = threadIdx.x;
-    for (uint32_t b = tid; b < kp.nb; b += NT_AB) hist[b] = 0;
+    const uint32_t nb1 = kp.nb1, nb = kp.nb;
+    for (uint32_t b = tid; b < nb; b += NT_B) fhist[b] = 0;
+    if (tid < (int)nb1) {
+        cnt1[tid] = 0;
+        lim1[tid] = end1[file * nb1 + tid];
+    }
     __syncthreads();
     const uint64_t start = (uint64_t)blockIdx.x * st_pos;
     const uint64_t end = start + st_pos < n ? start + st_pos : n;
-    uint32_t cnt = 0;
-    for (uint64_t t0 = start; t0 < end; t0 += TILE_POS) {
-        const uint64_t p0 = t0 + (uint64_t)tid * P_AB;
-        scan_count_windows<P_AB>(s, n, p0, kp.k, kp.mask, kp.sh, [&](uint64_t canon, int) {
-            const uint64_t h = mix_fwd(canon, kp.mix);
-            atomicAdd(&hist[bucket_of(h, kp)], 1u);
-            ++cnt;
-        });
+    uint32_t inst = 0;
+    bool ovf = false;
+    for (uint64_t t0 = start; t0 < end; t0 += TP_B) {
+        const uint64_t p0 = t0 + (uint64_t)tid * P_B;
+        Frame<P_B> f;
+        const uint64_t v64 = load_frame<P_B, false>(pk, vd, PAD_WORDS + p0 / 16 - 2, kp.k, f);
+        const uint32_t wm = (uint32_t)(runs_of(v64, kp.k) >> 32);   // bit j: window at p0+j valid
+        uint32_t dd[P_B], rk[P_B];
+        E1 ee[P_B];
+#pragma unroll
+        for (int j = 0; j < P_B; ++j) {
+            const uint64_t h = mix_fwd(frame_canon<P_B>(f, j, kp.mask), kp.mix);
+            dd[j] = region_of(h, kp);
+            ee[j] = (E1)(h & kp.r1mask);
+            rk[j] = 0;
+            if ((wm >> j) & 1u) {
+                rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
+                atomicAdd(&fhist[bucket_of(h, kp)], 1u);
+            }
+        }
+        inst += __popc(wm);
+        __syncthreads();
+        if (tid < 64) {   // one wave: scan the <= 64 region counts, reserve global space
+            const uint32_t c = tid < (int)nb1 ? cnt1[tid] : 0u;
+            const uint32_t inc = wave_incl_scan(c, tid);
+            if (tid < (int)nb1) {
+                off1[tid] = inc - c;
+                base1[tid] = c ? atomicAdd(&cursor1[file * nb1 + tid], (unsigned long long)c) : 0ull;
+                cnt1[tid] = 0;
+            }
+            if (tid == 63) off1[nb1] = inc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < P_B; ++j)
+            if ((wm >> j) & 1u) {
+                const uint32_t pos = off1[dd[j]] + rk[j];
+                stage[pos] = ee[j];
+                sd1[pos] = (uint8_t)dd[j];
+            }
+        __syncthreads();
+        const uint32_t tot = off1[nb1];
+        for (uint32_t i = tid; i < tot; i += NT_B) {
+            const uint32_t d = sd1[i];
+            const unsigned long long g = base1[d] + (i - off1[d]);
+            if (g < lim1[d]) out1[g] = stage[i];
+            else ovf = true;
+        }
+        __syncthreads();
+    }
+    for (uint32_t b = tid; b < nb; b += NT_B) {
+        const uint32_t v = fhist[b];
+        if (v) atomicAdd(&fine_hist[(uint64_t)b * F + file], (unsigned long long)v);
     }
     uint32_t tot;
-    (void)block_excl_scan<NT_AB>(cnt, ws, &tot);
-    if (tid == 0 && tot) atomicAdd(instances, (unsigned long long)tot);
-    uint32_t* row = st_hist + (uint64_t)(st0 + blockIdx.x) * kp.nb;
-    for (uint32_t b = tid; b < kp.nb; b += NT_AB) row[b] = hist[b];
+    (void)block_excl_scan<NT_B>(inst, ws, &tot);
+    if (tid == 0 && tot) atomicAdd(&gstat[4], (unsigned long long)tot);
+    if (__any(ovf) && (tid & 63) == 0) atomicOr(&gstat[2], 4ull);
 }
 
-// ---------------------------------------------------------------- scans
-// In place: st_hist[st][b] -> exclusive prefix over st; row n_st receives the totals.
-__global__ void kc_scan_cols(uint32_t* __restrict__ st, uint32_t n_st, uint32_t nb) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    uint32_t run = 0;
-    uint32_t i = 0;
-    for (; i + 4 <= n_st; i += 4) {
-        const uint32_t v0 = st[(uint64_t)(i + 0) * nb + b], v1 = st[(uint64_t)(i + 1) * nb + b];
-        const uint32_t v2 = st[(uint64_t)(i + 2) * nb + b], v3 = st[(uint64_t)(i + 3) * nb + b];
-        st[(uint64_t)(i + 0) * nb + b] = run; run += v0;
-        st[(uint64_t)(i + 1) * nb + b] = run; run += v1;
-        st[(uint64_t)(i + 2) * nb + b] = run; run += v2;
-        st[(uint64_t)(i + 3) * nb + b] = run; run += v3;
-    }
-    for (; i < n_st; ++i) {
-        const uint32_t v = st[(uint64_t)i * nb + b];
-        st[(uint64_t)i * nb + b] = run;
-        run += v;
-    }
-    st[(uint64_t)n_st * nb + b] = run;
-}
-
-// bucket_base[b] = Σ_{b'<b} totals[b'] (u64), bucket_base[nb] = grand total.
-__global__ void __launch_bounds__(1024) kc_bucket_scan(const uint32_t* __restrict__ totals,
-                                                       uint32_t nb, uint64_t* __restrict__ base) {
+// ---------------------------------------------------------------- layout
+// One workgroup.  fs[b*(F+1)+f] = start of file f's run in fine bucket b (bucket-major,
+// file-minor), fs[b*(F+1)+F] = bucket end; cursor2 = copy of fs (re-bin write cursors).
+// Level-1 regions: sizes, chunk table chunk_start[rg] (exclusive), chunk_start[R] = total.
+__global__ void __launch_bounds__(1024) kc_layout(const unsigned long long* __restrict__ fine_hist,
+                                                  uint32_t nb, uint32_t F, uint64_t* __restrict__ fs,
+                                                  unsigned long long* __restrict__ cursor2,
+                                                  const unsigned long long* __restrict__ cursor1,
+                                                  const uint64_t* __restrict__ start1,
+                                                  const uint64_t* __restrict__ end1, uint32_t R,
+                                                  uint64_t* __restrict__ size1,
+                                                  uint64_t* __restrict__ chunk_start,
+                                                  unsigned long long* __restrict__ gstat) {
     __shared__ uint64_t ws[17];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint64_t v[4], s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t b = tid * 4 + i;
-        v[i] = b < nb ? totals[b] : 0ull;
-        s += v[i];
+    auto block_scan64 = [&](uint64_t v, uint64_t& total) -> uint64_t {
+        const uint64_t inc = wave_incl_scan64(v, lane);
+        if (lane == 63) ws[wave] = inc;
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t t = 0;
+            for (int w = 0; w < 16; ++w) { const uint64_t x = ws[w]; ws[w] = t; t += x; }
+            ws[16] = t;
+        }
+        __syncthreads();
+        const uint64_t r = ws[wave] + inc - v;
+        total = ws[16];
+        __syncthreads();
+        return r;
+    };
+    // fine buckets: linear (b, f) order, 1024 entries per round
+    const uint64_t NF = (uint64_t)nb * F;
+    uint64_t carry = 0;
+    for (uint64_t r0 = 0; r0 < NF; r0 += 1024) {
+        const uint64_t i = r0 + tid;
+        const uint64_t v = i < NF ? fine_hist[i] : 0ull;
+        uint64_t tot;
+        const uint64_t ex = block_scan64(v, tot) + carry;
+        if (i < NF) {
+            const uint64_t b = i / F, f = i % F;
+            fs[b * (F + 1) + f] = ex;
+            cursor2[b * (F + 1) + f] = ex;
+            if (f == F - 1) {
+                fs[b * (F + 1) + F] = ex + v;
+                cursor2[b * (F + 1) + F] = ex + v;
+            }
+        }
+        carry += tot;
     }
-    const uint64_t inc = wave_incl_scan64(s, lane);
-    if (lane == 63) ws[wave] = inc;
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t t = 0;
-        for (int w = 0; w < 16; ++w) { uint64_t x = ws[w]; ws[w] = t; t += x; }
-        ws[16] = t;
+    // level-1 regions
+    uint64_t ccarry = 0;
+    for (uint32_t r0 = 0; r0 < R; r0 += 1024) {
+        const uint32_t rg = r0 + tid;
+        uint64_t chunks = 0;
+        if (rg < R) {
+            const uint64_t used = cursor1[rg] - start1[rg];
+            if (cursor1[rg] > end1[rg]) atomicOr(&gstat[2], 4ull);
+            const uint64_t sz = start1[rg] + used <= end1[rg] ? used : end1[rg] - start1[rg];
+            size1[rg] = sz;
+            chunks = (sz + CH_R - 1) / CH_R;
+        }
+        uint64_t tot;
+        const uint64_t ex = block_scan64(chunks, tot) + ccarry;
+        if (rg < R) chunk_start[rg] = ex;
+        ccarry += tot;
     }
-    __syncthreads();
-    uint64_t run = ws[wave] + inc - s;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t b = tid * 4 + i;
-        if (b < nb) base[b] = run;
-        run += v[i];
-    }
-    if (tid == 0) base[nb] = ws[16];
+    if (tid == 0) chunk_start[R] = ccarry;
 }
 
-// fs[b*(F+1)+f] = start of file f's run inside bucket b; fs[b*(F+1)+F] = bucket end.
-__global__ void kc_file_start(const uint32_t* __restrict__ st_off, const uint64_t* __restrict__ base,
-                              const uint32_t* __restrict__ st_first, uint32_t F, uint32_t nb,
-                              uint64_t* __restrict__ fs) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    for (uint32_t f = 0; f < F; ++f)
-        fs[(uint64_t)b * (F + 1) + f] = base[b] + st_off[(uint64_t)st_first[f] * nb + b];
-    fs[(uint64_t)b * (F + 1) + F] = base[b + 1];
-}
-
-// ---------------------------------------------------------------- pass B
-template <class E, int P, int NT>
-__global__ void __launch_bounds__(NT) kc_bin(const uint8_t* __restrict__ s, uint64_t n,
-                                                uint64_t st_pos, uint32_t st0, KP kp,
-                                                const uint64_t* __restrict__ bucket_base,
-                                                const uint32_t* __restrict__ st_off,
-                                                E* __restrict__ out) {
-    __shared__ uint64_t run[MAX_NB];
-    __shared__ uint32_t off[MAX_NB + 1];
-    __shared__ E stage[P * NT];
-    __shared__ uint16_t sbk[P * NT];
-    __shared__ uint32_t ws[NT / 64 + 1];
+// ---------------------------------------------------------------- pass B2
+template <class E1, class E>
+__global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1,
+                                                 const uint64_t* __restrict__ start1,
+                                                 const uint64_t* __restrict__ size1,
+                                                 const uint64_t* __restrict__ chunk_start, uint32_t R,
+                                                 uint32_t F, KP kp,
+                                                 unsigned long long* __restrict__ cursor2,
+                                                 E* __restrict__ out) {
+    constexpr int IT = CH_R / NT_R;
+    __shared__ uint32_t cnt2[NB1_MAX];
+    __shared__ uint32_t off2[NB1_MAX + 1];
+    __shared__ unsigned long long base2[NB1_MAX];
+    __shared__ E stage[CH_R];
+    __shared__ uint8_t sd2[CH_R];
     const int tid = threadIdx.x;
-    const uint32_t nb = kp.nb;
-    const uint32_t* row = st_off + (uint64_t)(st0 + blockIdx.x) * nb;
-    for (uint32_t b = tid; b < nb; b += NT) {
-        run[b] = bucket_base[b] + row[b];
-        off[b] = 0;
+    const uint64_t id = blockIdx.x;
+    if (id >= chunk_start[R]) return;
+    uint32_t lo = 0, hi = R;   // chunk_start[lo] <= id < chunk_start[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (chunk_start[mid] <= id) lo = mid; else hi = mid;
+    }
+    while (lo + 1 < R && chunk_start[lo + 1] <= id) ++lo;   // skip empty regions
+    const uint32_t rg = lo;
+    const uint32_t file = rg / kp.nb1, d1 = rg % kp.nb1;
+    const uint64_t a = start1[rg] + (id - chunk_start[rg]) * CH_R;
+    const uint64_t e = start1[rg] + size1[rg];
+    const uint32_t nb2 = kp.nb2;
+    if (tid < (int)nb2) cnt2[tid] = 0;
+    __syncthreads();
+    uint32_t dd[IT], rk[IT];
+    E ee[IT];
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const uint64_t i = a + (uint64_t)j * NT_R + tid;
+        const E1 v = i < e ? in1[i] : E1(0);
+        dd[j] = kp.fb2 ? (uint32_t)((uint64_t)v >> kp.rbits) : 0u;
+        ee[j] = (E)((uint64_t)v & kp.rmask);
+        rk[j] = i < e ? atomicAdd(&cnt2[dd[j]], 1u) : 0u;
     }
     __syncthreads();
-    const uint64_t start = (uint64_t)blockIdx.x * st_pos;
-    const uint64_t end = start + st_pos < n ? start + st_pos : n;
-    constexpr uint64_t TP = (uint64_t)P * NT;
-    constexpr int BPT = MAX_NB / NT;   // bins per thread in the scan
-    for (uint64_t t0 = start; t0 < end; t0 += TP) {
-        const uint64_t p0 = t0 + (uint64_t)tid * P;
-        uint32_t bk[P], rk[P];
-        E rr[P];
-        uint32_t vm = 0;
-#pragma unroll
-        for (int j = 0; j < P; ++j) { bk[j] = 0; rr[j] = 0; rk[j] = 0; }
-        scan_count_windows<P>(s, n, p0, kp.k, kp.mask, kp.sh, [&](uint64_t canon, int j) {
-            const uint64_t h = mix_fwd(canon, kp.mix);
-            bk[j] = bucket_of(h, kp);
-            rr[j] = (E)(h & kp.rmask);
-            vm |= 1u << j;
-        });
-#pragma unroll
-        for (int j = 0; j < P; ++j)
-            if ((vm >> j) & 1u) rk[j] = atomicAdd(&off[bk[j]], 1u);
-        __syncthreads();
-        {   // exclusive scan of off[0..nb) in place, off[nb] = tile total
-            uint32_t v[BPT], sm = 0;
-#pragma unroll
-            for (int i = 0; i < BPT; ++i) {
-                const uint32_t b = tid * BPT + i;
-                v[i] = b < nb ? off[b] : 0u;
-                sm += v[i];
-            }
-            uint32_t tot;
-            uint32_t ex = block_excl_scan<NT>(sm, ws, &tot);
-#pragma unroll
-            for (int i = 0; i < BPT; ++i) {
-                const uint32_t b = tid * BPT + i;
-                if (b < nb) off[b] = ex;
-                ex += v[i];
-            }
-            if (tid == 0) off[nb] = tot;
+    if (tid < 64) {
+        const uint32_t c = tid < (int)nb2 ? cnt2[tid] : 0u;
+        const uint32_t inc = wave_incl_scan(c, tid);
+        if (tid < (int)nb2) {
+            off2[tid] = inc - c;
+            const uint64_t b = ((uint64_t)d1 << kp.fb2) | (uint64_t)tid;
+            base2[tid] = c ? atomicAdd(&cursor2[b * (F + 1) + file], (unsigned long long)c) : 0ull;
         }
-        __syncthreads();
+        if (tid == 63) off2[nb2] = inc;
+    }
+    __syncthreads();
 #pragma unroll
-        for (int j = 0; j < P; ++j)
-            if ((vm >> j) & 1u) {
-                const uint32_t pos = off[bk[j]] + rk[j];
-                stage[pos] = rr[j];
-                sbk[pos] = (uint16_t)bk[j];
-            }
-        __syncthreads();
-        const uint32_t tot = off[nb];
-        for (uint32_t i = tid; i < tot; i += NT) {
-            const uint32_t b = sbk[i];
-            out[run[b] + (i - off[b])] = stage[i];
+    for (int j = 0; j < IT; ++j) {
+        const uint64_t i = a + (uint64_t)j * NT_R + tid;
+        if (i < e) {
+            const uint32_t pos = off2[dd[j]] + rk[j];
+            stage[pos] = ee[j];
+            sd2[pos] = (uint8_t)dd[j];
         }
-        __syncthreads();
-        for (uint32_t b = tid; b < nb; b += NT) run[b] += off[b + 1] - off[b];
-        __syncthreads();
-        for (uint32_t b = tid; b < nb; b += NT) off[b] = 0;
-        __syncthreads();
+    }
+    __syncthreads();
+    const uint32_t tot = off2[nb2];
+    for (uint32_t i = tid; i < tot; i += NT_R) {
+        const uint32_t d = sd2[i];
+        out[base2[d] + (i - off2[d])] = stage[i];
     }
 }
 
@@ -271,29 +373,69 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
         for (uint32_t ff = 0; ff < F; ++ff) {
             const uint64_t a = f[ff], e = f[ff + 1];
             uint32_t* cf = cnt + (size_t)ff * T;
-            for (uint64_t i = a + tid; i < e; i += NT_C) {
-                if (*(volatile uint32_t*)&s_ovf) break;
-                const E r = binned[i];
-                if (filt) {
-                    const uint32_t sk = SUBB ? (uint32_t)(r >> (rbits - SUBB)) : 0u;
-                    if (sk < lo || sk >= hi) continue;
+            for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)NT_C * PF_C) {
+                E rv[PF_C];   // PF_C loads in flight per thread
+#pragma unroll
+                for (int q = 0; q < PF_C; ++q) {
+                    const uint64_t i = i0 + (uint64_t)q * NT_C + tid;
+                    rv[q] = i < e ? binned[i] : EMPTY;
                 }
-                uint32_t slot = (uint32_t)r & (T - 1);
-                while (true) {
-                    const E cur = keys[slot];
-                    if (cur == r) { atomicAdd(&cf[slot], 1u); break; }
-                    if (cur == EMPTY) {
-                        const E old = atomicCAS(&keys[slot], EMPTY, r);
-                        if (old == EMPTY) {
-                            const uint32_t o = atomicAdd(&s_occ, 1u);
-                            if (o + 1 >= maxload) s_ovf = 1;
-                            atomicAdd(&cf[slot], 1u);
-                            break;
-                        }
-                        if (old == r) { atomicAdd(&cf[slot], 1u); break; }
+                // 1) all home slots read before any is consumed: one LDS round trip settles
+                //    every element whose key already sits in its home slot (fire-and-forget add)
+                uint32_t miss = 0;
+#pragma unroll
+                for (int q = 0; q < PF_C; ++q) {
+                    bool live = rv[q] != EMPTY;
+                    if (filt && live) {
+                        const uint32_t sk = SUBB ? (uint32_t)(rv[q] >> (rbits - SUBB)) : 0u;
+                        live = sk >= lo && sk < hi;
                     }
-                    slot = (slot + 1) & (T - 1);
+                    const uint32_t sl = (uint32_t)rv[q] & (T - 1);
+                    const E c = keys[sl];
+                    if (live && c == rv[q]) atomicAdd(&cf[sl], 1u);
+                    else if (live) miss |= 1u << q;
                 }
+                // 2) the rest: one probe step per lane per iteration, a lane takes its next
+                //    missed element when the current one is settled
+                E r = EMPTY;
+                uint32_t sl = 0;
+                while (__any(miss != 0u || r != EMPTY)) {
+                    if (r == EMPTY && miss) {
+                        const int q = __builtin_ctz(miss);
+                        miss &= miss - 1u;
+                        E pick = rv[0];
+#pragma unroll
+                        for (int t = 1; t < PF_C; ++t) pick = q == t ? rv[t] : pick;
+                        r = pick;
+                        sl = (uint32_t)r & (T - 1);
+                    }
+                    if (r != EMPTY) {
+                        const E c = keys[sl];
+                        if (c == r) {
+                            atomicAdd(&cf[sl], 1u);
+                            r = EMPTY;
+                        } else if (c == EMPTY) {
+                            if (*(volatile uint32_t*)&s_ovf) {
+                                r = EMPTY;   // this sub-range is redone after the split
+                            } else {
+                                const E old = atomicCAS(&keys[sl], EMPTY, r);
+                                if (old == EMPTY || old == r) {
+                                    if (old == EMPTY) {
+                                        const uint32_t o = atomicAdd(&s_occ, 1u);
+                                        if (o + 1 >= maxload) s_ovf = 1;
+                                    }
+                                    atomicAdd(&cf[sl], 1u);
+                                    r = EMPTY;
+                                } else {
+                                    sl = (sl + 1) & (T - 1);
+                                }
+                            }
+                        } else {
+                            sl = (sl + 1) & (T - 1);
+                        }
+                    }
+                }
+                if (*(volatile uint32_t*)&s_ovf) break;
             }
         }
         __syncthreads();
@@ -400,6 +542,7 @@ __global__ void __launch_bounds__(NT_H) kc_spec_hist(const uint32_t* __restrict_
     }
 }
 
+constexpr int SEL_R = 16;   // rows per thread: one cursor atomic per 4096 rows
 __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ keys,
                                                   const uint32_t* __restrict__ cnt, uint64_t rows,
                                                   uint64_t cap, uint32_t F, int64_t lower,
@@ -408,10 +551,12 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
                                                   unsigned long long* __restrict__ stat) {
     __shared__ uint32_t ws[NT_H / 64 + 1];
     __shared__ unsigned long long s_base;
-    const uint64_t r = (uint64_t)blockIdx.x * NT_H + threadIdx.x;
-    bool take = false, disc = false;
-    uint64_t key = 0;
-    if (r < rows) {
+    const uint64_t base = (uint64_t)blockIdx.x * NT_H * SEL_R;
+    uint32_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
+#pragma unroll
+    for (int q = 0; q < SEL_R; ++q) {
+        const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
+        if (r >= rows) continue;
         int64_t total = 0;
         uint32_t nz = 0;
         for (uint32_t f = 0; f < F; ++f) {
@@ -419,20 +564,28 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
             total += c;
             nz += c > 0;
         }
-        take = lower <= total && total <= upper;
-        disc = take && nz == 1;
-        key = keys[r];
+        if (lower <= total && total <= upper) {
+            take |= 1u << q;
+            if (nz == 1) disc |= 1u << q;
+        }
     }
     uint32_t tot;
-    const uint32_t ex = block_excl_scan<NT_H>(take ? 1u : 0u, ws, &tot);
-    const uint64_t dm = __ballot(disc);
-    if ((threadIdx.x & 63) == 0 && dm) atomicAdd(&stat[1], (unsigned long long)__popcll(dm));
+    const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popc(take), ws, &tot);
+    uint32_t dsum = (uint32_t)__popc(disc);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
+    if ((threadIdx.x & 63) == 0 && dsum) atomicAdd(&stat[1], (unsigned long long)dsum);
     if (threadIdx.x == 0) s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
     __syncthreads();
-    if (take) {
-        out[s_base + ex] = key;
-        out_flag[s_base + ex] = disc ? 1u : 0u;
-    }
+    uint64_t o = s_base + ex;
+#pragma unroll
+    for (int q = 0; q < SEL_R; ++q)
+        if ((take >> q) & 1u) {
+            const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
+            out[o] = keys[r];
+            out_flag[o] = (disc >> q) & 1u;
+            ++o;
+        }
 }
 
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
@@ -509,80 +662,73 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     kp.mask = s.k >= 32 ? ~0ull : ((1ull << (2 * s.k)) - 1);
     kp.mix = make_mix(s.k);
     const uint32_t nbits = 2u * (uint32_t)s.k;
-    // fan-out: ~16K windows per bucket, at most 4096 buckets, never more bits than the key
-    uint32_t fb = 0;
-    while (fb < (uint32_t)MAX_FB && fb < nbits && (total_bytes >> fb) > 16384) ++fb;
+    // fan-out: ~16K windows per fine bucket, at most 4096 buckets, never more bits than the key
+    uint32_t fb = 0, fb_max = MAX_FB;
+    if (const char* e = std::getenv("HGA_FB_MAX")) fb_max = std::min<uint32_t>(MAX_FB, (uint32_t)std::atoi(e));
+    while (fb < fb_max && fb < nbits && (total_bytes >> fb) > 16384) ++fb;
     kp.fb = fb;
     kp.nb = 1u << fb;
     kp.rbits = nbits - fb;
     kp.rmask = kp.rbits >= 64 ? ~0ull : ((1ull << kp.rbits) - 1);
+    kp.fb1 = std::min<uint32_t>(fb, MAX_FB1);
+    kp.nb1 = 1u << kp.fb1;
+    kp.r1bits = nbits - kp.fb1;
+    kp.r1mask = kp.r1bits >= 64 ? ~0ull : ((1ull << kp.r1bits) - 1);
+    kp.fb2 = fb - kp.fb1;
+    kp.nb2 = 1u << kp.fb2;
+    const bool e1_32 = kp.r1bits <= 32;
     const bool e32 = kp.rbits <= 31;
     s.fb = fb;
     s.buckets = kp.nb;
+    const uint32_t nb = kp.nb, nb1 = kp.nb1, R = F * nb1;
 
-    // super-tiles: ~4 per CU over all files, a multiple of the tile
+    // super-tiles: ~4 per CU over all files, whole tiles
     uint64_t st_pos = total_bytes / ((uint64_t)c->num_cu * 4) + 1;
-    st_pos = std::max<uint64_t>(TILE_POS, (st_pos + TILE_POS - 1) / TILE_POS * TILE_POS);
-    std::vector<uint32_t> st_first(F + 1, 0), n_st(F, 0);
-    for (uint32_t f = 0; f < F; ++f) {
-        n_st[f] = (uint32_t)((s.seq_len[f] + st_pos - 1) / st_pos);
-        st_first[f + 1] = st_first[f] + n_st[f];
-    }
-    const uint32_t n_st_tot = st_first[F];
-    const uint32_t nb = kp.nb;
+    st_pos = std::max<uint64_t>(ST_ALIGN, (st_pos + ST_ALIGN - 1) / ST_ALIGN * ST_ALIGN);
+    std::vector<uint32_t> n_st(F, 0);
+    for (uint32_t f = 0; f < F; ++f) n_st[f] = (uint32_t)((s.seq_len[f] + st_pos - 1) / st_pos);
 
-    uint32_t* st_hist = static_cast<uint32_t*>(s.st_hist.ensure((size_t)(n_st_tot + 1) * nb * 4));
-    uint64_t* bucket_base = static_cast<uint64_t*>(s.bucket_base.ensure((size_t)(nb + 1) * 8));
-    uint64_t* fs = static_cast<uint64_t*>(s.file_start.ensure((size_t)nb * (F + 1) * 8));
-    uint32_t* d_st_first = static_cast<uint32_t*>(s.misc.ensure((F + 1) * 4 + 256));
+    // level-1 regions (file f, digit d): estimated capacity, or the exact sizes a previous
+    // overflowing attempt measured
     auto* gstat = static_cast<unsigned long long*>(s.cursor.ensure(8 * 8));
-    HGA_HIP(hipMemcpyAsync(d_st_first, st_first.data(), (F + 1) * 4, hipMemcpyHostToDevice, c->stream));
-    HGA_HIP(hipMemsetAsync(gstat, 0, 8 * 8, c->stream));
-    if (n_st_tot == 0) HGA_HIP(hipMemsetAsync(st_hist, 0, (size_t)nb * 4, c->stream));
+    uint64_t* fs = static_cast<uint64_t*>(s.file_start.ensure((size_t)nb * (F + 1) * 8));
+    auto* cursor2 = static_cast<unsigned long long*>(s.cursor2.ensure((size_t)nb * (F + 1) * 8));
+    auto* fine_hist = static_cast<unsigned long long*>(s.fine_hist.ensure((size_t)nb * F * 8));
+    char* rgb = static_cast<char*>(s.regions.ensure((size_t)(R + 1) * 8 * 5 + 256));
+    uint64_t* d_start1 = reinterpret_cast<uint64_t*>(rgb);
+    uint64_t* d_end1 = d_start1 + (R + 1);
+    auto* cursor1 = reinterpret_cast<unsigned long long*>(d_end1 + (R + 1));
+    uint64_t* size1 = reinterpret_cast<uint64_t*>(cursor1 + (R + 1));
+    uint64_t* chunk_start = size1 + (R + 1);
 
-    // A: per-super-tile bucket histograms + instance count (gstat[4])
+    // P: pack every file (2-bit codes + valid bits), pad words zeroed (= invalid)
+    std::vector<const uint32_t*> pks(F);
+    std::vector<const uint16_t*> vds(F);
+    const uint64_t tail_words = ST_ALIGN / 16 + 8;
+    while (s.packed.size() < F) { s.packed.push_back(new DevBuf()); s.valid.push_back(new DevBuf()); }
     for (uint32_t f = 0; f < F; ++f) {
-        if (!n_st[f]) continue;
-        const uint8_t* sp = s.seq[f]->as<uint8_t>();
         const uint64_t n = s.seq_len[f];
-        c->launch("kc_hist", [&] {
-            hipLaunchKernelGGL(kc_hist, dim3(n_st[f]), dim3(NT_AB), 0, c->stream, sp, n, st_pos,
-                               st_first[f], kp, st_hist, gstat + 4);
-        });
-        c->check_launch("kc_hist");
-    }
-    // S: offsets
-    c->launch("kc_scan", [&] {
-        hipLaunchKernelGGL(kc_scan_cols, dim3(blocks_for(nb, 256)), dim3(256), 0, c->stream,
-                           st_hist, n_st_tot, nb);
-        hipLaunchKernelGGL(kc_bucket_scan, dim3(1), dim3(1024), 0, c->stream,
-                           st_hist + (size_t)n_st_tot * nb, nb, bucket_base);
-        hipLaunchKernelGGL(kc_file_start, dim3(blocks_for(nb, 256)), dim3(256), 0, c->stream,
-                           st_hist, bucket_base, d_st_first, F, nb, fs);
-    });
-    c->check_launch("kc_scan");
-
-    // B: bin (capacity bound = bytes; instances <= bytes)
-    const size_t esz = e32 ? 4 : 8;
-    void* binned = s.binned.ensure(std::max<size_t>(total_bytes, 1) * esz);
-    for (uint32_t f = 0; f < F; ++f) {
-        if (!n_st[f]) continue;
-        const uint8_t* sp = s.seq[f]->as<uint8_t>();
-        const uint64_t n = s.seq_len[f];
-        c->launch("kc_bin", [&] {
-            if (e32)
-                hipLaunchKernelGGL((kc_bin<uint32_t, P_AB, NT_AB>), dim3(n_st[f]), dim3(NT_AB), 0, c->stream,
-                                   sp, n, st_pos, st_first[f], kp, bucket_base, st_hist,
-                                   static_cast<uint32_t*>(binned));
-            else
-                hipLaunchKernelGGL((kc_bin<uint64_t, P_AB, NT_B64>), dim3(n_st[f]), dim3(NT_B64), 0,
-                                   c->stream, sp, n, st_pos, st_first[f], kp, bucket_base, st_hist,
-                                   static_cast<uint64_t*>(binned));
-        });
-        c->check_launch("kc_bin");
+        const uint64_t nw = (n + 15) / 16;
+        const uint64_t alloc = PAD_WORDS + nw + tail_words;
+        uint32_t* pk = static_cast<uint32_t*>(s.packed[f]->ensure(alloc * 4));
+        uint16_t* vd = static_cast<uint16_t*>(s.valid[f]->ensure(alloc * 2));
+        HGA_HIP(hipMemsetAsync(vd, 0, PAD_WORDS * 2, c->stream));
+        HGA_HIP(hipMemsetAsync(vd + PAD_WORDS + nw, 0, tail_words * 2, c->stream));
+        HGA_HIP(hipMemsetAsync(pk, 0, PAD_WORDS * 4, c->stream));
+        HGA_HIP(hipMemsetAsync(pk + PAD_WORDS + nw, 0, tail_words * 4, c->stream));
+        if (nw) {
+            const uint8_t* sp = s.seq[f]->as<uint8_t>();
+            c->launch("kc_pack", [&] {
+                hipLaunchKernelGGL(kc_pack<false>, dim3(blocks_for(nw, 256)), dim3(256), 0, c->stream, sp, n,
+                                   pk, vd, nw);
+            });
+            c->check_launch("kc_pack");
+        }
+        pks[f] = pk;
+        vds[f] = vd;
     }
 
-    // C: per-bucket count
+    const size_t esz1 = e1_32 ? 4 : 8, esz = e32 ? 4 : 8;
     const uint64_t cap = total_bytes / std::max<uint32_t>(1, min_per_file) + 1;
     s.rows_key.ensure(cap * 8);
     s.rows_cnt.ensure(cap * 4 * F);
@@ -590,21 +736,93 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     uint32_t T = 1;
     while ((uint64_t)T * 2 * slot_b <= LDS_TAB) T *= 2;
     HGA_REQUIRE(T >= 2 * NT_C, HGA_ERR_INVALID, "too many files for the LDS table");
-    uint32_t maxload = std::min<uint32_t>((uint32_t)(T * 0.8), T - NT_C - 8);
-    c->launch("kc_count", [&] {
-        if (e32)
-            hipLaunchKernelGGL(kc_count<uint32_t>, dim3(nb), dim3(NT_C), 0, c->stream,
-                               static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file,
-                               kp, s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
-        else
-            hipLaunchKernelGGL(kc_count<uint64_t>, dim3(nb), dim3(NT_C), 0, c->stream,
-                               static_cast<const uint64_t*>(binned), fs, F, T, maxload, min_per_file,
-                               kp, s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
-    });
-    c->check_launch("kc_count");
+    const uint32_t maxload = std::min<uint32_t>((uint32_t)(T * 0.8), T - NT_C - 8);
+    void* binned = s.binned.ensure(std::max<size_t>(total_bytes, 1) * esz);
+
     unsigned long long h_stat[8];
-    HGA_HIP(hipMemcpyAsync(h_stat, gstat, sizeof(h_stat), hipMemcpyDeviceToHost, c->stream));
-    c->sync();
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        std::vector<uint64_t> start1(R + 1), end1(R + 1);
+        uint64_t at = 0;
+        for (uint32_t f = 0; f < F; ++f)
+            for (uint32_t d = 0; d < nb1; ++d) {
+                const uint32_t rg = f * nb1 + d;
+                const uint64_t capr = attempt == 0 || s.l1_exact.size() != R
+                                          ? s.seq_len[f] / nb1 + s.seq_len[f] / (8 * nb1) + 16384
+                                          : s.l1_exact[rg];
+                start1[rg] = at;
+                end1[rg] = at + capr;
+                at += (capr + 63) / 64 * 64;
+            }
+        start1[R] = end1[R] = at;
+        const uint64_t l1_elems = at;
+        void* binned1 = s.binned1.ensure(std::max<uint64_t>(l1_elems, 1) * esz1);
+        HGA_HIP(hipMemcpyAsync(d_start1, start1.data(), (R + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        HGA_HIP(hipMemcpyAsync(d_end1, end1.data(), (R + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        HGA_HIP(hipMemcpyAsync(cursor1, start1.data(), (R + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        HGA_HIP(hipMemsetAsync(gstat, 0, 8 * 8, c->stream));
+        HGA_HIP(hipMemsetAsync(fine_hist, 0, (size_t)nb * F * 8, c->stream));
+
+        // B1: level-1 binning + fine histogram + instance count
+        for (uint32_t f = 0; f < F; ++f) {
+            if (!n_st[f]) continue;
+            const uint64_t n = s.seq_len[f];
+            c->launch("kc_bin1", [&] {
+                if (e1_32)
+                    hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f],
+                                       n, st_pos, f, F, kp, cursor1, d_end1, static_cast<uint32_t*>(binned1),
+                                       fine_hist, gstat);
+                else
+                    hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f],
+                                       n, st_pos, f, F, kp, cursor1, d_end1, static_cast<uint64_t*>(binned1),
+                                       fine_hist, gstat);
+            });
+            c->check_launch("kc_bin1");
+        }
+        // L: fine layout + level-1 chunk table
+        c->launch("kc_layout", [&] {
+            hipLaunchKernelGGL(kc_layout, dim3(1), dim3(1024), 0, c->stream, fine_hist, nb, F, fs, cursor2,
+                               cursor1, d_start1, d_end1, R, size1, chunk_start, gstat);
+        });
+        c->check_launch("kc_layout");
+        // B2: re-bin every level-1 region into the fine buckets
+        uint64_t max_chunks = 0;
+        for (uint32_t rg = 0; rg < R; ++rg) max_chunks += (end1[rg] - start1[rg] + CH_R - 1) / CH_R;
+        if (max_chunks) {
+            c->launch("kc_rebin", [&] {
+#define HGA_REBIN(E1T, ET)                                                                                 \
+    hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3((unsigned)max_chunks), dim3(NT_R), 0, c->stream,          \
+                       static_cast<const E1T*>(binned1), d_start1, size1, chunk_start, R, F, kp, cursor2, \
+                       static_cast<ET*>(binned))
+                if (e1_32 && e32) HGA_REBIN(uint32_t, uint32_t);
+                else if (e32) HGA_REBIN(uint64_t, uint32_t);
+                else if (e1_32) HGA_REBIN(uint32_t, uint64_t);
+                else HGA_REBIN(uint64_t, uint64_t);
+#undef HGA_REBIN
+            });
+            c->check_launch("kc_rebin");
+        }
+        // C: per-bucket count
+        c->launch("kc_count", [&] {
+            if (e32)
+                hipLaunchKernelGGL(kc_count<uint32_t>, dim3(nb), dim3(NT_C), 0, c->stream,
+                                   static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
+                                   s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+            else
+                hipLaunchKernelGGL(kc_count<uint64_t>, dim3(nb), dim3(NT_C), 0, c->stream,
+                                   static_cast<const uint64_t*>(binned), fs, F, T, maxload, min_per_file, kp,
+                                   s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+        });
+        c->check_launch("kc_count");
+        HGA_HIP(hipMemcpyAsync(h_stat, gstat, sizeof(h_stat), hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        if (!(h_stat[2] & 4ull)) break;
+        // a level-1 region overflowed its estimate: the cursors hold the exact sizes
+        HGA_REQUIRE(attempt == 0, HGA_ERR_INVALID, "level-1 region overflow with exact capacities");
+        std::vector<unsigned long long> cur(R);
+        HGA_HIP(hipMemcpy(cur.data(), cursor1, R * 8, hipMemcpyDeviceToHost));
+        s.l1_exact.assign(R, 0);
+        for (uint32_t rg = 0; rg < R; ++rg) s.l1_exact[rg] = cur[rg] - start1[rg];
+    }
     HGA_REQUIRE(!(h_stat[2] & 1ull), HGA_ERR_INVALID, "a bucket could not be split to fit the LDS table");
     HGA_REQUIRE(!(h_stat[2] & 2ull), HGA_ERR_OOM, "row capacity exceeded");
     s.rows = h_stat[0];
@@ -679,7 +897,7 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     HGA_HIP(hipMemsetAsync(stat, 0, 16, c->stream));
     if (s.rows) {
         c->launch("kc_select", [&] {
-            hipLaunchKernelGGL(kc_select, dim3(blocks_for(s.rows, NT_H)), dim3(NT_H), 0, c->stream,
+            hipLaunchKernelGGL(kc_select, dim3(blocks_for(s.rows, NT_H * SEL_R)), dim3(NT_H), 0, c->stream,
                                s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), s.rows,
                                s.rows_cap, s.n_files, lower, upper, out, flag, stat);
         });

@@ -15,9 +15,10 @@
 
 namespace hga {
 
-// Bijective mix on n = 2k bits (all arithmetic mod 2^n).  The xor-shift uses
-// s = ceil(n/2) so it is its own inverse; the multipliers are odd so they invert
-// mod 2^n.  Buckets take the top bits of the mixed value, LDS slots the low bits.
+// Bijective mix on n = 2k bits (arithmetic mod 2^n): multiply by an odd constant (the
+// top bits then depend on every key bit), then xor the top half into the bottom half
+// (s = ceil(n/2), so the xor-shift is its own inverse).  Buckets take the top bits of
+// the mixed value, LDS table slots the low bits.
 struct Mix {
     uint64_t mask, c1, c2, c1i, c2i;
     uint32_t n, s;
@@ -25,17 +26,11 @@ struct Mix {
 
 __host__ __device__ inline uint64_t mix_fwd(uint64_t x, const Mix& m) {
     x = (x * m.c1) & m.mask;
-    x ^= x >> m.s;
-    x = (x * m.c2) & m.mask;
-    x ^= x >> m.s;
-    return x;
+    return x ^ (x >> m.s);
 }
 __host__ __device__ inline uint64_t mix_inv(uint64_t h, const Mix& m) {
     h ^= h >> m.s;
-    h = (h * m.c2i) & m.mask;
-    h ^= h >> m.s;
-    h = (h * m.c1i) & m.mask;
-    return h;
+    return (h * m.c1i) & m.mask;
 }
 
 inline uint64_t inv_odd_u64(uint64_t a) {  // a * x == 1 mod 2^64 (Newton)
@@ -87,30 +82,104 @@ __device__ __forceinline__ uint4 load16(const uint8_t* s, int64_t base, uint64_t
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Counting-semantics scan of the P window-ends [p0, p0+P) (p0 % 16 == 0, P % 16 == 0).
-// Rolls the 32 preceding bytes as halo (k <= 32), then calls f(canonical, j) for
-// every j in [0,P) whose window [p0+j-k+1, p0+j] consists of bases only.  Fully
-// unrolled so per-position state stays in registers.
-template <int P, class F>
-__device__ __forceinline__ void scan_count_windows(const uint8_t* s, uint64_t n, uint64_t p0,
-                                                   int k, uint64_t mask, int sh, F&& f) {
-    static_assert(P % 16 == 0 && P > 0, "P must be a positive multiple of 16");
-    uint64_t fwd = 0, rc = 0;
-    int run = 0;
+// ---------------------------------------------------------------- packed frames (K1/K2)
+// The sequence stream is packed once (kc_pack / lk_pack): per 16 bases one u32 of 2-bit
+// codes (first base in the top bits) and one u16 of base-valid bits (bit b = base b).
+// Two leading pad words (all invalid) let every frame read two words before its start.
+constexpr int PAD_WORDS = 2;
+
+// Reverse the order of the 16 2-bit groups of a word.
+__device__ __forceinline__ uint32_t rev2(uint32_t x) {
+    const uint32_t y = __builtin_bitreverse32(x);
+    return ((y >> 1) & 0x55555555u) | ((y & 0x55555555u) << 1);
+}
+
+// Base-valid bits of one word expanded to the 2-bit code positions (base b -> bits 31-2b, 30-2b).
+__device__ __forceinline__ uint32_t expand2(uint32_t v16) {
+    uint32_t x = __builtin_bitreverse32(v16) >> 16;   // base b -> bit 15-b
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x | (x << 1);
+}
+
+// Bit e of the result is set iff bits [e-len+1, e] of v are all set (len in [1, 64]).
+__device__ __forceinline__ uint64_t runs_of(uint64_t v, int len) {
+    uint64_t p[7];
+    p[0] = v;
 #pragma unroll
-    for (int c = -2; c < P / 16; ++c) {
-        const uint4 v = load16(s, (int64_t)p0 + 16 * c, n);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int b = 1; b < 7; ++b) p[b] = p[b - 1] & (p[b - 1] << (1 << (b - 1)));
+    uint64_t w = ~0ull;
+    int off = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            bool ok;
-            const uint32_t code = jf_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu, ok);
-            fwd = ((fwd << 2) | code) & mask;
-            rc = (rc >> 2) | ((uint64_t)(3u - code) << sh);
-            run = ok ? run + 1 : 0;
-            if (c >= 0 && run >= k) f(fwd < rc ? fwd : rc, 16 * c + j);
+    for (int b = 6; b >= 0; --b)
+        if (len & (1 << b)) {
+            w &= p[b] << off;
+            off += 1 << b;
         }
+    return w;
+}
+
+// 64-bit field of an NW-word big-endian bit string starting at bit `sh` from the bottom
+// (sh a compile-time constant after unrolling -> two alignbit instructions).
+template <int NW>
+__device__ __forceinline__ uint64_t field64(const uint32_t (&x)[NW], int sh) {
+    const int wb = sh >> 5, b = sh & 31;
+    const int i0 = NW - 1 - wb, i1 = NW - 2 - wb, i2 = NW - 3 - wb;
+    const uint32_t a0 = i0 >= 0 ? x[i0] : 0u, a1 = i1 >= 0 ? x[i1] : 0u, a2 = i2 >= 0 ? x[i2] : 0u;
+    const uint32_t lo = __builtin_amdgcn_alignbit(a1, a0, b);
+    const uint32_t hi = __builtin_amdgcn_alignbit(a2, a1, b);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Per-thread frame of P window ends [p0, p0+P): bases [p0-32, p0+P) as NW words of the
+// forward codes, the matching reverse-complement string pre-shifted so that the rc code of
+// the window ending at p0+j is field64(r, 2j), and the valid-window bits.
+template <int P>
+struct Frame {
+    static constexpr int NW = 2 + P / 16;
+    uint32_t x[NW];
+    uint32_t r[NW];
+};
+
+// REF = KmerIterator semantics (non-bases contribute 0 to both strands); otherwise the
+// counting semantics (a window with a non-base is never used, so rc = revcomp(fwd)).
+// w0 = index (with padding) of the frame's first word.  Returns the frame's valid bits.
+template <int P, bool REF>
+__device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
+                                               const uint16_t* __restrict__ vd, uint64_t w0, int k,
+                                               Frame<P>& f) {
+    constexpr int NW = Frame<P>::NW;
+    uint64_t v64 = 0;
+    uint32_t vw[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        f.x[i] = pk[w0 + i];
+        vw[i] = vd[w0 + i];
+        v64 |= (uint64_t)vw[i] << (16 * i);
     }
+    uint32_t R[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        uint32_t c = ~f.x[NW - 1 - i];
+        if (REF) c &= expand2(vw[NW - 1 - i]);
+        R[i] = rev2(c);
+    }
+    // f.r = R >> (66 - 2k)   (v in [2, 64]; a and b are uniform across the wave)
+    const int v = 66 - 2 * k;
+    const int a = v >> 5, b = v & 31;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {        // i counts words from the bottom
+        const uint32_t c0 = i < NW ? R[NW - 1 - i] : 0u;
+        const uint32_t c1 = i + 1 < NW ? R[NW - 2 - i] : 0u;
+        const uint32_t c2 = i + 2 < NW ? R[NW - 3 - i] : 0u;
+        const uint32_t c3 = i + 3 < NW ? R[NW - 4 - i] : 0u;
+        const uint32_t lo = a == 0 ? c0 : (a == 1 ? c1 : c2);
+        const uint32_t hi = a == 0 ? c1 : (a == 1 ? c2 : c3);
+        f.r[NW - 1 - i] = __builtin_amdgcn_alignbit(hi, lo, b);
+    }
+    return v64;
 }
 
 // Wave / block scans (wave64).

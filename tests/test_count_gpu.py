@@ -157,3 +157,12 @@ def test_count_conservation_large(gpu_ctx, hga_mod):
     keys, counts = gpu_ctx.rows()
     assert int(counts.sum()) == st.instances
     assert np.all(np.diff(keys.astype(np.int64)) > 0)
+
+
+def test_count_level1_overflow_retry(gpu_ctx, hga_mod):
+    # one k-mer dominating the input overflows its estimated level-1 region; the run must
+    # detect it and redo the binning with the exact region sizes
+    g = hga_mod.gen_genome(400_000, 5)
+    streams = [b"A" * 3_000_000 + b"\n" + g, b"C" * 1_000_000 + b"\n" + g[:200_000]]
+    o = oracle.count_pipeline(streams, 21, 1, 10 ** 9, min_count=1)
+    assert_same(run_gpu(gpu_ctx, streams, 21, 1, 10 ** 9, min_count=1), o)

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSV passes (one directory per pass) per kernel.
+
+    python tools/pmc_summary.py gpurun_out/pmc4_*      [--json out.json]
+
+FETCH_SIZE / WRITE_SIZE are reported in KB by rocprofv3.  Per MI355X_MICROARCH.md §HBM,
+FETCH_SIZE reads ½ of the bytes of wide coalesced streaming reads on gfx950, so the HBM-read
+estimate doubles it ("read_bytes_corr"); WRITE_SIZE is exact for 16-B streaming stores.
+"""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+
+def kname(full):
+    m = re.search(r"\b((?:kc|lk|rs|sc)_[A-Za-z0-9_]+)(<[^>]*>)?", full)
+    return (m.group(1) + (m.group(2) or "")) if m else full.split("(")[0][:40]
+
+
+def main(dirs, out=None):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    for d in dirs:
+        for f in glob.glob(f"{d}/*counter_collection.csv"):
+            for r in csv.DictReader(open(f)):
+                k = kname(r["Kernel_Name"])
+                agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for f in glob.glob(f"{d}/*kernel_trace.csv"):
+            for r in csv.DictReader(open(f)):
+                k = kname(r["Kernel_Name"])
+                dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    cols = ["FETCH_SIZE", "WRITE_SIZE", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+            "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"]
+    res = {}
+    print("kernel".ljust(26), "ms(med)".rjust(8), *[c.replace("SQ_", "")[:10].rjust(11) for c in cols])
+    for k in sorted(agg):
+        if k.startswith("__amd"):
+            continue
+        ds = sorted(dur.get(k, [0.0]))
+        med = ds[len(ds) // 2]
+        row = {c: (sum(v) / len(v) if v else 0.0) for c, v in ((c, agg[k].get(c, [])) for c in cols)}
+        row["ms_median"] = med
+        row["dispatches"] = len(ds)
+        row["read_bytes_corr"] = 2 * row["FETCH_SIZE"] * 1024
+        row["write_bytes"] = row["WRITE_SIZE"] * 1024
+        res[k] = row
+        print(k[:26].ljust(26), f"{med:8.3f}", *[f"{row[c]:11.3g}" for c in cols])
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    if out in args:
+        args.remove(out)
+    main(args, out)
