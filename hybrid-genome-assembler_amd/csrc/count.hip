@@ -62,30 +62,6 @@ __device__ __forceinline__ uint32_t region_of(uint64_t h, const KP& kp) {
     return kp.fb1 ? (uint32_t)(h >> kp.r1bits) : 0u;
 }
 
-// ---------------------------------------------------------------- pass P
-// One thread per 16 bases: packed codes (first base in bits 31:30) and valid bits.
-template <bool REF>
-__global__ void kc_pack(const uint8_t* __restrict__ s, uint64_t n, uint32_t* __restrict__ pk,
-                        uint16_t* __restrict__ vd, uint64_t nw) {
-    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nw) return;
-    const uint4 v = load16(s, (int64_t)(w * 16), n);
-    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-    uint32_t code = 0, valid = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t b = (ws[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-        const uint32_t u = REF ? b : (b & 0xDFu);
-        const uint32_t d = u - 0x41u;
-        const bool ok = d < 20u && ((kBaseBits >> d) & 1u);
-        const uint32_t c = ok ? (((u >> 1) ^ (u >> 2)) & 3u) : 0u;
-        code |= c << (30 - 2 * j);
-        valid |= (ok ? 1u : 0u) << j;
-    }
-    pk[PAD_WORDS + w] = code;
-    vd[PAD_WORDS + w] = (uint16_t)valid;
-}
-
 // Canonical code of the window ending at p0+j, from a loaded frame.
 template <int P>
 __device__ __forceinline__ uint64_t frame_canon(const Frame<P>& f, int j, uint64_t mask) {
@@ -96,21 +72,54 @@ __device__ __forceinline__ uint64_t frame_canon(const Frame<P>& f, int j, uint64
 }
 
 // ---------------------------------------------------------------- pass B1
+// LDS-only barrier: waits for this wave's LDS traffic, not for its global loads, so a
+// prefetch issued before it stays in flight (a __syncthreads() would drain vmcnt too).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Level-1 blocks: every workgroup takes BLK-element blocks per region from one pool with a
+// single atomic (and a new one only when a block fills), so a tile's region runs are
+// written without any global atomic.  block table entry: start, used, file<<8 | region.
+struct Blk {
+    unsigned long long start;
+    uint32_t used;
+    uint32_t tag;
+};
+constexpr uint32_t BLK = TP_B;   // >= a tile, so a tile's run spans at most two blocks
+
 // gstat: [0] row cursor, [1] max split, [2] error bits (1 unsplittable, 2 row capacity,
-// 4 level-1 region overflow), [4] instances.
+// 4 level-1 pool exhausted), [3] blocks used, [4] instances, [5] pool cursor.
+__device__ __forceinline__ uint32_t new_block(unsigned long long* gstat, Blk* table, uint64_t table_cap,
+                                              uint64_t pool_cap, uint32_t tag, unsigned long long& start) {
+    start = atomicAdd(&gstat[5], (unsigned long long)BLK);
+    const unsigned long long e = atomicAdd(&gstat[3], 1ull);
+    if (start + BLK > pool_cap || e >= table_cap) {
+        atomicOr(&gstat[2], 4ull);
+        start = pool_cap;   // writes into this block are dropped
+        return 0xFFFFFFFFu;
+    }
+    table[e].start = start;
+    table[e].used = 0;
+    table[e].tag = tag;
+    return (uint32_t)e;
+}
+
 template <class E1>
 __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
                                                 const uint16_t* __restrict__ vd, uint64_t n,
                                                 uint64_t st_pos, uint32_t file, uint32_t F, KP kp,
-                                                unsigned long long* __restrict__ cursor1,
-                                                const uint64_t* __restrict__ end1,
-                                                E1* __restrict__ out1,
+                                                Blk* __restrict__ table, uint64_t table_cap,
+                                                uint64_t pool_cap, E1* __restrict__ out1,
                                                 unsigned long long* __restrict__ fine_hist,
                                                 unsigned long long* __restrict__ gstat) {
     __shared__ uint32_t cnt1[NB1_MAX];
     __shared__ uint32_t off1[NB1_MAX + 1];
-    __shared__ unsigned long long base1[NB1_MAX];
-    __shared__ unsigned long long lim1[NB1_MAX];
+    __shared__ unsigned long long bstart[NB1_MAX];   // current block of each region
+    __shared__ uint32_t bfill[NB1_MAX];              // elements already in it
+    __shared__ uint32_t bent[NB1_MAX];               // its table entry
+    __shared__ unsigned long long base_a[NB1_MAX], base_b[NB1_MAX];
+    __shared__ uint32_t take_a[NB1_MAX];
     __shared__ uint32_t fhist[MAX_NB];
     __shared__ E1 stage[TP_B];
     __shared__ uint8_t sd1[TP_B];
@@ -118,15 +127,32 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
     const int tid = threadIdx.x;
     const uint32_t nb1 = kp.nb1, nb = kp.nb;
     for (uint32_t b = tid; b < nb; b += NT_B) fhist[b] = 0;
+    __shared__ unsigned long long s_pool0, s_ent0;
+    if (tid == 0) {   // one pair of atomics reserves this workgroup's first block of every region
+        s_pool0 = atomicAdd(&gstat[5], (unsigned long long)nb1 * BLK);
+        s_ent0 = atomicAdd(&gstat[3], (unsigned long long)nb1);
+    }
+    __syncthreads();
     if (tid < (int)nb1) {
         cnt1[tid] = 0;
-        lim1[tid] = end1[file * nb1 + tid];
+        const unsigned long long st = s_pool0 + (unsigned long long)tid * BLK, e = s_ent0 + tid;
+        if (st + BLK > pool_cap || e >= table_cap) {
+            atomicOr(&gstat[2], 4ull);
+            bent[tid] = 0xFFFFFFFFu;
+            bstart[tid] = pool_cap;
+        } else {
+            table[e].start = st;
+            table[e].used = 0;
+            table[e].tag = (file << 8) | tid;
+            bent[tid] = (uint32_t)e;
+            bstart[tid] = st;
+        }
+        bfill[tid] = 0;
     }
     __syncthreads();
     const uint64_t start = (uint64_t)blockIdx.x * st_pos;
     const uint64_t end = start + st_pos < n ? start + st_pos : n;
     uint32_t inst = 0;
-    bool ovf = false;
     for (uint64_t t0 = start; t0 < end; t0 += TP_B) {
         const uint64_t p0 = t0 + (uint64_t)tid * P_B;
         Frame<P_B> f;
@@ -146,18 +172,31 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
             }
         }
         inst += __popc(wm);
-        __syncthreads();
-        if (tid < 64) {   // one wave: scan the <= 64 region counts, reserve global space
+        lds_barrier();
+        if (tid < 64) {   // one wave: scan the <= 64 region counts, place them in the blocks
             const uint32_t c = tid < (int)nb1 ? cnt1[tid] : 0u;
             const uint32_t inc = wave_incl_scan(c, tid);
             if (tid < (int)nb1) {
                 off1[tid] = inc - c;
-                base1[tid] = c ? atomicAdd(&cursor1[file * nb1 + tid], (unsigned long long)c) : 0ull;
                 cnt1[tid] = 0;
+                const uint32_t room = BLK - bfill[tid];
+                base_a[tid] = bstart[tid] + bfill[tid];
+                if (c <= room) {
+                    take_a[tid] = c;
+                    bfill[tid] += c;
+                } else {   // the run spills into a fresh block
+                    take_a[tid] = room;
+                    if (bent[tid] != 0xFFFFFFFFu) table[bent[tid]].used = BLK;
+                    unsigned long long st;
+                    bent[tid] = new_block(gstat, table, table_cap, pool_cap, (file << 8) | tid, st);
+                    bstart[tid] = st;
+                    base_b[tid] = st;
+                    bfill[tid] = c - room;
+                }
             }
             if (tid == 63) off1[nb1] = inc;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int j = 0; j < P_B; ++j)
             if ((wm >> j) & 1u) {
@@ -165,16 +204,18 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
                 stage[pos] = ee[j];
                 sd1[pos] = (uint8_t)dd[j];
             }
-        __syncthreads();
+        lds_barrier();
         const uint32_t tot = off1[nb1];
         for (uint32_t i = tid; i < tot; i += NT_B) {
             const uint32_t d = sd1[i];
-            const unsigned long long g = base1[d] + (i - off1[d]);
-            if (g < lim1[d]) out1[g] = stage[i];
-            else ovf = true;
+            const uint32_t jj = i - off1[d];
+            const unsigned long long g = jj < take_a[d] ? base_a[d] + jj : base_b[d] + (jj - take_a[d]);
+            if (g < pool_cap) out1[g] = stage[i];
         }
-        __syncthreads();
+        lds_barrier();
     }
+    __syncthreads();
+    if (tid < (int)nb1 && bent[tid] != 0xFFFFFFFFu) table[bent[tid]].used = bfill[tid];
     for (uint32_t b = tid; b < nb; b += NT_B) {
         const uint32_t v = fhist[b];
         if (v) atomicAdd(&fine_hist[(uint64_t)b * F + file], (unsigned long long)v);
@@ -182,25 +223,21 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
     uint32_t tot;
     (void)block_excl_scan<NT_B>(inst, ws, &tot);
     if (tid == 0 && tot) atomicAdd(&gstat[4], (unsigned long long)tot);
-    if (__any(ovf) && (tid & 63) == 0) atomicOr(&gstat[2], 4ull);
 }
 
 // ---------------------------------------------------------------- layout
 // One workgroup.  fs[b*(F+1)+f] = start of file f's run in fine bucket b (bucket-major,
 // file-minor), fs[b*(F+1)+F] = bucket end; cursor2 = copy of fs (re-bin write cursors).
-// Level-1 regions: sizes, chunk table chunk_start[rg] (exclusive), chunk_start[R] = total.
 __global__ void __launch_bounds__(1024) kc_layout(const unsigned long long* __restrict__ fine_hist,
                                                   uint32_t nb, uint32_t F, uint64_t* __restrict__ fs,
-                                                  unsigned long long* __restrict__ cursor2,
-                                                  const unsigned long long* __restrict__ cursor1,
-                                                  const uint64_t* __restrict__ start1,
-                                                  const uint64_t* __restrict__ end1, uint32_t R,
-                                                  uint64_t* __restrict__ size1,
-                                                  uint64_t* __restrict__ chunk_start,
-                                                  unsigned long long* __restrict__ gstat) {
+                                                  unsigned long long* __restrict__ cursor2) {
     __shared__ uint64_t ws[17];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    auto block_scan64 = [&](uint64_t v, uint64_t& total) -> uint64_t {
+    const uint64_t NF = (uint64_t)nb * F;
+    uint64_t carry = 0;
+    for (uint64_t r0 = 0; r0 < NF; r0 += 1024) {
+        const uint64_t i = r0 + tid;
+        const uint64_t v = i < NF ? fine_hist[i] : 0ull;
         const uint64_t inc = wave_incl_scan64(v, lane);
         if (lane == 63) ws[wave] = inc;
         __syncthreads();
@@ -210,19 +247,9 @@ __global__ void __launch_bounds__(1024) kc_layout(const unsigned long long* __re
             ws[16] = t;
         }
         __syncthreads();
-        const uint64_t r = ws[wave] + inc - v;
-        total = ws[16];
+        const uint64_t ex = ws[wave] + inc - v + carry;
+        const uint64_t tot = ws[16];
         __syncthreads();
-        return r;
-    };
-    // fine buckets: linear (b, f) order, 1024 entries per round
-    const uint64_t NF = (uint64_t)nb * F;
-    uint64_t carry = 0;
-    for (uint64_t r0 = 0; r0 < NF; r0 += 1024) {
-        const uint64_t i = r0 + tid;
-        const uint64_t v = i < NF ? fine_hist[i] : 0ull;
-        uint64_t tot;
-        const uint64_t ex = block_scan64(v, tot) + carry;
         if (i < NF) {
             const uint64_t b = i / F, f = i % F;
             fs[b * (F + 1) + f] = ex;
@@ -234,54 +261,29 @@ __global__ void __launch_bounds__(1024) kc_layout(const unsigned long long* __re
         }
         carry += tot;
     }
-    // level-1 regions
-    uint64_t ccarry = 0;
-    for (uint32_t r0 = 0; r0 < R; r0 += 1024) {
-        const uint32_t rg = r0 + tid;
-        uint64_t chunks = 0;
-        if (rg < R) {
-            const uint64_t used = cursor1[rg] - start1[rg];
-            if (cursor1[rg] > end1[rg]) atomicOr(&gstat[2], 4ull);
-            const uint64_t sz = start1[rg] + used <= end1[rg] ? used : end1[rg] - start1[rg];
-            size1[rg] = sz;
-            chunks = (sz + CH_R - 1) / CH_R;
-        }
-        uint64_t tot;
-        const uint64_t ex = block_scan64(chunks, tot) + ccarry;
-        if (rg < R) chunk_start[rg] = ex;
-        ccarry += tot;
-    }
-    if (tid == 0) chunk_start[R] = ccarry;
 }
 
 // ---------------------------------------------------------------- pass B2
+// One workgroup per level-1 block: the next fb2 bits pick the fine bucket (<= 64-way,
+// ranked through LDS so each bucket's run is one coalesced segment).
 template <class E1, class E>
-__global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1,
-                                                 const uint64_t* __restrict__ start1,
-                                                 const uint64_t* __restrict__ size1,
-                                                 const uint64_t* __restrict__ chunk_start, uint32_t R,
+__global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, const Blk* __restrict__ table,
+                                                 const unsigned long long* __restrict__ gstat,
                                                  uint32_t F, KP kp,
                                                  unsigned long long* __restrict__ cursor2,
                                                  E* __restrict__ out) {
     constexpr int IT = CH_R / NT_R;
+    static_assert(CH_R >= (int)BLK, "a block must fit one re-bin pass");
     __shared__ uint32_t cnt2[NB1_MAX];
     __shared__ uint32_t off2[NB1_MAX + 1];
     __shared__ unsigned long long base2[NB1_MAX];
     __shared__ E stage[CH_R];
     __shared__ uint8_t sd2[CH_R];
     const int tid = threadIdx.x;
-    const uint64_t id = blockIdx.x;
-    if (id >= chunk_start[R]) return;
-    uint32_t lo = 0, hi = R;   // chunk_start[lo] <= id < chunk_start[hi]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (chunk_start[mid] <= id) lo = mid; else hi = mid;
-    }
-    while (lo + 1 < R && chunk_start[lo + 1] <= id) ++lo;   // skip empty regions
-    const uint32_t rg = lo;
-    const uint32_t file = rg / kp.nb1, d1 = rg % kp.nb1;
-    const uint64_t a = start1[rg] + (id - chunk_start[rg]) * CH_R;
-    const uint64_t e = start1[rg] + size1[rg];
+    const uint64_t blk = blockIdx.x;
+    if (blk >= gstat[3]) return;
+    const Blk bk = table[blk];
+    const uint32_t used = bk.used, file = bk.tag >> 8, d1 = bk.tag & 0xFFu;
     const uint32_t nb2 = kp.nb2;
     if (tid < (int)nb2) cnt2[tid] = 0;
     __syncthreads();
@@ -289,11 +291,11 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1,
     E ee[IT];
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
-        const uint64_t i = a + (uint64_t)j * NT_R + tid;
-        const E1 v = i < e ? in1[i] : E1(0);
+        const uint32_t i = (uint32_t)j * NT_R + tid;
+        const E1 v = i < used ? in1[bk.start + i] : E1(0);
         dd[j] = kp.fb2 ? (uint32_t)((uint64_t)v >> kp.rbits) : 0u;
         ee[j] = (E)((uint64_t)v & kp.rmask);
-        rk[j] = i < e ? atomicAdd(&cnt2[dd[j]], 1u) : 0u;
+        rk[j] = i < used ? atomicAdd(&cnt2[dd[j]], 1u) : 0u;
     }
     __syncthreads();
     if (tid < 64) {
@@ -309,8 +311,8 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1,
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
-        const uint64_t i = a + (uint64_t)j * NT_R + tid;
-        if (i < e) {
+        const uint32_t i = (uint32_t)j * NT_R + tid;
+        if (i < used) {
             const uint32_t pos = off2[dd[j]] + rk[j];
             stage[pos] = ee[j];
             sd2[pos] = (uint8_t)dd[j];
@@ -325,8 +327,22 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1,
 }
 
 // ---------------------------------------------------------------- pass C
+// LDS table: T slots in T/4 groups of 4 (one ds_read_b128 per probe for u32 keys), keys
+// SoA with one u32 counter per file per slot.  A key's home group is its low bits.
+template <class E>
+__device__ __forceinline__ void read_group(const E* keys, uint32_t g, E (&k)[4]) {
+    if constexpr (sizeof(E) == 4) {
+        const uint4 v = reinterpret_cast<const uint4*>(keys)[g];
+        k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
+    } else {
+        const ulonglong2 a = reinterpret_cast<const ulonglong2*>(keys)[2 * g];
+        const ulonglong2 b = reinterpret_cast<const ulonglong2*>(keys)[2 * g + 1];
+        k[0] = a.x; k[1] = a.y; k[2] = b.x; k[3] = b.y;
+    }
+}
+
 // gstat: [0] output cursor, [1] max sub-ranges any bucket needed, [2] error bits
-// (1 = unsplittable overflow, 2 = output capacity exceeded).
+// (1 = unsplittable overflow, 2 = output capacity exceeded, 4 = level-1 overflow).
 template <class E>
 __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                                                  const uint64_t* __restrict__ fs, uint32_t F,
@@ -349,6 +365,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
     const uint32_t SUBB = rbits < 16 ? rbits : 16;
     const uint32_t full_hi = 1u << SUBB;
     const uint32_t mc = min_count ? min_count : 1u;
+    const uint32_t G = T / 4;
     if (tid == 0) {
         stk_lo[0] = 0;
         stk_hi[0] = full_hi;
@@ -380,8 +397,8 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                     const uint64_t i = i0 + (uint64_t)q * NT_C + tid;
                     rv[q] = i < e ? binned[i] : EMPTY;
                 }
-                // 1) all home slots read before any is consumed: one LDS round trip settles
-                //    every element whose key already sits in its home slot (fire-and-forget add)
+                // 1) all home groups read before any is consumed: one LDS round trip settles
+                //    every element whose key already sits in its home group
                 uint32_t miss = 0;
 #pragma unroll
                 for (int q = 0; q < PF_C; ++q) {
@@ -390,15 +407,19 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                         const uint32_t sk = SUBB ? (uint32_t)(rv[q] >> (rbits - SUBB)) : 0u;
                         live = sk >= lo && sk < hi;
                     }
-                    const uint32_t sl = (uint32_t)rv[q] & (T - 1);
-                    const E c = keys[sl];
-                    if (live && c == rv[q]) atomicAdd(&cf[sl], 1u);
+                    const uint32_t g = (uint32_t)rv[q] & (G - 1);
+                    E kg[4];
+                    read_group(keys, g, kg);
+                    int w = -1;
+#pragma unroll
+                    for (int t = 3; t >= 0; --t) w = kg[t] == rv[q] ? t : w;
+                    if (live && w >= 0) atomicAdd(&cf[4 * g + w], 1u);
                     else if (live) miss |= 1u << q;
                 }
-                // 2) the rest: one probe step per lane per iteration, a lane takes its next
-                //    missed element when the current one is settled
+                // 2) the rest (new keys, keys displaced from their home group): one probe
+                //    step per lane per iteration; a lane takes its next miss when settled
                 E r = EMPTY;
-                uint32_t sl = 0;
+                uint32_t g = 0;
                 while (__any(miss != 0u || r != EMPTY)) {
                     if (r == EMPTY && miss) {
                         const int q = __builtin_ctz(miss);
@@ -407,17 +428,25 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 #pragma unroll
                         for (int t = 1; t < PF_C; ++t) pick = q == t ? rv[t] : pick;
                         r = pick;
-                        sl = (uint32_t)r & (T - 1);
+                        g = (uint32_t)r & (G - 1);
                     }
                     if (r != EMPTY) {
-                        const E c = keys[sl];
-                        if (c == r) {
-                            atomicAdd(&cf[sl], 1u);
+                        E kg[4];
+                        read_group(keys, g, kg);
+                        int w = -1, e0 = -1;
+#pragma unroll
+                        for (int t = 3; t >= 0; --t) {
+                            w = kg[t] == r ? t : w;
+                            e0 = kg[t] == EMPTY ? t : e0;
+                        }
+                        if (w >= 0) {
+                            atomicAdd(&cf[4 * g + w], 1u);
                             r = EMPTY;
-                        } else if (c == EMPTY) {
+                        } else if (e0 >= 0) {
                             if (*(volatile uint32_t*)&s_ovf) {
                                 r = EMPTY;   // this sub-range is redone after the split
                             } else {
+                                const uint32_t sl = 4 * g + (uint32_t)e0;
                                 const E old = atomicCAS(&keys[sl], EMPTY, r);
                                 if (old == EMPTY || old == r) {
                                     if (old == EMPTY) {
@@ -426,12 +455,10 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                                     }
                                     atomicAdd(&cf[sl], 1u);
                                     r = EMPTY;
-                                } else {
-                                    sl = (sl + 1) & (T - 1);
-                                }
+                                }   // else: lost the slot to another key, re-read the group
                             }
                         } else {
-                            sl = (sl + 1) & (T - 1);
+                            g = (g + 1) & (G - 1);   // group full: next group
                         }
                     }
                 }
@@ -539,6 +566,21 @@ __global__ void __launch_bounds__(NT_H) kc_spec_hist(const uint32_t* __restrict_
     for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_H) {
         const uint32_t v = lh[i];
         if (v) atomicAdd(&hist[(uint64_t)(i / TL) * TD + (i % TL)], (unsigned long long)v);
+    }
+}
+
+// Nonzero dense bins -> (threshold index << 56 | total, count) pairs.
+__global__ void kc_hist_compact(const unsigned long long* __restrict__ hist, uint64_t n,
+                                unsigned long long* __restrict__ out, unsigned long long* __restrict__ cur,
+                                uint64_t cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long v = hist[i];
+    if (!v) return;
+    const unsigned long long o = atomicAdd(cur, 1ull);
+    if (o < cap) {
+        out[2 * o] = ((unsigned long long)(i / TD) << 56) | (i % TD);
+        out[2 * o + 1] = v;
     }
 }
 
@@ -680,7 +722,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const bool e32 = kp.rbits <= 31;
     s.fb = fb;
     s.buckets = kp.nb;
-    const uint32_t nb = kp.nb, nb1 = kp.nb1, R = F * nb1;
+    const uint32_t nb = kp.nb, nb1 = kp.nb1;
 
     // super-tiles: ~4 per CU over all files, whole tiles
     uint64_t st_pos = total_bytes / ((uint64_t)c->num_cu * 4) + 1;
@@ -688,19 +730,10 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     std::vector<uint32_t> n_st(F, 0);
     for (uint32_t f = 0; f < F; ++f) n_st[f] = (uint32_t)((s.seq_len[f] + st_pos - 1) / st_pos);
 
-    // level-1 regions (file f, digit d): estimated capacity, or the exact sizes a previous
-    // overflowing attempt measured
     auto* gstat = static_cast<unsigned long long*>(s.cursor.ensure(8 * 8));
     uint64_t* fs = static_cast<uint64_t*>(s.file_start.ensure((size_t)nb * (F + 1) * 8));
     auto* cursor2 = static_cast<unsigned long long*>(s.cursor2.ensure((size_t)nb * (F + 1) * 8));
     auto* fine_hist = static_cast<unsigned long long*>(s.fine_hist.ensure((size_t)nb * F * 8));
-    char* rgb = static_cast<char*>(s.regions.ensure((size_t)(R + 1) * 8 * 5 + 256));
-    uint64_t* d_start1 = reinterpret_cast<uint64_t*>(rgb);
-    uint64_t* d_end1 = d_start1 + (R + 1);
-    auto* cursor1 = reinterpret_cast<unsigned long long*>(d_end1 + (R + 1));
-    uint64_t* size1 = reinterpret_cast<uint64_t*>(cursor1 + (R + 1));
-    uint64_t* chunk_start = size1 + (R + 1);
-
     // P: pack every file (2-bit codes + valid bits), pad words zeroed (= invalid)
     std::vector<const uint32_t*> pks(F);
     std::vector<const uint16_t*> vds(F);
@@ -719,7 +752,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
         if (nw) {
             const uint8_t* sp = s.seq[f]->as<uint8_t>();
             c->launch("kc_pack", [&] {
-                hipLaunchKernelGGL(kc_pack<false>, dim3(blocks_for(nw, 256)), dim3(256), 0, c->stream, sp, n,
+                hipLaunchKernelGGL(pack_kernel<false>, dim3(blocks_for(nw, 256)), dim3(256), 0, c->stream, sp, n,
                                    pk, vd, nw);
             });
             c->check_launch("kc_pack");
@@ -736,93 +769,69 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     uint32_t T = 1;
     while ((uint64_t)T * 2 * slot_b <= LDS_TAB) T *= 2;
     HGA_REQUIRE(T >= 2 * NT_C, HGA_ERR_INVALID, "too many files for the LDS table");
-    const uint32_t maxload = std::min<uint32_t>((uint32_t)(T * 0.8), T - NT_C - 8);
+    const uint32_t maxload = std::min<uint32_t>((uint32_t)(T * 0.85), T - NT_C - 8);
     void* binned = s.binned.ensure(std::max<size_t>(total_bytes, 1) * esz);
 
-    unsigned long long h_stat[8];
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        std::vector<uint64_t> start1(R + 1), end1(R + 1);
-        uint64_t at = 0;
-        for (uint32_t f = 0; f < F; ++f)
-            for (uint32_t d = 0; d < nb1; ++d) {
-                const uint32_t rg = f * nb1 + d;
-                const uint64_t capr = attempt == 0 || s.l1_exact.size() != R
-                                          ? s.seq_len[f] / nb1 + s.seq_len[f] / (8 * nb1) + 16384
-                                          : s.l1_exact[rg];
-                start1[rg] = at;
-                end1[rg] = at + capr;
-                at += (capr + 63) / 64 * 64;
-            }
-        start1[R] = end1[R] = at;
-        const uint64_t l1_elems = at;
-        void* binned1 = s.binned1.ensure(std::max<uint64_t>(l1_elems, 1) * esz1);
-        HGA_HIP(hipMemcpyAsync(d_start1, start1.data(), (R + 1) * 8, hipMemcpyHostToDevice, c->stream));
-        HGA_HIP(hipMemcpyAsync(d_end1, end1.data(), (R + 1) * 8, hipMemcpyHostToDevice, c->stream));
-        HGA_HIP(hipMemcpyAsync(cursor1, start1.data(), (R + 1) * 8, hipMemcpyHostToDevice, c->stream));
-        HGA_HIP(hipMemsetAsync(gstat, 0, 8 * 8, c->stream));
-        HGA_HIP(hipMemsetAsync(fine_hist, 0, (size_t)nb * F * 8, c->stream));
+    // level-1 pool: every (workgroup, region) wastes less than one block
+    uint64_t n_wg = 0;
+    for (uint32_t f = 0; f < F; ++f) n_wg += n_st[f];
+    const uint64_t pool_cap = total_bytes + n_wg * nb1 * BLK + BLK;
+    const uint64_t table_cap = pool_cap / BLK + 1;
+    void* binned1 = s.binned1.ensure(pool_cap * esz1);
+    Blk* table = static_cast<Blk*>(s.regions.ensure(table_cap * sizeof(Blk)));
+    HGA_HIP(hipMemsetAsync(gstat, 0, 8 * 8, c->stream));
+    HGA_HIP(hipMemsetAsync(fine_hist, 0, (size_t)nb * F * 8, c->stream));
 
-        // B1: level-1 binning + fine histogram + instance count
-        for (uint32_t f = 0; f < F; ++f) {
-            if (!n_st[f]) continue;
-            const uint64_t n = s.seq_len[f];
-            c->launch("kc_bin1", [&] {
-                if (e1_32)
-                    hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f],
-                                       n, st_pos, f, F, kp, cursor1, d_end1, static_cast<uint32_t*>(binned1),
-                                       fine_hist, gstat);
-                else
-                    hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f],
-                                       n, st_pos, f, F, kp, cursor1, d_end1, static_cast<uint64_t*>(binned1),
-                                       fine_hist, gstat);
-            });
-            c->check_launch("kc_bin1");
-        }
-        // L: fine layout + level-1 chunk table
-        c->launch("kc_layout", [&] {
-            hipLaunchKernelGGL(kc_layout, dim3(1), dim3(1024), 0, c->stream, fine_hist, nb, F, fs, cursor2,
-                               cursor1, d_start1, d_end1, R, size1, chunk_start, gstat);
-        });
-        c->check_launch("kc_layout");
-        // B2: re-bin every level-1 region into the fine buckets
-        uint64_t max_chunks = 0;
-        for (uint32_t rg = 0; rg < R; ++rg) max_chunks += (end1[rg] - start1[rg] + CH_R - 1) / CH_R;
-        if (max_chunks) {
-            c->launch("kc_rebin", [&] {
-#define HGA_REBIN(E1T, ET)                                                                                 \
-    hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3((unsigned)max_chunks), dim3(NT_R), 0, c->stream,          \
-                       static_cast<const E1T*>(binned1), d_start1, size1, chunk_start, R, F, kp, cursor2, \
-                       static_cast<ET*>(binned))
-                if (e1_32 && e32) HGA_REBIN(uint32_t, uint32_t);
-                else if (e32) HGA_REBIN(uint64_t, uint32_t);
-                else if (e1_32) HGA_REBIN(uint32_t, uint64_t);
-                else HGA_REBIN(uint64_t, uint64_t);
-#undef HGA_REBIN
-            });
-            c->check_launch("kc_rebin");
-        }
-        // C: per-bucket count
-        c->launch("kc_count", [&] {
-            if (e32)
-                hipLaunchKernelGGL(kc_count<uint32_t>, dim3(nb), dim3(NT_C), 0, c->stream,
-                                   static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
-                                   s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+    // B1: level-1 binning into pool blocks + fine histogram + instance count
+    for (uint32_t f = 0; f < F; ++f) {
+        if (!n_st[f]) continue;
+        const uint64_t n = s.seq_len[f];
+        c->launch("kc_bin1", [&] {
+            if (e1_32)
+                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f], n,
+                                   st_pos, f, F, kp, table, table_cap, pool_cap, static_cast<uint32_t*>(binned1),
+                                   fine_hist, gstat);
             else
-                hipLaunchKernelGGL(kc_count<uint64_t>, dim3(nb), dim3(NT_C), 0, c->stream,
-                                   static_cast<const uint64_t*>(binned), fs, F, T, maxload, min_per_file, kp,
-                                   s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f], n,
+                                   st_pos, f, F, kp, table, table_cap, pool_cap, static_cast<uint64_t*>(binned1),
+                                   fine_hist, gstat);
         });
-        c->check_launch("kc_count");
-        HGA_HIP(hipMemcpyAsync(h_stat, gstat, sizeof(h_stat), hipMemcpyDeviceToHost, c->stream));
-        c->sync();
-        if (!(h_stat[2] & 4ull)) break;
-        // a level-1 region overflowed its estimate: the cursors hold the exact sizes
-        HGA_REQUIRE(attempt == 0, HGA_ERR_INVALID, "level-1 region overflow with exact capacities");
-        std::vector<unsigned long long> cur(R);
-        HGA_HIP(hipMemcpy(cur.data(), cursor1, R * 8, hipMemcpyDeviceToHost));
-        s.l1_exact.assign(R, 0);
-        for (uint32_t rg = 0; rg < R; ++rg) s.l1_exact[rg] = cur[rg] - start1[rg];
+        c->check_launch("kc_bin1");
     }
+    // L: fine layout
+    c->launch("kc_layout", [&] {
+        hipLaunchKernelGGL(kc_layout, dim3(1), dim3(1024), 0, c->stream, fine_hist, nb, F, fs, cursor2);
+    });
+    c->check_launch("kc_layout");
+    // B2: re-bin every level-1 block into the fine buckets (persistent grid)
+    const unsigned rebin_grid = (unsigned)std::max<uint64_t>(1, table_cap);   // exits past gstat[3]
+    c->launch("kc_rebin", [&] {
+#define HGA_REBIN(E1T, ET)                                                                                 \
+    hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3(rebin_grid), dim3(NT_R), 0, c->stream,                    \
+                       static_cast<const E1T*>(binned1), table, gstat, F, kp, cursor2, static_cast<ET*>(binned))
+        if (e1_32 && e32) HGA_REBIN(uint32_t, uint32_t);
+        else if (e32) HGA_REBIN(uint64_t, uint32_t);
+        else if (e1_32) HGA_REBIN(uint32_t, uint64_t);
+        else HGA_REBIN(uint64_t, uint64_t);
+#undef HGA_REBIN
+    });
+    c->check_launch("kc_rebin");
+    // C: per-bucket count
+    c->launch("kc_count", [&] {
+        if (e32)
+            hipLaunchKernelGGL(kc_count<uint32_t>, dim3(nb), dim3(NT_C), 0, c->stream,
+                               static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
+                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+        else
+            hipLaunchKernelGGL(kc_count<uint64_t>, dim3(nb), dim3(NT_C), 0, c->stream,
+                               static_cast<const uint64_t*>(binned), fs, F, T, maxload, min_per_file, kp,
+                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+    });
+    c->check_launch("kc_count");
+    unsigned long long h_stat[8];
+    HGA_HIP(hipMemcpyAsync(h_stat, gstat, sizeof(h_stat), hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+    HGA_REQUIRE(!(h_stat[2] & 4ull), HGA_ERR_OOM, "level-1 block pool exhausted");
     HGA_REQUIRE(!(h_stat[2] & 1ull), HGA_ERR_INVALID, "a bucket could not be split to fit the LDS table");
     HGA_REQUIRE(!(h_stat[2] & 2ull), HGA_ERR_OOM, "row capacity exceeded");
     s.rows = h_stat[0];
@@ -859,30 +868,39 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
                            hist, over, ctrl, over_cap, ctrl + 1);
     });
     c->check_launch("kc_spec_hist");
-    std::vector<unsigned long long> h((size_t)n_thr * TD);
-    unsigned long long hc[2];
-    HGA_HIP(hipMemcpyAsync(h.data(), hist, hbytes, hipMemcpyDeviceToHost, c->stream));
-    HGA_HIP(hipMemcpyAsync(hc, ctrl, 16, hipMemcpyDeviceToHost, c->stream));
+    // compact the dense bins on the device: only (threshold, total, count) triples cross PCIe
+    const uint64_t ncap = 1u << 20;
+    auto* comp = static_cast<unsigned long long*>(s.hist_comp.ensure(ncap * 16 + 64));
+    HGA_HIP(hipMemsetAsync(ctrl + 2, 0, 8, c->stream));
+    const uint64_t nd = (uint64_t)n_thr * TD;
+    c->launch("kc_spec_hist", [&] {
+        hipLaunchKernelGGL(kc_hist_compact, dim3(blocks_for(nd, 256)), dim3(256), 0, c->stream, hist, nd, comp,
+                           ctrl + 2, ncap);
+    });
+    c->check_launch("kc_hist_compact");
+    unsigned long long hc[3];
+    HGA_HIP(hipMemcpyAsync(hc, ctrl, 24, hipMemcpyDeviceToHost, c->stream));
     c->sync();
     HGA_REQUIRE(!(hc[1] & 1ull), HGA_ERR_INVALID, "a row's specificity is above the last threshold");
     HGA_REQUIRE(!(hc[1] & 2ull), HGA_ERR_OOM, "histogram overflow list full");
-    std::map<std::pair<uint32_t, uint64_t>, uint64_t> sparse;
+    HGA_REQUIRE(hc[2] <= ncap, HGA_ERR_OOM, "histogram compaction buffer full");
+    std::map<std::pair<uint32_t, uint64_t>, uint64_t> bins;
+    if (hc[2]) {
+        std::vector<unsigned long long> cv(2 * hc[2]);
+        HGA_HIP(hipMemcpy(cv.data(), comp, hc[2] * 16, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < hc[2]; ++i)
+            bins[{(uint32_t)(cv[2 * i] >> 56), cv[2 * i] & ((1ull << 56) - 1)}] += cv[2 * i + 1];
+    }
     if (hc[0]) {
-        std::vector<unsigned long long> ov(hc[0]);
-        HGA_HIP(hipMemcpy(ov.data(), over, hc[0] * 8, hipMemcpyDeviceToHost));
-        for (auto v : ov) sparse[{(uint32_t)(v >> 56), v & ((1ull << 56) - 1)}] += 1;
+        std::vector<unsigned long long> ov(std::min<uint64_t>(hc[0], over_cap));
+        HGA_HIP(hipMemcpy(ov.data(), over, ov.size() * 8, hipMemcpyDeviceToHost));
+        for (auto v : ov) bins[{(uint32_t)(v >> 56), v & ((1ull << 56) - 1)}] += 1;
     }
     out.clear();
-    for (uint32_t t = 0; t < n_thr; ++t) {
-        for (uint32_t tot = 0; tot < TD; ++tot) {
-            const auto v = h[(size_t)t * TD + tot];
-            if (v) { out.push_back(t); out.push_back(tot); out.push_back((int64_t)v); }
-        }
-        for (auto it = sparse.lower_bound({t, 0}); it != sparse.end() && it->first.first == t; ++it) {
-            out.push_back(t);
-            out.push_back((int64_t)it->first.second);
-            out.push_back((int64_t)it->second);
-        }
+    for (auto& kv : bins) {   // std::map order: threshold, then total
+        out.push_back(kv.first.first);
+        out.push_back((int64_t)kv.first.second);
+        out.push_back((int64_t)kv.second);
     }
 }
 

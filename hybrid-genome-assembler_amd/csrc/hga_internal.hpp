@@ -103,7 +103,7 @@ struct CountState {
     std::vector<DevBuf*> packed, valid;   // 2-bit codes / valid bits per file (kc_pack)
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
-        sel_keys, sel_tmp, hist_dense;
+        sel_keys, sel_tmp, hist_dense, hist_comp;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t buckets = 0, fb = 0, max_split = 1;
@@ -118,15 +118,15 @@ struct LookupState {
     bool loaded = false, have_reads = false, ran = false;
     int k = 0;
     uint32_t n_sdk = 0;
-    uint64_t slots = 0;
-    DevBuf tab_key, tab_id;
+    uint64_t slots = 0, fwords = 0, pk_words = 0;
+    DevBuf tab_key, tab_id, filter, packed, valid, starts;
     uint64_t n_reads = 0, n_bases = 0;
     uint32_t first_read_id = 1;
     DevBuf bases, offsets;
     // results
     DevBuf tile_cnt, hit_read, hit_kid, hit_pos, hit_ptr, s_key, s_val, s_key2, s_val2,
         first_flag, first_kid, first_pos, first_read, first_ptr, kci_key, kci_val, kci_ptr, scratch,
-        scratch2;
+        scratch2, scratch3;
     std::vector<uint64_t> h_offsets;
     uint64_t windows = 0, hits = 0, firsts = 0, reads_hit = 0;
 };

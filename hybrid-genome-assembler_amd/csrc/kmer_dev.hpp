@@ -182,6 +182,31 @@ __device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
     return v64;
 }
 
+// ASCII -> packed frames (kc_pack / lk_pack).  REF = KmerIterator semantics (upper-case
+// ACGT only), otherwise jellyfish semantics (either case).
+// One thread per 16 bases: packed codes (first base in bits 31:30) and valid bits.
+template <bool REF>
+__global__ void pack_kernel(const uint8_t* __restrict__ s, uint64_t n, uint32_t* __restrict__ pk,
+                        uint16_t* __restrict__ vd, uint64_t nw) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const uint4 v = load16(s, (int64_t)(w * 16), n);
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    uint32_t code = 0, valid = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (ws[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        const uint32_t u = REF ? b : (b & 0xDFu);
+        const uint32_t d = u - 0x41u;
+        const bool ok = d < 20u && ((kBaseBits >> d) & 1u);
+        const uint32_t c = ok ? (((u >> 1) ^ (u >> 2)) & 3u) : 0u;
+        code |= c << (30 - 2 * j);
+        valid |= (ok ? 1u : 0u) << j;
+    }
+    pk[PAD_WORDS + w] = code;
+    vd[PAD_WORDS + w] = (uint16_t)valid;
+}
+
 // Wave / block scans (wave64).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll

@@ -34,6 +34,8 @@ def main(dirs, out=None):
                 dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     cols = ["FETCH_SIZE", "WRITE_SIZE", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
             "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"]
+    if any("TCC_HIT_sum" in agg[k] for k in agg):
+        cols += ["TCC_HIT_sum", "TCC_MISS_sum"]
     res = {}
     print("kernel".ljust(26), "ms(med)".rjust(8), *[c.replace("SQ_", "")[:10].rjust(11) for c in cols])
     for k in sorted(agg):
