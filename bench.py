@@ -8,9 +8,11 @@ reads against the C2 export at [10,25] (configs[2], "C3"), with the CPU oracle t
 A step is one pass of the counting hot path over the resident reads: bin + per-file count +
 merge (hga_count_run), the specificity histogram (hga_count_spec_hist) and the sorted export
 selection at [10,25] (hga_count_select_device) — everything jf_occurrences does on the device.
-Inputs are resident in HBM before the timed region.  N > 1 (torchrun, one rank per GPU): every
-rank counts its own C2-sized shard of reads (weak scaling); barrier + max-over-ranks timing.
-Rank 0 prints one JSON line.
+Inputs are resident in HBM before the timed region.  N > 1 (torchrun, one rank per GPU, RCCL):
+every rank holds its own C2-sized shard of reads (weak scaling) and a step is the distributed
+count of DESIGN.md §6 — local count, owner partition, all-to-all of the rows over xGMI, owner
+merge + `--bc` drop, histogram reduction, per-owner export selection (hga_dist.OwnerExchange);
+barrier + max-over-ranks timing.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -77,7 +79,7 @@ class Dist:
             import torch
             import torch.distributed as dist
             torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl")
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local}"))
             self.torch, self.dist = torch, dist
             self.pg = True
         if n != self.world and self.world > 1:
@@ -111,6 +113,12 @@ def count_step(ctx):
     ctx.count_run(2)
     ctx.spec_hist(THRESHOLDS)
     return ctx.select_device(LOWER, UPPER)
+
+
+def dist_count_step(ex):
+    ex.count(2)
+    ex.spec_hist(THRESHOLDS)
+    return ex.select_counts(LOWER, UPPER)
 
 
 KERNEL_BYTES = {
@@ -174,8 +182,13 @@ def main():
     ctx.count_begin(K, 2)
     ctx.count_add(0, ra.seq)
     ctx.count_add(1, rb.seq)
+    ex = None
+    if D.world > 1:
+        import hga_dist
+        ex = hga_dist.OwnerExchange(hga_dist.HgaEngine(ctx, K, 2, f"cuda:{dev}"))
+    step = (lambda: dist_count_step(ex)) if ex else (lambda: count_step(ctx))
     for _ in range(args.warmup):
-        count_step(ctx)
+        step()
     st = ctx.count_stats()
     stats = {"bytes": st.bytes, "instances": st.instances, "rows": st.distinct_rows, "files": 2}
     ctx.profile(True)
@@ -184,7 +197,7 @@ def main():
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        n_sel, n_disc = count_step(ctx)
+        n_sel, n_disc = step()
     ctx.sync()
     D.barrier()
     dt = time.perf_counter() - t0
@@ -195,7 +208,7 @@ def main():
 
     kernels = {}
     for name in ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
-                 "radix_upsweep", "radix_downsweep", "scan"):
+                 "kx_partition", "kx_merge", "radix_upsweep", "radix_downsweep", "scan"):
         ms, n = ctx.profile_get(name)
         if n:
             kernels[name] = {"ms_total": ms, "launches": n, "ms_per_step": ms / args.steps}
@@ -222,7 +235,9 @@ def main():
                    "k": K, "reads": ra.n + rb.n, "bases": st.bytes, "instances_per_gpu": st.instances,
                    "distinct_rows": st.distinct_rows, "selected": n_sel, "discriminative": n_disc,
                    "buckets": st.buckets, "max_split": st.max_split, "parallelism": f"dp{D.world}",
-                   "exchange": "none: ranks count independent shards (replicas)" if D.world > 1 else None},
+                   "exchange": ("owner all-to-all of (key, counts) rows over RCCL, "
+                                f"{ex.local_rows} local rows -> {ex.received_rows} owned rows on rank 0")
+                   if ex else None},
         "roofline": roofline,
         "pipeline_roofline": {"model": "16.25 B per k-mer instance (SURVEY.md §8(d))",
                               "achieved": round(pipe_gbs, 1), "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)},
@@ -234,8 +249,12 @@ def main():
         bases, offsets = make_c3(ga, gb, D.rank)
         log(f"[rank {D.rank}] C3 generated in {time.perf_counter() - t_gen:.1f}s: {len(offsets) - 1} reads")
         ctx2 = hga.Ctx(dev)
-        ctx.count_run(2)
-        sdk, _, _ = ctx.select(LOWER, UPPER)
+        if ex:
+            ex.count(2)
+            sdk = ex.select_all(LOWER, UPPER)
+        else:
+            ctx.count_run(2)
+            sdk, _, _ = ctx.select(LOWER, UPPER)
         ctx2.lookup_load(K, sdk)
         ctx2.lookup_set_reads(bases, offsets, 1)
         ctx2.lookup_run()

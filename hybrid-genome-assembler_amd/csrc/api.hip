@@ -182,6 +182,19 @@ hga_status hga_count_select_device(hga_ctx* c, int64_t lower, int64_t upper, uin
     });
 }
 
+hga_status hga_count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_owners, uint64_t* keys_out,
+                               uint32_t* counts_out, uint64_t* rows_per_owner) {
+    HGA_CTX_GUARD(c, {
+        HGA_REQUIRE(rows_per_owner && (n_owners <= 1 || splitters), HGA_ERR_INVALID, "null pointer");
+        hga::count_partition(c, splitters, n_owners, keys_out, counts_out, rows_per_owner);
+    });
+}
+
+hga_status hga_count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint64_t n,
+                           uint32_t min_per_file) {
+    HGA_CTX_GUARD(c, { hga::count_merge(c, keys, counts, n, min_per_file); });
+}
+
 hga_status hga_count_rows(hga_ctx* c, uint64_t** keys, uint32_t** counts, uint64_t* rows) {
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(keys && counts && rows, HGA_ERR_INVALID, "null pointer");

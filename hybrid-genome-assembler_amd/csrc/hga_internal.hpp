@@ -103,7 +103,7 @@ struct CountState {
     std::vector<DevBuf*> packed, valid;   // 2-bit codes / valid bits per file (kc_pack)
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
-        sel_keys, sel_tmp, hist_dense, hist_comp;
+        sel_keys, sel_tmp, hist_dense, hist_comp, xch, xch2;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t buckets = 0, fb = 0, max_split = 1;
@@ -169,6 +169,9 @@ void count_spec_hist(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<
 void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* n_discr);
 void count_fetch_selected(hga_ctx* c, uint64_t* dst, uint8_t* flags);
 void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);
+void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* keys_out,
+                     uint32_t* counts_out, uint64_t* rows_per_owner);
+void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min_c);
 
 void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n);
 void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, uint64_t n,

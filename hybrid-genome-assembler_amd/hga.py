@@ -66,6 +66,8 @@ HGA_SYMBOLS = {
     "hga_count_select_ex": (C.c_int, [_vp, C.c_int64, C.c_int64, C.POINTER(_u64p), C.POINTER(_u8p), _u64p,
                                       _u64p]),
     "hga_count_select_device": (C.c_int, [_vp, C.c_int64, C.c_int64, _u64p, _u64p]),
+    "hga_count_partition": (C.c_int, [_vp, _u64p, C.c_uint32, C.c_void_p, C.c_void_p, _u64p]),
+    "hga_count_merge": (C.c_int, [_vp, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]),
     "hga_count_rows": (C.c_int, [_vp, C.POINTER(_u64p), C.POINTER(_u32p), _u64p]),
     "hga_count_dump": (C.c_int, [_vp, C.c_uint32, C.POINTER(_u64p), C.POINTER(_u32p), _u64p]),
     "hga_lookup_load": (C.c_int, [_vp, C.c_int, _u64p, C.c_uint32]),
@@ -226,6 +228,20 @@ class Ctx:
         d = C.c_uint64()
         _ck(lib().hga_count_select_device(self._h, lower, upper, C.byref(n), C.byref(d)))
         return n.value, d.value
+
+    def count_partition(self, splitters, keys_out_ptr: int, counts_out_ptr: int):
+        """Rows grouped by owner into device buffers (raw pointers, e.g. torch data_ptr()).
+        Returns rows per owner (numpy u64)."""
+        spl = np.ascontiguousarray(splitters, dtype=np.uint64)
+        n_own = len(spl) + 1
+        out = np.zeros(n_own, np.uint64)
+        _ck(lib().hga_count_partition(self._h, _p(spl, C.c_uint64), n_own, C.c_void_p(keys_out_ptr),
+                                      C.c_void_p(counts_out_ptr), _p(out, C.c_uint64)))
+        return out
+
+    def count_merge(self, keys_ptr: int, counts_ptr: int, n: int, min_per_file: int = 2):
+        """Owner-side merge of received rows (device pointers); they become the ctx rows."""
+        _ck(lib().hga_count_merge(self._h, C.c_void_p(keys_ptr), C.c_void_p(counts_ptr), n, min_per_file))
 
     def rows(self):
         k = _u64p()

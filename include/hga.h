@@ -113,6 +113,25 @@ hga_status hga_count_rows(hga_ctx* ctx, uint64_t** keys, uint32_t** counts, uint
 hga_status hga_count_dump(hga_ctx* ctx, uint32_t file, uint64_t** keys, uint32_t** counts,
                           uint64_t* rows);
 
+/* Multi-GPU owner exchange (the reference is single-process).  Each rank
+ * counts its shard with hga_count_run(ctx, 1), so no per-file singleton is dropped before
+ * the global sum, then:
+ *   hga_count_partition  writes the rank's merged rows grouped by owner into caller-owned
+ *     DEVICE buffers keys_out[rows] and counts_out[rows * n_files] (row-major), owner o first
+ *     covering codes in [splitters[o-1], splitters[o]) (n_owners-1 ascending splitters, host
+ *     memory); rows_per_owner[n_owners] (host) receives each owner's slice length.  The
+ *     buffers hold hga_count_get_stats().distinct_rows rows.  Returns when they are complete.
+ *   (caller) one all-to-all per array over RCCL.
+ *   hga_count_merge      takes the rows received by this owner (DEVICE pointers, any order,
+ *     at most one row per key per source rank), sums equal keys, applies the per-file drop
+ *     (count >= min_per_file, the `--bc` of run_jellyfish.sh:3-6) and makes the result the
+ *     ctx's merged rows: spec_hist / select / rows / dump then run on this owner's key range,
+ *     ascending, exactly as JellyfishOccurrenceReader.cpp:63-135 would over the whole input. */
+hga_status hga_count_partition(hga_ctx* ctx, const uint64_t* splitters, uint32_t n_owners,
+                               uint64_t* keys_out, uint32_t* counts_out, uint64_t* rows_per_owner);
+hga_status hga_count_merge(hga_ctx* ctx, const uint64_t* keys, const uint32_t* counts, uint64_t n,
+                           uint32_t min_per_file);
+
 /* ------------------------------------------------------------------------------
  * SDK lookup — replaces the per-read loop of ReadClusteringEngine::construct_indices
  * (src/clustering/ReadClusteringEngine.cpp:234-299).  The host keeps SDK loading

@@ -1,0 +1,128 @@
+"""GPU side of the owner exchange (exchange.hip through the C ABI, hga_dist.py).
+
+(a) G ranks simulated in one process: G contexts count contiguous shards with min 1, partition
+    their rows by owner into torch device buffers, owner o merges the slices addressed to it;
+    the union of owner rows must equal the oracle's merged rows over all reads with the `--bc`
+    drop (run_jellyfish.sh:3-6), and the per-owner histograms / exports must add up to the
+    single-context results.
+(b) The product protocol (hga_dist.OwnerExchange + HgaEngine) in 2 processes sharing cuda:0,
+    collectives over gloo with host staging (RCCL needs one GPU per rank; the 8-GPU RCCL run is
+    the driver's bench)."""
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import hga
+import hga_dist
+import oracle
+from test_dist import make_streams
+
+THR = oracle.THRESHOLDS
+pytestmark = pytest.mark.gpu
+
+
+def _sim(streams, k, G, lower, upper, min_c=2):
+    F = len(streams)
+    dev = torch.device("cuda:0")
+    ctxs = [hga.Ctx(0) for _ in range(G)]
+    spl = hga_dist.owner_splitters(k, G)
+    sends = []
+    for r, c in enumerate(ctxs):
+        c.count_begin(k, F)
+        for f, s in enumerate(streams):
+            c.count_add(f, hga_dist.shard_reads(s, r, G))
+        c.count_run(1)
+        rows = c.count_stats().distinct_rows
+        kb = torch.empty(rows, dtype=torch.int64, device=dev)
+        cb = torch.empty(rows * F, dtype=torch.int32, device=dev)
+        per = c.count_partition(spl, kb.data_ptr(), cb.data_ptr()).astype(np.int64)
+        assert int(per.sum()) == rows
+        off = np.concatenate([[0], np.cumsum(per)])
+        sends.append((kb, cb, off))
+    keys, counts, hist, sel, disc = [], [], [], [], 0
+    for o, c in enumerate(ctxs):
+        rk = torch.cat([kb[off[o]:off[o + 1]] for kb, _, off in sends])
+        rc = torch.cat([cb[off[o] * F:off[o + 1] * F] for _, cb, off in sends])
+        torch.cuda.synchronize()
+        c.count_merge(rk.data_ptr(), rc.data_ptr(), len(rk), min_c)
+        kk, cc = c.rows()
+        if len(kk):
+            lo = 0 if o == 0 else int(spl[o - 1])
+            hi = 1 << 64 if o == G - 1 else int(spl[o])
+            assert lo <= int(kk.min()) and int(kk.max()) < hi
+        keys.append(kk)
+        counts.append(cc)
+        hist.append(c.spec_hist(THR) if len(kk) else np.zeros((0, 3), np.int64))
+        s, f, d = c.select(lower, upper)
+        sel.append(s)
+        disc += d
+    for c in ctxs:
+        c.close()
+    acc = {}
+    for h in hist:
+        for t, tot, n in h:
+            acc[(int(t), int(tot))] = acc.get((int(t), int(tot)), 0) + int(n)
+    H = np.array([[t, tot, acc[(t, tot)]] for t, tot in sorted(acc)], np.int64).reshape(-1, 3)
+    return np.concatenate(keys), np.concatenate(counts), H, np.concatenate(sel), disc
+
+
+@pytest.mark.parametrize("k,G", [(11, 2), (11, 3), (19, 4), (32, 5), (3, 8)])
+def test_partition_merge_equals_oracle(k, G):
+    streams = make_streams()
+    keys, counts, H, sel, disc = _sim(streams, k, G, 3, 40)
+    ref = oracle.count_pipeline(streams, k, 3, 40)
+    assert np.array_equal(keys, ref["keys"])
+    assert np.array_equal(counts, ref["counts"])
+    assert np.array_equal(H, ref["hist"])
+    assert np.array_equal(sel, ref["selected"]) and disc == ref["n_discr"]
+
+
+def test_partition_merge_min_counts_and_empty_owner():
+    streams = make_streams(seed=3, n_reads=200)
+    for min_c in (1, 3):
+        keys, counts, _, _, _ = _sim(streams, 9, 3, 2, 10, min_c)
+        dumps = [oracle.count_stream(s, 9, min_c) for s in streams]
+        rk, rc = oracle.merge(dumps)
+        assert np.array_equal(keys, rk) and np.array_equal(counts, rc)
+    # a world larger than the distinct codes of k=1 leaves owners empty
+    keys, counts, _, _, _ = _sim(streams, 1, 6, 1, 10 ** 9)
+    rk, rc = oracle.merge([oracle.count_stream(s, 1, 2) for s in streams])
+    assert np.array_equal(keys, rk) and np.array_equal(counts, rc)
+
+
+def _worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ctx = hga.Ctx(0)
+    try:
+        streams = make_streams()
+        ctx.count_begin(13, len(streams))
+        for f, s in enumerate(streams):
+            ctx.count_add(f, hga_dist.shard_reads(s, rank, world))
+        ex = hga_dist.OwnerExchange(hga_dist.HgaEngine(ctx, 13, len(streams), "cuda:0"))
+        ex.count(2)
+        hist = ex.spec_hist(THR)
+        keys, flags = ex.select(3, 40)
+        n, d = ex.select_counts(3, 40)
+        if rank == 0:
+            np.savez(out_path, hist=hist, keys=keys, flags=flags, n=n, d=d)
+    finally:
+        ctx.close()
+        dist.destroy_process_group()
+
+
+def test_owner_exchange_two_processes(tmp_path):
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "d.npz")
+    mp.start_processes(_worker, args=(2, port, out), nprocs=2, start_method="spawn")
+    r = np.load(out)
+    ref = oracle.count_pipeline(make_streams(), 13, 3, 40)
+    assert np.array_equal(r["hist"], ref["hist"])
+    assert np.array_equal(r["keys"], ref["selected"])
+    assert int(r["n"]) == len(ref["selected"]) and int(r["d"]) == ref["n_discr"]
