@@ -41,8 +41,10 @@ def log(*a):
 
 
 def make_c2(rank):
-    ga = hga.gen_genome(LA, 1)
-    gb = hga.gen_haplotype(ga, DIV, LB - LA, 2)
+    """Rank r's shard: its own MG1655/UTI89-sized pair at 30x (rank 0 = the N=1 workload), so the
+    global genome grows with N at constant coverage (weak scaling, like SURVEY.md's C4)."""
+    ga = hga.gen_genome(LA, 1 + 1000 * rank)
+    gb = hga.gen_haplotype(ga, DIV, LB - LA, 2 + 1000 * rank)
     na, nb = COVERAGE * LA // READ_LEN, COVERAGE * LB // READ_LEN
     ra = hga.gen_art(ga, na, READ_LEN, 1000 + 2 * rank)
     rb = hga.gen_art(gb, nb, READ_LEN, 1001 + 2 * rank)
@@ -78,8 +80,16 @@ class Dist:
         if self.world > 1:
             import torch
             import torch.distributed as dist
+            # HGA_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks
+            backend = os.environ.get("HGA_BENCH_BACKEND", "nccl")
+            if backend != "nccl":
+                self.local %= max(1, torch.cuda.device_count())
             torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local}"))
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local}"))
+            else:
+                dist.init_process_group(backend)
+            self.comm_dev = f"cuda:{self.local}" if backend == "nccl" else "cpu"
             self.torch, self.dist = torch, dist
             self.pg = True
         if n != self.world and self.world > 1:
@@ -93,14 +103,14 @@ class Dist:
     def max(self, v):
         if not self.pg:
             return v
-        t = self.torch.tensor([v], dtype=self.torch.float64, device=f"cuda:{self.local}")
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.comm_dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum(self, v):
         if not self.pg:
             return v
-        t = self.torch.tensor([v], dtype=self.torch.float64, device=f"cuda:{self.local}")
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.comm_dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
