@@ -89,35 +89,46 @@ struct Blk {
 constexpr uint32_t BLK = TP_B;   // >= a tile, so a tile's run spans at most two blocks
 
 // gstat: [0] row cursor, [1] max split, [2] error bits (1 unsplittable, 2 row capacity,
-// 4 level-1 pool exhausted), [3] blocks used, [4] instances, [5] pool cursor.
+// 4 level-1 pool exhausted), [3] blocks used, [4] instances.
+// Block e always starts at e * BLK in the pool.  Workgroup w's first block of region r is
+// entry w * nb1 + r (no atomic); spill blocks are numbered from W * nb1 up (gstat[3]).
 __device__ __forceinline__ uint32_t new_block(unsigned long long* gstat, Blk* table, uint64_t table_cap,
-                                              uint64_t pool_cap, uint32_t tag, unsigned long long& start) {
-    start = atomicAdd(&gstat[5], (unsigned long long)BLK);
+                                              uint32_t tag, unsigned long long& start) {
     const unsigned long long e = atomicAdd(&gstat[3], 1ull);
-    if (start + BLK > pool_cap || e >= table_cap) {
+    if (e >= table_cap) {
         atomicOr(&gstat[2], 4ull);
-        start = pool_cap;   // writes into this block are dropped
+        start = table_cap * (unsigned long long)BLK;   // writes into this block are dropped
         return 0xFFFFFFFFu;
     }
+    start = e * (unsigned long long)BLK;
     table[e].start = start;
     table[e].used = 0;
     table[e].tag = tag;
     return (uint32_t)e;
 }
 
+// One level-1 binning launch covers every file: workgroup w belongs to file f when
+// files[f].w0 <= w < files[f+1].w0 (file-major, so per-file runs stay contiguous).
+struct BinFile {
+    const uint32_t* pk;
+    const uint16_t* vd;
+    uint64_t n;
+    uint32_t w0, pad;
+};
+
 template <class E1>
-__global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
-                                                const uint16_t* __restrict__ vd, uint64_t n,
-                                                uint64_t st_pos, uint32_t file, uint32_t F, KP kp,
+__global__ void __launch_bounds__(NT_B) kc_bin1(const BinFile* __restrict__ files, uint32_t F,
+                                                uint64_t st_pos, KP kp,
                                                 Blk* __restrict__ table, uint64_t table_cap,
                                                 uint64_t pool_cap, E1* __restrict__ out1,
-                                                unsigned long long* __restrict__ fine_hist,
+                                                uint32_t* __restrict__ wcnt, uint32_t* __restrict__ nblk,
                                                 unsigned long long* __restrict__ gstat) {
     __shared__ uint32_t cnt1[NB1_MAX];
     __shared__ uint32_t off1[NB1_MAX + 1];
     __shared__ unsigned long long bstart[NB1_MAX];   // current block of each region
     __shared__ uint32_t bfill[NB1_MAX];              // elements already in it
     __shared__ uint32_t bent[NB1_MAX];               // its table entry
+    __shared__ uint32_t nchain[NB1_MAX];             // blocks this workgroup used per region
     __shared__ unsigned long long base_a[NB1_MAX], base_b[NB1_MAX];
     __shared__ uint32_t take_a[NB1_MAX];
     __shared__ uint32_t fhist[MAX_NB];
@@ -126,31 +137,27 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
     __shared__ uint32_t ws[NT_B / 64 + 1];
     const int tid = threadIdx.x;
     const uint32_t nb1 = kp.nb1, nb = kp.nb;
+    const uint32_t w = blockIdx.x;
+    uint32_t file = 0;
+    while (file + 1 < F && files[file + 1].w0 <= w) ++file;
+    const uint32_t* __restrict__ pk = files[file].pk;
+    const uint16_t* __restrict__ vd = files[file].vd;
+    const uint64_t n = files[file].n;
+    const uint32_t tag0 = w << 8;
     for (uint32_t b = tid; b < nb; b += NT_B) fhist[b] = 0;
-    __shared__ unsigned long long s_pool0, s_ent0;
-    if (tid == 0) {   // one pair of atomics reserves this workgroup's first block of every region
-        s_pool0 = atomicAdd(&gstat[5], (unsigned long long)nb1 * BLK);
-        s_ent0 = atomicAdd(&gstat[3], (unsigned long long)nb1);
-    }
-    __syncthreads();
     if (tid < (int)nb1) {
         cnt1[tid] = 0;
-        const unsigned long long st = s_pool0 + (unsigned long long)tid * BLK, e = s_ent0 + tid;
-        if (st + BLK > pool_cap || e >= table_cap) {
-            atomicOr(&gstat[2], 4ull);
-            bent[tid] = 0xFFFFFFFFu;
-            bstart[tid] = pool_cap;
-        } else {
-            table[e].start = st;
-            table[e].used = 0;
-            table[e].tag = (file << 8) | tid;
-            bent[tid] = (uint32_t)e;
-            bstart[tid] = st;
-        }
+        const unsigned long long e = (unsigned long long)w * nb1 + tid;
+        table[e].start = e * BLK;
+        table[e].used = 0;
+        table[e].tag = tag0 | tid;
+        bent[tid] = (uint32_t)e;
+        bstart[tid] = e * BLK;
         bfill[tid] = 0;
+        nchain[tid] = 1;
     }
     __syncthreads();
-    const uint64_t start = (uint64_t)blockIdx.x * st_pos;
+    const uint64_t start = (uint64_t)(w - files[file].w0) * st_pos;
     const uint64_t end = start + st_pos < n ? start + st_pos : n;
     uint32_t inst = 0;
     for (uint64_t t0 = start; t0 < end; t0 += TP_B) {
@@ -188,7 +195,8 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
                     take_a[tid] = room;
                     if (bent[tid] != 0xFFFFFFFFu) table[bent[tid]].used = BLK;
                     unsigned long long st;
-                    bent[tid] = new_block(gstat, table, table_cap, pool_cap, (file << 8) | tid, st);
+                    bent[tid] = new_block(gstat, table, table_cap, tag0 | tid, st);
+                    ++nchain[tid];
                     bstart[tid] = st;
                     base_b[tid] = st;
                     bfill[tid] = c - room;
@@ -215,52 +223,45 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk,
         lds_barrier();
     }
     __syncthreads();
-    if (tid < (int)nb1 && bent[tid] != 0xFFFFFFFFu) table[bent[tid]].used = bfill[tid];
-    for (uint32_t b = tid; b < nb; b += NT_B) {
-        const uint32_t v = fhist[b];
-        if (v) atomicAdd(&fine_hist[(uint64_t)b * F + file], (unsigned long long)v);
+    if (tid < (int)nb1) {
+        if (bent[tid] != 0xFFFFFFFFu) table[bent[tid]].used = bfill[tid];
+        nblk[(uint64_t)w * nb1 + tid] = nchain[tid];
     }
+    for (uint32_t b = tid; b < nb; b += NT_B) wcnt[(uint64_t)w * nb + b] = fhist[b];
     uint32_t tot;
     (void)block_excl_scan<NT_B>(inst, ws, &tot);
     if (tid == 0 && tot) atomicAdd(&gstat[4], (unsigned long long)tot);
 }
 
 // ---------------------------------------------------------------- layout
-// One workgroup.  fs[b*(F+1)+f] = start of file f's run in fine bucket b (bucket-major,
-// file-minor), fs[b*(F+1)+F] = bucket end; cursor2 = copy of fs (re-bin write cursors).
-__global__ void __launch_bounds__(1024) kc_layout(const unsigned long long* __restrict__ fine_hist,
-                                                  uint32_t nb, uint32_t F, uint64_t* __restrict__ fs,
-                                                  unsigned long long* __restrict__ cursor2) {
-    __shared__ uint64_t ws[17];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t NF = (uint64_t)nb * F;
-    uint64_t carry = 0;
-    for (uint64_t r0 = 0; r0 < NF; r0 += 1024) {
-        const uint64_t i = r0 + tid;
-        const uint64_t v = i < NF ? fine_hist[i] : 0ull;
-        const uint64_t inc = wave_incl_scan64(v, lane);
-        if (lane == 63) ws[wave] = inc;
-        __syncthreads();
-        if (tid == 0) {
-            uint64_t t = 0;
-            for (int w = 0; w < 16; ++w) { const uint64_t x = ws[w]; ws[w] = t; t += x; }
-            ws[16] = t;
-        }
-        __syncthreads();
-        const uint64_t ex = ws[wave] + inc - v + carry;
-        const uint64_t tot = ws[16];
-        __syncthreads();
-        if (i < NF) {
-            const uint64_t b = i / F, f = i % F;
-            fs[b * (F + 1) + f] = ex;
-            cursor2[b * (F + 1) + f] = ex;
-            if (f == F - 1) {
-                fs[b * (F + 1) + F] = ex + v;
-                cursor2[b * (F + 1) + F] = ex + v;
-            }
-        }
-        carry += tot;
+// off[b * W + w] = wcnt[w * nb + b] (64 x 64 LDS tiles), off[nb * W] = 0.  One exclusive scan
+// of off then gives every (fine bucket, workgroup) its first output slot: buckets in order,
+// inside a bucket the workgroups in order (files are workgroup ranges, so file runs are
+// contiguous) — the re-bin needs no cursor atomics.
+__global__ void __launch_bounds__(256) kc_transpose(const uint32_t* __restrict__ wcnt, uint32_t W, uint32_t nb,
+                                                    uint64_t* __restrict__ off) {
+    __shared__ uint32_t t[64][65];
+    const uint32_t b0 = blockIdx.x * 64, w0 = blockIdx.y * 64;
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (uint32_t r = ty; r < 64; r += 4) {
+        const uint32_t w = w0 + r, b = b0 + tx;
+        t[r][tx] = (w < W && b < nb) ? wcnt[(uint64_t)w * nb + b] : 0u;
     }
+    __syncthreads();
+    for (uint32_t r = ty; r < 64; r += 4) {
+        const uint32_t b = b0 + r, w = w0 + tx;
+        if (b < nb && w < W) off[(uint64_t)b * W + w] = t[tx][r];
+    }
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) off[(uint64_t)nb * W] = 0;
+}
+
+// fs[b*(F+1)+f] = start of file f's run in fine bucket b, fs[b*(F+1)+F] = bucket end.
+__global__ void kc_fs(const uint64_t* __restrict__ off, const BinFile* __restrict__ files, uint32_t W,
+                      uint32_t nb, uint32_t F, uint64_t* __restrict__ fs) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)nb * (F + 1)) return;
+    const uint64_t b = i / (F + 1), f = i % (F + 1);
+    fs[i] = f == F ? off[(b + 1) * W] : off[b * W + files[f].w0];
 }
 
 // ---------------------------------------------------------------- pass B2
@@ -268,9 +269,9 @@ __global__ void __launch_bounds__(1024) kc_layout(const unsigned long long* __re
 // ranked through LDS so each bucket's run is one coalesced segment).
 template <class E1, class E>
 __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, const Blk* __restrict__ table,
-                                                 const unsigned long long* __restrict__ gstat,
-                                                 uint32_t F, KP kp,
-                                                 unsigned long long* __restrict__ cursor2,
+                                                 const unsigned long long* __restrict__ gstat, uint32_t W,
+                                                 KP kp, const uint32_t* __restrict__ nblk,
+                                                 unsigned long long* __restrict__ off,
                                                  E* __restrict__ out) {
     constexpr int IT = CH_R / NT_R;
     static_assert(CH_R >= (int)BLK, "a block must fit one re-bin pass");
@@ -281,10 +282,30 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
     __shared__ uint8_t sd2[CH_R];
     const int tid = threadIdx.x;
     const uint64_t blk = blockIdx.x;
-    if (blk >= gstat[3]) return;
-    const Blk bk = table[blk];
-    const uint32_t used = bk.used, file = bk.tag >> 8, d1 = bk.tag & 0xFFu;
     const uint32_t nb2 = kp.nb2;
+    const uint64_t n_first = (uint64_t)W * kp.nb1;
+    // first blocks: everything is known from the index, so the element, size and offset loads
+    // all go out together; spill blocks (rare) look themselves up
+    if (blk >= n_first && blk >= gstat[3]) return;
+    const E1* __restrict__ src = in1 + blk * BLK;
+    E1 v[IT];
+#pragma unroll
+    for (int j = 0; j < IT; ++j) v[j] = src[(uint32_t)j * NT_R + tid];
+    uint32_t w, d1;
+    if (blk < n_first) {
+        w = (uint32_t)(blk / kp.nb1);
+        d1 = (uint32_t)(blk % kp.nb1);
+    } else {
+        const uint32_t tag = table[blk].tag;
+        w = tag >> 8;
+        d1 = tag & 0xFFu;
+    }
+    const uint32_t used = table[blk].used;
+    // a workgroup's only block of a region owns the whole (bucket, workgroup) slot range;
+    // chained blocks (spills) share it atomically
+    const bool sole = nblk[(uint64_t)w * kp.nb1 + d1] == 1u;
+    const uint64_t oidx = ((((uint64_t)d1 << kp.fb2) | (uint64_t)(tid & 63)) * W) + w;
+    const unsigned long long pre = (tid < (int)nb2 && sole) ? off[oidx] : 0ull;
     if (tid < (int)nb2) cnt2[tid] = 0;
     __syncthreads();
     uint32_t dd[IT], rk[IT];
@@ -292,9 +313,8 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
         const uint32_t i = (uint32_t)j * NT_R + tid;
-        const E1 v = i < used ? in1[bk.start + i] : E1(0);
-        dd[j] = kp.fb2 ? (uint32_t)((uint64_t)v >> kp.rbits) : 0u;
-        ee[j] = (E)((uint64_t)v & kp.rmask);
+        dd[j] = kp.fb2 ? (uint32_t)((uint64_t)v[j] >> kp.rbits) : 0u;
+        ee[j] = (E)((uint64_t)v[j] & kp.rmask);
         rk[j] = i < used ? atomicAdd(&cnt2[dd[j]], 1u) : 0u;
     }
     __syncthreads();
@@ -303,8 +323,7 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
         const uint32_t inc = wave_incl_scan(c, tid);
         if (tid < (int)nb2) {
             off2[tid] = inc - c;
-            const uint64_t b = ((uint64_t)d1 << kp.fb2) | (uint64_t)tid;
-            base2[tid] = c ? atomicAdd(&cursor2[b * (F + 1) + file], (unsigned long long)c) : 0ull;
+            base2[tid] = sole ? pre : (c ? atomicAdd(&off[oidx], (unsigned long long)c) : 0ull);
         }
         if (tid == 63) off2[nb2] = inc;
     }
@@ -724,16 +743,25 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     s.buckets = kp.nb;
     const uint32_t nb = kp.nb, nb1 = kp.nb1;
 
-    // super-tiles: ~4 per CU over all files, whole tiles
-    uint64_t st_pos = total_bytes / ((uint64_t)c->num_cu * 4) + 1;
+    // super-tiles: ~2 per CU over all files (one resident wave of bin1 workgroups, so each
+    // (workgroup, region) fills about one level-1 block), whole tiles
+    uint64_t st_pos = total_bytes / ((uint64_t)c->num_cu * 2) + 1;
     st_pos = std::max<uint64_t>(ST_ALIGN, (st_pos + ST_ALIGN - 1) / ST_ALIGN * ST_ALIGN);
     std::vector<uint32_t> n_st(F, 0);
-    for (uint32_t f = 0; f < F; ++f) n_st[f] = (uint32_t)((s.seq_len[f] + st_pos - 1) / st_pos);
+    std::vector<BinFile> bf(F);
+    uint32_t W = 0;
+    for (uint32_t f = 0; f < F; ++f) {
+        n_st[f] = (uint32_t)((s.seq_len[f] + st_pos - 1) / st_pos);
+        bf[f].n = s.seq_len[f];
+        bf[f].w0 = W;
+        W += n_st[f];
+    }
 
     auto* gstat = static_cast<unsigned long long*>(s.cursor.ensure(8 * 8));
     uint64_t* fs = static_cast<uint64_t*>(s.file_start.ensure((size_t)nb * (F + 1) * 8));
-    auto* cursor2 = static_cast<unsigned long long*>(s.cursor2.ensure((size_t)nb * (F + 1) * 8));
-    auto* fine_hist = static_cast<unsigned long long*>(s.fine_hist.ensure((size_t)nb * F * 8));
+    uint32_t* wcnt = static_cast<uint32_t*>(s.fine_hist.ensure((size_t)std::max<uint32_t>(W, 1) * nb * 4));
+    auto* off = static_cast<unsigned long long*>(s.cursor2.ensure(((size_t)W * nb + 1) * 8));
+    uint32_t* nblk = static_cast<uint32_t*>(s.nblk.ensure((size_t)std::max<uint32_t>(W, 1) * nb1 * 4));
     // P: pack every file (2-bit codes + valid bits), pad words zeroed (= invalid)
     std::vector<const uint32_t*> pks(F);
     std::vector<const uint16_t*> vds(F);
@@ -759,7 +787,11 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
         }
         pks[f] = pk;
         vds[f] = vd;
+        bf[f].pk = pk;
+        bf[f].vd = vd;
     }
+    BinFile* d_bf = static_cast<BinFile*>(s.bin_files.ensure(sizeof(BinFile) * F));
+    HGA_HIP(hipMemcpyAsync(d_bf, bf.data(), sizeof(BinFile) * F, hipMemcpyHostToDevice, c->stream));
 
     const size_t esz1 = e1_32 ? 4 : 8, esz = e32 ? 4 : 8;
     const uint64_t cap = total_bytes / std::max<uint32_t>(1, min_per_file) + 1;
@@ -772,43 +804,45 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const uint32_t maxload = std::min<uint32_t>((uint32_t)(T * 0.85), T - NT_C - 8);
     void* binned = s.binned.ensure(std::max<size_t>(total_bytes, 1) * esz);
 
-    // level-1 pool: every (workgroup, region) wastes less than one block
-    uint64_t n_wg = 0;
-    for (uint32_t f = 0; f < F; ++f) n_wg += n_st[f];
-    const uint64_t pool_cap = total_bytes + n_wg * nb1 * BLK + BLK;
-    const uint64_t table_cap = pool_cap / BLK + 1;
+    // level-1 pool: one first block per (workgroup, region) + spill blocks for the worst case
+    const uint64_t n_first = (uint64_t)W * nb1;
+    const uint64_t table_cap = n_first + total_bytes / BLK + 2;
+    const uint64_t pool_cap = table_cap * BLK;
     void* binned1 = s.binned1.ensure(pool_cap * esz1);
     Blk* table = static_cast<Blk*>(s.regions.ensure(table_cap * sizeof(Blk)));
     HGA_HIP(hipMemsetAsync(gstat, 0, 8 * 8, c->stream));
-    HGA_HIP(hipMemsetAsync(fine_hist, 0, (size_t)nb * F * 8, c->stream));
+    HGA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(gstat + 3), (int)n_first, 1, c->stream));
 
-    // B1: level-1 binning into pool blocks + fine histogram + instance count
-    for (uint32_t f = 0; f < F; ++f) {
-        if (!n_st[f]) continue;
-        const uint64_t n = s.seq_len[f];
+    // B1: level-1 binning of every file into pool blocks + per-workgroup fine histograms
+    if (W) {
         c->launch("kc_bin1", [&] {
             if (e1_32)
-                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f], n,
-                                   st_pos, f, F, kp, table, table_cap, pool_cap, static_cast<uint32_t*>(binned1),
-                                   fine_hist, gstat);
+                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
+                                   table_cap, pool_cap, static_cast<uint32_t*>(binned1), wcnt, nblk, gstat);
             else
-                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(n_st[f]), dim3(NT_B), 0, c->stream, pks[f], vds[f], n,
-                                   st_pos, f, F, kp, table, table_cap, pool_cap, static_cast<uint64_t*>(binned1),
-                                   fine_hist, gstat);
+                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
+                                   table_cap, pool_cap, static_cast<uint64_t*>(binned1), wcnt, nblk, gstat);
         });
         c->check_launch("kc_bin1");
     }
-    // L: fine layout
+    // L: (bucket, workgroup) output offsets and per-file bucket runs
     c->launch("kc_layout", [&] {
-        hipLaunchKernelGGL(kc_layout, dim3(1), dim3(1024), 0, c->stream, fine_hist, nb, F, fs, cursor2);
+        hipLaunchKernelGGL(kc_transpose, dim3(blocks_for(nb, 64), blocks_for(std::max<uint32_t>(W, 1), 64)), dim3(256),
+                           0, c->stream, wcnt, W, nb, reinterpret_cast<uint64_t*>(off));
     });
-    c->check_launch("kc_layout");
-    // B2: re-bin every level-1 block into the fine buckets (persistent grid)
+    c->check_launch("kc_transpose");
+    exclusive_scan_u64(c, reinterpret_cast<uint64_t*>(off), (uint64_t)W * nb + 1, s.scratch);
+    c->launch("kc_layout", [&] {
+        hipLaunchKernelGGL(kc_fs, dim3(blocks_for((uint64_t)nb * (F + 1), 256)), dim3(256), 0, c->stream,
+                           reinterpret_cast<const uint64_t*>(off), d_bf, W, nb, F, fs);
+    });
+    c->check_launch("kc_fs");
+    // B2: re-bin every level-1 block into the fine buckets
     const unsigned rebin_grid = (unsigned)std::max<uint64_t>(1, table_cap);   // exits past gstat[3]
     c->launch("kc_rebin", [&] {
 #define HGA_REBIN(E1T, ET)                                                                                 \
     hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3(rebin_grid), dim3(NT_R), 0, c->stream,                    \
-                       static_cast<const E1T*>(binned1), table, gstat, F, kp, cursor2, static_cast<ET*>(binned))
+                       static_cast<const E1T*>(binned1), table, gstat, W, kp, nblk, off, static_cast<ET*>(binned))
         if (e1_32 && e32) HGA_REBIN(uint32_t, uint32_t);
         else if (e32) HGA_REBIN(uint64_t, uint32_t);
         else if (e1_32) HGA_REBIN(uint32_t, uint64_t);

@@ -103,7 +103,7 @@ struct CountState {
     std::vector<DevBuf*> packed, valid;   // 2-bit codes / valid bits per file (kc_pack)
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
-        sel_keys, sel_tmp, hist_dense, hist_comp, xch, xch2;
+        sel_keys, sel_tmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t buckets = 0, fb = 0, max_split = 1;
