@@ -34,15 +34,28 @@ constexpr int NT_B = 512;     // level-1 binning workgroup
 constexpr int P_B = 16;       // window ends per thread
 constexpr int TP_B = NT_B * P_B;       // 8192 window ends per tile
 constexpr uint64_t ST_ALIGN = TP_B;    // super-tiles are whole tiles
-constexpr int MAX_FB = 12;
+#ifndef HGA_MAX_FB
+#define HGA_MAX_FB 12
+#endif
+#ifndef HGA_NT_C
+#define HGA_NT_C 1024
+#endif
+#ifndef HGA_LDS_TAB_KB
+#define HGA_LDS_TAB_KB 128
+#endif
+constexpr int MAX_FB = HGA_MAX_FB;
 constexpr int MAX_NB = 1 << MAX_FB;
 constexpr int MAX_FB1 = 6;    // level-1 fan-out <= 64
 constexpr int NB1_MAX = 1 << MAX_FB1;
+constexpr int NB2_MAX = 1 << (MAX_FB - MAX_FB1 > 6 ? MAX_FB - MAX_FB1 : 6);   // level-2 fan-out
 constexpr int NT_R = 512;     // re-bin workgroup
 constexpr int CH_R = NT_R * 16;        // 8192 elements per re-bin chunk
-constexpr int NT_C = 1024;    // threads of the per-bucket count workgroup
-constexpr int PF_C = 8;       // binned elements each count thread has in flight
-constexpr uint32_t LDS_TAB = 128 * 1024;
+constexpr int NT_C = HGA_NT_C;   // threads of the per-bucket count workgroup
+#ifndef HGA_PF_C
+#define HGA_PF_C 8
+#endif
+constexpr int PF_C = HGA_PF_C;   // binned elements each count thread has in flight
+constexpr uint32_t LDS_TAB = HGA_LDS_TAB_KB * 1024;
 
 struct KP {
     int k, sh;
@@ -110,14 +123,15 @@ __device__ __forceinline__ uint32_t new_block(unsigned long long* gstat, Blk* ta
 // One level-1 binning launch covers every file: workgroup w belongs to file f when
 // files[f].w0 <= w < files[f+1].w0 (file-major, so per-file runs stay contiguous).
 struct BinFile {
-    const uint32_t* pk;
-    const uint16_t* vd;
-    uint64_t n;
+    uint64_t woff;   // first word of the file's region in the packed buffers
+    uint64_t n;      // bases
     uint32_t w0, pad;
 };
 
 template <class E1>
-__global__ void __launch_bounds__(NT_B) kc_bin1(const BinFile* __restrict__ files, uint32_t F,
+__global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk_all,
+                                                const uint16_t* __restrict__ vd_all,
+                                                const BinFile* __restrict__ files, uint32_t F,
                                                 uint64_t st_pos, KP kp,
                                                 Blk* __restrict__ table, uint64_t table_cap,
                                                 uint64_t pool_cap, E1* __restrict__ out1,
@@ -140,8 +154,8 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const BinFile* __restrict__ file
     const uint32_t w = blockIdx.x;
     uint32_t file = 0;
     while (file + 1 < F && files[file + 1].w0 <= w) ++file;
-    const uint32_t* __restrict__ pk = files[file].pk;
-    const uint16_t* __restrict__ vd = files[file].vd;
+    const uint32_t* __restrict__ pk = pk_all + files[file].woff;
+    const uint16_t* __restrict__ vd = vd_all + files[file].woff;
     const uint64_t n = files[file].n;
     const uint32_t tag0 = w << 8;
     for (uint32_t b = tid; b < nb; b += NT_B) fhist[b] = 0;
@@ -275,9 +289,10 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
                                                  E* __restrict__ out) {
     constexpr int IT = CH_R / NT_R;
     static_assert(CH_R >= (int)BLK, "a block must fit one re-bin pass");
-    __shared__ uint32_t cnt2[NB1_MAX];
-    __shared__ uint32_t off2[NB1_MAX + 1];
-    __shared__ unsigned long long base2[NB1_MAX];
+    __shared__ uint32_t cnt2[NB2_MAX];
+    __shared__ uint32_t off2[NB2_MAX + 1];
+    __shared__ unsigned long long base2[NB2_MAX];
+    __shared__ uint32_t s_w0;
     __shared__ E stage[CH_R];
     __shared__ uint8_t sd2[CH_R];
     const int tid = threadIdx.x;
@@ -304,7 +319,7 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
     // a workgroup's only block of a region owns the whole (bucket, workgroup) slot range;
     // chained blocks (spills) share it atomically
     const bool sole = nblk[(uint64_t)w * kp.nb1 + d1] == 1u;
-    const uint64_t oidx = ((((uint64_t)d1 << kp.fb2) | (uint64_t)(tid & 63)) * W) + w;
+    const uint64_t oidx = ((((uint64_t)d1 << kp.fb2) | (uint64_t)(tid & (NB2_MAX - 1))) * W) + w;
     const unsigned long long pre = (tid < (int)nb2 && sole) ? off[oidx] : 0ull;
     if (tid < (int)nb2) cnt2[tid] = 0;
     __syncthreads();
@@ -318,14 +333,20 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
         rk[j] = i < used ? atomicAdd(&cnt2[dd[j]], 1u) : 0u;
     }
     __syncthreads();
-    if (tid < 64) {
-        const uint32_t c = tid < (int)nb2 ? cnt2[tid] : 0u;
-        const uint32_t inc = wave_incl_scan(c, tid);
+    uint32_t c2 = 0, inc2 = 0;
+    if (tid < NB2_MAX) {   // two waves scan the <= 128 digit counts
+        c2 = tid < (int)nb2 ? cnt2[tid] : 0u;
+        inc2 = wave_incl_scan(c2, tid & 63);
+        if (tid == 63) s_w0 = inc2;
+    }
+    __syncthreads();
+    if (tid < NB2_MAX) {
+        if (tid >= 64) inc2 += s_w0;
         if (tid < (int)nb2) {
-            off2[tid] = inc - c;
-            base2[tid] = sole ? pre : (c ? atomicAdd(&off[oidx], (unsigned long long)c) : 0ull);
+            off2[tid] = inc2 - c2;
+            base2[tid] = sole ? pre : (c2 ? atomicAdd(&off[oidx], (unsigned long long)c2) : 0ull);
         }
-        if (tid == 63) off2[nb2] = inc;
+        if (tid == NB2_MAX - 1) off2[nb2] = inc2;
     }
     __syncthreads();
 #pragma unroll
@@ -348,17 +369,85 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
 // ---------------------------------------------------------------- pass C
 // LDS table: T slots in T/4 groups of 4 (one ds_read_b128 per probe for u32 keys), keys
 // SoA with one u32 counter per file per slot.  A key's home group is its low bits.
+#ifndef HGA_GROUP
+#define HGA_GROUP 4
+#endif
+constexpr int GRP = HGA_GROUP;   // slots per probe group (4: one ds_read_b128 of u32 keys)
 template <class E>
-__device__ __forceinline__ void read_group(const E* keys, uint32_t g, E (&k)[4]) {
+__device__ __forceinline__ void read_group(const E* keys, uint32_t g, E (&k)[GRP]) {
     if constexpr (sizeof(E) == 4) {
-        const uint4 v = reinterpret_cast<const uint4*>(keys)[g];
-        k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
+#pragma unroll
+        for (int t = 0; t < GRP / 4; ++t) {
+            const uint4 v = reinterpret_cast<const uint4*>(keys)[g * (GRP / 4) + t];
+            k[4 * t] = v.x; k[4 * t + 1] = v.y; k[4 * t + 2] = v.z; k[4 * t + 3] = v.w;
+        }
     } else {
-        const ulonglong2 a = reinterpret_cast<const ulonglong2*>(keys)[2 * g];
-        const ulonglong2 b = reinterpret_cast<const ulonglong2*>(keys)[2 * g + 1];
-        k[0] = a.x; k[1] = a.y; k[2] = b.x; k[3] = b.y;
+#pragma unroll
+        for (int t = 0; t < GRP / 2; ++t) {
+            const ulonglong2 a = reinterpret_cast<const ulonglong2*>(keys)[g * (GRP / 2) + t];
+            k[2 * t] = a.x; k[2 * t + 1] = a.y;
+        }
     }
 }
+
+// One probe step for key r at group g: count it if present, claim an empty slot if the group
+// has one, else move to the next group.  r becomes EMPTY once settled (or dropped because the
+// table is over its load limit, in which case the whole sub-range is redone after a split).
+template <class E>
+__device__ __forceinline__ bool count_step(E* keys, uint32_t* cf, uint32_t G, uint32_t& s_ovf, E& r,
+                                           uint32_t& g) {
+    const E EMPTY = ~E(0);
+    E kg[GRP];
+    read_group(keys, g, kg);
+    int w = -1, e0 = -1;
+#pragma unroll
+    for (int t = GRP - 1; t >= 0; --t) {
+        w = kg[t] == r ? t : w;
+        e0 = kg[t] == EMPTY ? t : e0;
+    }
+    if (w >= 0) {
+        atomicAdd(&cf[GRP * g + w], 1u);
+        r = EMPTY;
+    } else if (e0 >= 0) {
+        if (__atomic_load_n(&s_ovf, __ATOMIC_RELAXED)) {
+            r = EMPTY;
+        } else {
+            const uint32_t sl = GRP * g + (uint32_t)e0;
+            const E old = atomicCAS(&keys[sl], EMPTY, r);
+            if (old == EMPTY || old == r) {
+                atomicAdd(&cf[sl], 1u);
+                r = EMPTY;
+                return old == EMPTY;
+            }   // else: lost the slot to another key, re-read the group
+        }
+    } else {
+        g = (g + 1) & (G - 1);
+    }
+    return false;
+}
+
+// Occupancy is accounted once per wave and probe iteration (at most 64 new keys), so the
+// table can exceed maxload by at most (waves x 64) before s_ovf stops insertions; the host
+// keeps maxload + NT_C below T, so a probe always finds an empty slot.
+__device__ __forceinline__ void count_occupancy(bool ins, uint32_t& s_occ, uint32_t& s_ovf, uint32_t maxload) {
+    const uint64_t bal = __ballot(ins);
+    if (bal && (threadIdx.x & 63) == 0) {
+        const uint32_t n = (uint32_t)__popcll(bal);
+        const uint32_t o = atomicAdd(&s_occ, n);
+        if (o + n >= maxload) __atomic_store_n(&s_ovf, 1u, __ATOMIC_RELAXED);
+    }
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    return (1ull << (threadIdx.x & 63)) - 1ull;
+}
+
+constexpr uint32_t QN_C = 128;   // miss-queue entries per wave
+#ifndef HGA_EMIT_STAGE
+#define HGA_EMIT_STAGE 1
+#endif
+constexpr int EMIT_F = 4;        // files handled by the LDS-staged emit
+constexpr int EMIT_S = 8;        // slots per thread in it (T == NT_C * EMIT_S)
 
 // gstat: [0] output cursor, [1] max sub-ranges any bucket needed, [2] error bits
 // (1 = unsplittable overflow, 2 = output capacity exceeded, 4 = level-1 overflow).
@@ -374,7 +463,10 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
     __shared__ uint32_t stk_lo[40], stk_hi[40];
     __shared__ uint32_t ws[NT_C / 64 + 1];
     __shared__ unsigned long long s_base;
+    __shared__ E qbuf[NT_C / 64][QN_C];
     E* keys = reinterpret_cast<E*>(smem);
+    const uint32_t lane = threadIdx.x & 63;
+    E* myq = qbuf[threadIdx.x >> 6];
     uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + (size_t)T * sizeof(E));
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;
@@ -384,7 +476,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
     const uint32_t SUBB = rbits < 16 ? rbits : 16;
     const uint32_t full_hi = 1u << SUBB;
     const uint32_t mc = min_count ? min_count : 1u;
-    const uint32_t G = T / 4;
+    const uint32_t G = T / GRP;
     if (tid == 0) {
         stk_lo[0] = 0;
         stk_hi[0] = full_hi;
@@ -409,34 +501,84 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
         for (uint32_t ff = 0; ff < F; ++ff) {
             const uint64_t a = f[ff], e = f[ff + 1];
             uint32_t* cf = cnt + (size_t)ff * T;
-            for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)NT_C * PF_C) {
-                E rv[PF_C];   // PF_C loads in flight per thread
+            constexpr uint64_t STEP = (uint64_t)NT_C * PF_C;
+            if (a == e) continue;
+            // full batches load from a uniform base (scalar address + lane offset, no bounds);
+            // only the last, partial batch checks bounds.  The next batch is in flight while
+            // this one is counted.
+            const uint64_t nfull = (e - a) / STEP;
+            E nx[PF_C];
+            auto load = [&](uint64_t i0, uint64_t bi) {
+                if (bi < nfull) {
+                    const E* __restrict__ bp = binned + i0;
 #pragma unroll
-                for (int q = 0; q < PF_C; ++q) {
-                    const uint64_t i = i0 + (uint64_t)q * NT_C + tid;
-                    rv[q] = i < e ? binned[i] : EMPTY;
+                    for (int q = 0; q < PF_C; ++q) nx[q] = bp[q * NT_C + tid];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < PF_C; ++q) {
+                        const uint64_t i = i0 + (uint64_t)q * NT_C + tid;
+                        nx[q] = i < e ? binned[i] : EMPTY;
+                    }
                 }
-                // 1) all home groups read before any is consumed: one LDS round trip settles
-                //    every element whose key already sits in its home group
+            };
+            load(a, 0);
+            uint64_t bi = 0;
+            for (uint64_t i0 = a; i0 < e; i0 += STEP, ++bi) {
+                E rv[PF_C];
+#pragma unroll
+                for (int q = 0; q < PF_C; ++q) rv[q] = nx[q];
+                if (i0 + STEP < e) load(i0 + STEP, bi + 1);
+                if (filt) {
+#pragma unroll
+                    for (int q = 0; q < PF_C; ++q) {
+                        const uint32_t sk = SUBB ? (uint32_t)(rv[q] >> (rbits - SUBB)) : 0u;
+                        rv[q] = (sk >= lo && sk < hi) ? rv[q] : EMPTY;
+                    }
+                }
+                // 1) every home group read before any counter is touched (the counters share
+                //    the LDS array, so an atomic in between would serialise the reads): one LDS
+                //    round trip settles every element whose key already sits in its home group
+                E kg[PF_C][GRP];
+#pragma unroll
+                for (int q = 0; q < PF_C; ++q) read_group(keys, (uint32_t)rv[q] & (G - 1), kg[q]);
                 uint32_t miss = 0;
 #pragma unroll
                 for (int q = 0; q < PF_C; ++q) {
-                    bool live = rv[q] != EMPTY;
-                    if (filt && live) {
-                        const uint32_t sk = SUBB ? (uint32_t)(rv[q] >> (rbits - SUBB)) : 0u;
-                        live = sk >= lo && sk < hi;
-                    }
                     const uint32_t g = (uint32_t)rv[q] & (G - 1);
-                    E kg[4];
-                    read_group(keys, g, kg);
                     int w = -1;
 #pragma unroll
-                    for (int t = 3; t >= 0; --t) w = kg[t] == rv[q] ? t : w;
-                    if (live && w >= 0) atomicAdd(&cf[4 * g + w], 1u);
+                    for (int t = GRP - 1; t >= 0; --t) w = kg[q][t] == rv[q] ? t : w;
+                    const bool live = rv[q] != EMPTY;   // EMPTY would match an empty slot
+                    if (live && w >= 0) atomicAdd(&cf[GRP * g + w], 1u);
                     else if (live) miss |= 1u << q;
                 }
-                // 2) the rest (new keys, keys displaced from their home group): one probe
-                //    step per lane per iteration; a lane takes its next miss when settled
+                // the misses (new keys, keys displaced from home) are compacted into this
+                // wave's queue once per batch
+                const uint32_t nm = (uint32_t)__popc(miss);
+                const uint32_t incl = wave_incl_scan(nm, (int)lane);
+                const uint32_t qn = __shfl(incl, 63);
+                uint32_t pos = incl - nm;
+                while (miss && pos < QN_C) {
+                    const int q = __builtin_ctz(miss);
+                    miss &= miss - 1u;
+                    E pick = rv[0];
+#pragma unroll
+                    for (int t = 1; t < PF_C; ++t) pick = q == t ? rv[t] : pick;
+                    myq[pos++] = pick;
+                }
+                __builtin_amdgcn_wave_barrier();
+                // 2) the queue, 64 misses at a time with every lane busy, one probe step per
+                //    iteration; then the (rare) queue overflow, lane by lane
+                const uint32_t nq = qn < QN_C ? qn : QN_C;
+                for (uint32_t q0 = 0; q0 < nq; q0 += 64) {
+                    E r = q0 + lane < nq ? myq[q0 + lane] : EMPTY;
+                    uint32_t g = (uint32_t)r & (G - 1);
+                    while (__any(r != EMPTY)) {
+                        const bool ins = r != EMPTY && count_step(keys, cf, G, s_ovf, r, g);
+                        count_occupancy(ins, s_occ, s_ovf, maxload);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
                 E r = EMPTY;
                 uint32_t g = 0;
                 while (__any(miss != 0u || r != EMPTY)) {
@@ -449,39 +591,10 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                         r = pick;
                         g = (uint32_t)r & (G - 1);
                     }
-                    if (r != EMPTY) {
-                        E kg[4];
-                        read_group(keys, g, kg);
-                        int w = -1, e0 = -1;
-#pragma unroll
-                        for (int t = 3; t >= 0; --t) {
-                            w = kg[t] == r ? t : w;
-                            e0 = kg[t] == EMPTY ? t : e0;
-                        }
-                        if (w >= 0) {
-                            atomicAdd(&cf[4 * g + w], 1u);
-                            r = EMPTY;
-                        } else if (e0 >= 0) {
-                            if (*(volatile uint32_t*)&s_ovf) {
-                                r = EMPTY;   // this sub-range is redone after the split
-                            } else {
-                                const uint32_t sl = 4 * g + (uint32_t)e0;
-                                const E old = atomicCAS(&keys[sl], EMPTY, r);
-                                if (old == EMPTY || old == r) {
-                                    if (old == EMPTY) {
-                                        const uint32_t o = atomicAdd(&s_occ, 1u);
-                                        if (o + 1 >= maxload) s_ovf = 1;
-                                    }
-                                    atomicAdd(&cf[sl], 1u);
-                                    r = EMPTY;
-                                }   // else: lost the slot to another key, re-read the group
-                            }
-                        } else {
-                            g = (g + 1) & (G - 1);   // group full: next group
-                        }
-                    }
+                    const bool ins = r != EMPTY && count_step(keys, cf, G, s_ovf, r, g);
+                    count_occupancy(ins, s_occ, s_ovf, maxload);
                 }
-                if (*(volatile uint32_t*)&s_ovf) break;
+                if (__atomic_load_n(&s_ovf, __ATOMIC_RELAXED)) break;
             }
         }
         __syncthreads();
@@ -502,6 +615,58 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
             continue;
         }
         // emit the rows of this sub-range
+        if (HGA_EMIT_STAGE && F <= EMIT_F && T == (uint32_t)NT_C * EMIT_S) {
+            // each thread owns EMIT_S consecutive slots: rows are compacted through LDS (in
+            // place, after everyone has read its slots) and then written out coalesced
+            E rk[EMIT_S];
+            uint32_t rc[EMIT_S][EMIT_F];
+            uint32_t keep = 0;
+#pragma unroll
+            for (int j = 0; j < EMIT_S; ++j) {
+                const uint32_t i = (uint32_t)tid * EMIT_S + j;
+                rk[j] = keys[i];
+                bool any = false;
+#pragma unroll
+                for (int ff = 0; ff < EMIT_F; ++ff) {
+                    const uint32_t c = ff < (int)F ? cnt[(size_t)ff * T + i] : 0u;
+                    rc[j][ff] = c >= mc ? c : 0u;
+                    any |= c >= mc;
+                }
+                if (rk[j] != EMPTY && any) keep |= 1u << j;
+            }
+            uint32_t tot;
+            const uint32_t ex = block_excl_scan<NT_C>((uint32_t)__popc(keep), ws, &tot);
+            if (tid == 0) {
+                s_base = tot ? atomicAdd(&gstat[0], (unsigned long long)tot) : 0ull;
+                ++s_ranges;
+            }
+            __syncthreads();   // every slot read: the table space becomes the staging area
+            E* sk = keys;
+            uint32_t* sc = reinterpret_cast<uint32_t*>(smem + (size_t)T * sizeof(E));
+            uint32_t o = ex;
+#pragma unroll
+            for (int j = 0; j < EMIT_S; ++j)
+                if ((keep >> j) & 1u) {
+                    sk[o] = rk[j];
+#pragma unroll
+                    for (int ff = 0; ff < EMIT_F; ++ff)
+                        if (ff < (int)F) sc[(size_t)ff * T + o] = rc[j][ff];
+                    ++o;
+                }
+            __syncthreads();
+            const uint64_t base = s_base;
+            if (base + tot > cap) {
+                if (tid == 0 && tot) atomicOr(&gstat[2], 2ull);
+            } else {
+                const uint64_t hb = kp.fb ? ((uint64_t)b << rbits) : 0ull;
+                for (uint32_t j = tid; j < tot; j += NT_C) {
+                    out_key[base + j] = mix_inv(hb | (uint64_t)sk[j], kp.mix);
+                    for (uint32_t ff = 0; ff < F; ++ff) out_cnt[(size_t)ff * cap + base + j] = sc[(size_t)ff * T + j];
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         uint32_t mine = 0;
         for (uint32_t i = tid; i < T; i += NT_C) {
             if (keys[i] == EMPTY) continue;
@@ -723,7 +888,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     kp.mask = s.k >= 32 ? ~0ull : ((1ull << (2 * s.k)) - 1);
     kp.mix = make_mix(s.k);
     const uint32_t nbits = 2u * (uint32_t)s.k;
-    // fan-out: ~16K windows per fine bucket, at most 4096 buckets, never more bits than the key
+    // fan-out: ~16K windows per fine bucket, at most 8192 buckets, never more bits than the key
     uint32_t fb = 0, fb_max = MAX_FB;
     if (const char* e = std::getenv("HGA_FB_MAX")) fb_max = std::min<uint32_t>(MAX_FB, (uint32_t)std::atoi(e));
     while (fb < fb_max && fb < nbits && (total_bytes >> fb) > 16384) ++fb;
@@ -762,17 +927,18 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     uint32_t* wcnt = static_cast<uint32_t*>(s.fine_hist.ensure((size_t)std::max<uint32_t>(W, 1) * nb * 4));
     auto* off = static_cast<unsigned long long*>(s.cursor2.ensure(((size_t)W * nb + 1) * 8));
     uint32_t* nblk = static_cast<uint32_t*>(s.nblk.ensure((size_t)std::max<uint32_t>(W, 1) * nb1 * 4));
-    // P: pack every file (2-bit codes + valid bits), pad words zeroed (= invalid)
-    std::vector<const uint32_t*> pks(F);
-    std::vector<const uint16_t*> vds(F);
+    // P: pack every file (2-bit codes + valid bits) into one buffer (one kernel argument, so
+    // kc_bin1's loads stay global loads), each file [pad | words | tail], pad/tail zero (= invalid)
     const uint64_t tail_words = ST_ALIGN / 16 + 8;
-    while (s.packed.size() < F) { s.packed.push_back(new DevBuf()); s.valid.push_back(new DevBuf()); }
+    std::vector<uint64_t> woff(F + 1, 0);
+    for (uint32_t f = 0; f < F; ++f) woff[f + 1] = woff[f] + PAD_WORDS + (s.seq_len[f] + 15) / 16 + tail_words;
+    uint32_t* pk_all = static_cast<uint32_t*>(s.pk_all.ensure(woff[F] * 4));
+    uint16_t* vd_all = static_cast<uint16_t*>(s.vd_all.ensure(woff[F] * 2));
     for (uint32_t f = 0; f < F; ++f) {
         const uint64_t n = s.seq_len[f];
         const uint64_t nw = (n + 15) / 16;
-        const uint64_t alloc = PAD_WORDS + nw + tail_words;
-        uint32_t* pk = static_cast<uint32_t*>(s.packed[f]->ensure(alloc * 4));
-        uint16_t* vd = static_cast<uint16_t*>(s.valid[f]->ensure(alloc * 2));
+        uint32_t* pk = pk_all + woff[f];
+        uint16_t* vd = vd_all + woff[f];
         HGA_HIP(hipMemsetAsync(vd, 0, PAD_WORDS * 2, c->stream));
         HGA_HIP(hipMemsetAsync(vd + PAD_WORDS + nw, 0, tail_words * 2, c->stream));
         HGA_HIP(hipMemsetAsync(pk, 0, PAD_WORDS * 4, c->stream));
@@ -785,10 +951,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
             });
             c->check_launch("kc_pack");
         }
-        pks[f] = pk;
-        vds[f] = vd;
-        bf[f].pk = pk;
-        bf[f].vd = vd;
+        bf[f].woff = woff[f];
     }
     BinFile* d_bf = static_cast<BinFile*>(s.bin_files.ensure(sizeof(BinFile) * F));
     HGA_HIP(hipMemcpyAsync(d_bf, bf.data(), sizeof(BinFile) * F, hipMemcpyHostToDevice, c->stream));
@@ -817,10 +980,10 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     if (W) {
         c->launch("kc_bin1", [&] {
             if (e1_32)
-                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
+                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(W), dim3(NT_B), 0, c->stream, pk_all, vd_all, d_bf, F, st_pos, kp, table,
                                    table_cap, pool_cap, static_cast<uint32_t*>(binned1), wcnt, nblk, gstat);
             else
-                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
+                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(W), dim3(NT_B), 0, c->stream, pk_all, vd_all, d_bf, F, st_pos, kp, table,
                                    table_cap, pool_cap, static_cast<uint64_t*>(binned1), wcnt, nblk, gstat);
         });
         c->check_launch("kc_bin1");

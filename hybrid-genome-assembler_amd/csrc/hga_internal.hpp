@@ -100,17 +100,14 @@ struct CountState {
     // per-file resident sequence bytes
     std::vector<DevBuf*> seq;
     std::vector<uint64_t> seq_len;
-    std::vector<DevBuf*> packed, valid;   // 2-bit codes / valid bits per file (kc_pack)
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
-        sel_keys, sel_tmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files;
+        sel_keys, sel_tmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, pk_all, vd_all;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t buckets = 0, fb = 0, max_split = 1;
     ~CountState() {
         for (auto* b : seq) delete b;
-        for (auto* b : packed) delete b;
-        for (auto* b : valid) delete b;
     }
 };
 

@@ -114,7 +114,7 @@ def lib():
     """The HIP library (lib/libhga.so).  Raises if it was not built."""
     global _lib
     if _lib is None:
-        path = os.path.join(LIB_DIR, "libhga.so")
+        path = os.environ.get("HGA_LIB") or os.path.join(LIB_DIR, "libhga.so")   # HGA_LIB: tuning variants
         if not os.path.exists(path):
             raise HgaError(f"{path} missing: build it with `make -C hybrid-genome-assembler_amd`")
         _lib = C.CDLL(path)
