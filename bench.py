@@ -280,7 +280,7 @@ def main():
         dtl = D.max((time.perf_counter() - t0) / reps)
         s = ctx2.lookup_sizes()
         lk = {}
-        for name in ("lk_count", "lk_emit", "lk_post", "radix_upsweep", "radix_downsweep", "scan"):
+        for name in ("lk_count", "lk_emit", "lk_post", "lk_sort", "radix_upsweep", "radix_downsweep", "scan"):
             ms, n = ctx2.profile_get(name)
             if n:
                 lk[name] = round(ms / reps, 4)

@@ -113,10 +113,10 @@ struct CountState {
 
 struct LookupState {
     bool loaded = false, have_reads = false, ran = false;
-    int k = 0;
+    int k = 0, km = 0;
     uint32_t n_sdk = 0;
-    uint64_t slots = 0, fwords = 0, pk_words = 0;
-    DevBuf tab_key, tab_id, filter, packed, valid, starts;
+    uint64_t slots = 0, fwords = 0, pk_words = 0;   // slots = table buckets
+    DevBuf tab_key, tab_id, filter, packed, valid, starts, word_read, win_kid;
     uint64_t n_reads = 0, n_bases = 0;
     uint32_t first_read_id = 1;
     DevBuf bases, offsets;

@@ -5,16 +5,18 @@
 //                 contributes 0 to both strands, KmerIterator.cpp:7-19,54-63) + valid bits.
 //   lk_starts     read-start bitmap (1 bit per base): a window is in one read iff no read
 //                 starts inside (start, end].
-//   lk_build      bucketised read-only table {canonical code -> KmerID} (8 keys per 64-B
-//                 line) and a blocked Bloom filter (one u64 per key, ~11 bits/key) small
-//                 enough to stay in every XCD's L2.  KmerIDs come from the host
-//                 (std::unordered_set order, ReadClusteringEngine.cpp:237-241).
-//   lk_scan<0>    32 window ends per thread from packed frames: closed-form canonical
-//                 codes, filter, table probe on filter pass; per-thread hit mask + tile counts.
-//   lk_scan<1>    threads with hits re-probe only their hits and write (read, KmerID,
-//                 end-exclusive position) at block-scanned offsets: read / window order.
-//   post          CSR pointers, stable radix sorts for the per-read sorted KmerID lists
-//                 (:272) and first positions (:267), and kmer_component_index (:282-284).
+//   lk_build      read-only table {canonical code -> KmerID}, 5 keys + 5 ids per 64-B bucket,
+//                 and a minimizer-blocked Bloom filter (16-B block per minimizer, 3 bits per
+//                 key in one word, 2 MiB at C3) small enough to stay in every XCD's L2.
+//                 KmerIDs come from the host (std::unordered_set order,
+//                 ReadClusteringEngine.cpp:237-241).
+//   lk_scan<0>    32 window ends per thread from packed frames: closed-form canonical codes,
+//                 minimizers, one filter block per minimizer run; passing windows are queued
+//                 per wave and probed with all lanes busy; KmerIDs kept per window slot.
+//   lk_scan<1>    threads with hits copy their KmerIDs to (read, KmerID, end-exclusive
+//                 position) at block-scanned offsets: read / window order.
+//   post          CSR pointers, per-read LDS sorts for the sorted KmerID lists (:272) and
+//                 first positions (:267), stable radix sort for kmer_component_index (:282-284).
 #include <algorithm>
 
 #include "hga_internal.hpp"
@@ -23,70 +25,159 @@
 namespace hga {
 namespace {
 
+#ifndef HGA_FBITS2
+#define HGA_FBITS2 22
+#endif
 constexpr int LK_T = 256;
 constexpr int LK_P = 32;                  // window ends per thread (frame of 4 words)
+constexpr int LK_QN = 256;                // filter-pass queue entries per wave
 constexpr uint64_t EMPTY_KEY = ~0ull;     // never canonical: min(fwd, rc) of all-T is 0
-constexpr int BKT = 8;                    // keys per table bucket (one 64-B line)
 constexpr int SB_PAD = 1;                 // leading zero words of the read-start bitmap
 
+// Table: buckets of one 64-B line = 5 keys + their 5 KmerIDs, so a probe is one line read
+// (no dependent id load).  Bucket = multiply-shift of 32 hash bits (any bucket count).
+constexpr int BKT = 5;
+struct alignas(64) Bucket {
+    uint64_t key[BKT];
+    uint32_t id[BKT];
+    uint32_t pad;
+};
+static_assert(sizeof(Bucket) == 64, "one line per bucket");
+
+// One 64-bit multiply + xorshift: filter bits from bits 40..58, table bucket from bits 24..55.
 __device__ __forceinline__ uint64_t tab_hash(uint64_t x) {
-    x ^= x >> 29;
-    x *= 0xBF58476D1CE4E5B9ull;
-    x ^= x >> 32;
-    x *= 0x94D049BB133111EBull;
-    x ^= x >> 31;
-    return x;
+    const uint64_t m = x * 0x9E3779B97F4A7C15ull;
+    return m ^ (m >> 31);
 }
-__device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
-    return (1ull << ((h >> 40) & 63)) | (1ull << ((h >> 46) & 63)) | (1ull << ((h >> 52) & 63)) |
-           (1ull << ((h >> 58) & 63));
+__device__ __forceinline__ uint64_t bucket_of(uint64_t h, uint64_t nbk) {
+    return (((h >> 24) & 0xFFFFFFFFull) * nbk) >> 32;
+}
+// Blocked Bloom filter bits: three bits of one 32-bit word.
+__device__ __forceinline__ uint32_t bloom_bits(uint64_t h) {
+    const uint32_t x = (uint32_t)(h >> 40);
+    return (1u << (x & 31)) | (1u << ((x >> 5) & 31)) | (1u << ((x >> 10) & 31));
 }
 
-__global__ void lk_fill(uint64_t* __restrict__ k, uint64_t n) {
+// Minimizer-blocked filter: a key's 16-B block (4 words) is picked by the smallest hash of its
+// canonical m-mers (m = k - KM), the word inside it and the three bits by the k-mer hash.  The
+// canonical m-mer set of a k-mer equals that of its reverse complement, so the block is a
+// function of the canonical k-mer; consecutive windows of a read share minimizers, so a
+// thread's 32 windows load a few filter blocks instead of 32 (the scan is bound by the L2
+// request rate, not by bytes).  Only used for ACGT-only windows (see lk_scan).
+#ifndef HGA_KM_MINK
+#define HGA_KM_MINK 15
+#endif
+constexpr int LK_KM = 7;   // m = k - 7 for k >= 15 (seven m-mers per window); k < 15: plain hashing
+__device__ __forceinline__ uint64_t revcomp_code(uint64_t x, int m) {
+    uint64_t y = ~x;                                           // complement: c -> 3 - c
+    y = __builtin_bitreverse64(y);                             // reverse bits (and each pair)
+    y = ((y >> 1) & 0x5555555555555555ull) | ((y & 0x5555555555555555ull) << 1);   // fix pairs
+    return y >> (64 - 2 * m);
+}
+__device__ __forceinline__ uint32_t mmer_hash(uint64_t canon_m) {
+    return (uint32_t)((canon_m * 0x9E3779B97F4A7C15ull) >> 32);
+}
+__device__ __forceinline__ uint64_t filter_word(uint32_t minh, uint64_t h, uint64_t fmask) {
+    return ((((uint64_t)minh) << 2) | ((h >> 56) & 3u)) & fmask;
+}
+// Build side: the minimizer hash of canonical k-mer x.
+__device__ __forceinline__ uint32_t key_minimizer(uint64_t x, int k, int km) {
+    const int m = k - km;
+    const uint64_t mm = m >= 32 ? ~0ull : ((1ull << (2 * m)) - 1);
+    uint32_t best = 0xFFFFFFFFu;
+    for (int i = 0; i <= km; ++i) {
+        const uint64_t fm = (x >> (2 * (km - i))) & mm;
+        const uint64_t rm = revcomp_code(fm, m);
+        const uint32_t hh = mmer_hash(fm < rm ? fm : rm);
+        best = hh < best ? hh : best;
+    }
+    return best;
+}
+
+__global__ void lk_fill(Bucket* __restrict__ t, uint64_t nbk) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) k[i] = EMPTY_KEY;
+    if (i >= nbk * BKT) return;
+    t[i / BKT].key[i % BKT] = EMPTY_KEY;
 }
 
-__global__ void lk_build(const uint64_t* __restrict__ keys, uint32_t n, uint64_t* __restrict__ tk,
-                         uint32_t* __restrict__ tid, uint64_t bmask, unsigned long long* __restrict__ filt,
-                         uint64_t fmask) {
+__global__ void lk_build(const uint64_t* __restrict__ keys, uint32_t n, Bucket* __restrict__ t, uint64_t nbk,
+                         uint32_t* __restrict__ filt, uint64_t fmask, int k, int km) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t key = keys[i];
     const uint64_t h = tab_hash(key);
-    atomicOr(&filt[h & fmask], (unsigned long long)bloom_bits(h));
-    uint64_t b = (h >> 20) & bmask;
+    atomicOr(&filt[filter_word(key_minimizer(key, k, km), h, fmask)], bloom_bits(h));
+    uint64_t b = bucket_of(h, nbk);
     while (true) {
         for (int s = 0; s < BKT; ++s) {
-            const unsigned long long old = atomicCAS((unsigned long long*)&tk[b * BKT + s],
+            const unsigned long long old = atomicCAS((unsigned long long*)&t[b].key[s],
                                                      (unsigned long long)EMPTY_KEY, (unsigned long long)key);
             if (old == EMPTY_KEY || old == key) {
-                tid[b * BKT + s] = i;
+                t[b].id[s] = i;
                 return;
             }
         }
-        b = (b + 1) & bmask;
+        b = b + 1 == nbk ? 0 : b + 1;
     }
 }
 
-// Table probe: KmerID or -1.
-__device__ __forceinline__ int64_t lk_probe(const uint64_t* __restrict__ tk, const uint32_t* __restrict__ tids,
-                                            uint64_t bmask, uint64_t key, uint64_t h) {
-    uint64_t b = (h >> 20) & bmask;
-    while (true) {
-        const uint4* line = reinterpret_cast<const uint4*>(tk + b * BKT);
-        bool any_empty = false;
-#pragma unroll
-        for (int q = 0; q < BKT / 2; ++q) {
-            const uint4 v = line[q];
-            const uint64_t k0 = ((uint64_t)v.y << 32) | v.x, k1 = ((uint64_t)v.w << 32) | v.z;
-            if (k0 == key) return tids[b * BKT + 2 * q];
-            if (k1 == key) return tids[b * BKT + 2 * q + 1];
-            any_empty |= (k0 == EMPTY_KEY) | (k1 == EMPTY_KEY);
-        }
-        if (any_empty) return -1;
-        b = (b + 1) & bmask;
+// Keys and ids of one bucket line.
+struct Line {
+    uint4 v[4];
+    __device__ __forceinline__ uint64_t key(int s) const {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(v);
+        return ((uint64_t)w[2 * s + 1] << 32) | w[2 * s];
     }
+    __device__ __forceinline__ uint32_t id(int s) const {
+        return reinterpret_cast<const uint32_t*>(v)[2 * BKT + s];
+    }
+};
+__device__ __forceinline__ Line load_line(const Bucket* __restrict__ t, uint64_t b) {
+    const uint4* p = reinterpret_cast<const uint4*>(t + b);
+    Line l;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) l.v[q] = p[q];
+    return l;
+}
+// Looks key up in a loaded line: 1 = found (id set), 0 = absent (the line has an empty slot),
+// -1 = line full without the key (continue with the next bucket).
+__device__ __forceinline__ int line_find(const Line& l, uint64_t key, uint32_t& id) {
+    bool found = false, empty = false;
+    uint32_t v = 0;
+#pragma unroll
+    for (int s = 0; s < BKT; ++s) {   // compile-time slots: no dynamic register indexing
+        const uint64_t kk = l.key(s);
+        v = kk == key ? l.id(s) : v;
+        found |= kk == key;
+        empty |= kk == EMPTY_KEY;
+    }
+    id = v;
+    return found ? 1 : (empty ? 0 : -1);
+}
+// Full probe from bucket b: KmerID or -1.
+__device__ __forceinline__ int64_t lk_probe(const Bucket* __restrict__ t, uint64_t nbk, uint64_t key, uint64_t b) {
+    while (true) {
+        uint32_t id;
+        const int r = line_find(load_line(t, b), key, id);
+        if (r > 0) return id;
+        if (r == 0) return -1;
+        b = b + 1 == nbk ? 0 : b + 1;
+    }
+}
+
+// word_read[w] = the read containing base 32w: last r with offs[r] <= 32w (reads are whole
+// CSR ranges; empty reads share their start with the next one).
+__global__ void lk_word_read(const uint64_t* __restrict__ offs, uint64_t nreads, uint64_t nwords,
+                             uint32_t* __restrict__ word_read) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    const uint64_t p = w * 32;
+    uint64_t lo = 0, hi = nreads;   // offs[lo] <= p < offs[hi]
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (offs[mid] <= p) lo = mid; else hi = mid;
+    }
+    word_read[w] = (uint32_t)lo;
 }
 
 __global__ void lk_starts(const uint64_t* __restrict__ offs, uint64_t nreads, uint64_t nbases,
@@ -98,10 +189,9 @@ __global__ void lk_starts(const uint64_t* __restrict__ offs, uint64_t nreads, ui
 }
 
 struct LkTab {
-    const uint64_t* tk;
-    const uint32_t* tid;
-    const unsigned long long* filt;
-    uint64_t bmask, fmask;
+    const Bucket* t;
+    const uint32_t* filt;
+    uint64_t nbk, fmask;
 };
 
 // Canonical code of the window ending at p0+j (j compile-time after unrolling).
@@ -132,48 +222,13 @@ __device__ __forceinline__ uint64_t lk_canon_rt(const Frame<LK_P>& f, int j, uin
     return fwd < rc ? fwd : rc;
 }
 
-constexpr int LK_FB = 16;   // filter words in flight per thread
-constexpr int LK_PB = 4;    // table lines in flight per thread
-
-// Up to LK_PB table probes with their first bucket line loaded together; a line without the
-// key but with an empty slot ends the probe, a full line (rare) falls back to lk_probe.
-__device__ __forceinline__ void lk_probe_batch(const LkTab& tab, const uint64_t (&key)[LK_PB], uint32_t live,
-                                               int64_t (&id)[LK_PB]) {
-    uint64_t b[LK_PB];
-    uint4 ln[LK_PB][BKT / 2];
-#pragma unroll
-    for (int q = 0; q < LK_PB; ++q) {
-        b[q] = (tab_hash(key[q]) >> 20) & tab.bmask;
-        if ((live >> q) & 1u) {
-            const uint4* line = reinterpret_cast<const uint4*>(tab.tk + b[q] * BKT);
-#pragma unroll
-            for (int t = 0; t < BKT / 2; ++t) ln[q][t] = line[t];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < LK_PB; ++q) {
-        id[q] = -1;
-        if (!((live >> q) & 1u)) continue;
-        bool any_empty = false;
-        int slot = -1;
-#pragma unroll
-        for (int t = 0; t < BKT / 2; ++t) {
-            const uint64_t k0 = ((uint64_t)ln[q][t].y << 32) | ln[q][t].x;
-            const uint64_t k1 = ((uint64_t)ln[q][t].w << 32) | ln[q][t].z;
-            slot = k0 == key[q] ? 2 * t : slot;
-            slot = k1 == key[q] ? 2 * t + 1 : slot;
-            any_empty |= (k0 == EMPTY_KEY) | (k1 == EMPTY_KEY);
-        }
-        if (slot >= 0) id[q] = tab.tid[b[q] * BKT + slot];
-        else if (!any_empty) id[q] = lk_probe(tab.tk, tab.tid, tab.bmask, key[q], tab_hash(key[q]));
-    }
-}
-
-template <bool EMIT>
+template <bool EMIT, int KM>
 __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk, const uint16_t* __restrict__ vd,
                                                 const unsigned int* __restrict__ sb, uint64_t nbases,
                                                 const uint64_t* __restrict__ offs, uint64_t nreads, int k,
+                                                const uint32_t* __restrict__ word_read,
                                                 LkTab tab, uint32_t* __restrict__ hmask,
+                                                uint32_t* __restrict__ win_kid,
                                                 unsigned long long* __restrict__ tile_cnt,
                                                 uint32_t* __restrict__ h_read, uint32_t* __restrict__ h_kid,
                                                 uint32_t* __restrict__ h_pos) {
@@ -182,53 +237,141 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
     const uint64_t p0 = gt * LK_P;
     const uint64_t mask = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1);
     if (!EMIT) {
-        uint32_t hits = 0;
+        __shared__ uint64_t qkey[LK_T / 64][LK_QN];
+        __shared__ uint16_t qorg[LK_T / 64][LK_QN];
+        __shared__ uint32_t qcnt[LK_T / 64];
+        __shared__ uint32_t lhit[LK_T];
+        const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) qcnt[wave] = 0;
+        lhit[threadIdx.x] = 0;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t hits = 0, ovf = 0;
+        Frame<LK_P> f;
         if (p0 < nbases) {
-            Frame<LK_P> f;
-            (void)load_frame<LK_P, true>(pk, vd, PAD_WORDS + p0 / 16 - 2, k, f);
+            const uint64_t v64 = load_frame<LK_P, true>(pk, vd, PAD_WORDS + p0 / 16 - 2, k, f);
+            const uint32_t acgt = (uint32_t)(runs_of(v64, k) >> 32);   // window has only ACGT
             const uint64_t s64 = (uint64_t)sb[SB_PAD + p0 / 32 - 1] | ((uint64_t)sb[SB_PAD + p0 / 32] << 32);
             uint32_t wm = (uint32_t)(runs_of(~s64, k - 1) >> 32);   // no read start in (s, e]
             const uint64_t left = nbases - p0;
             if (left < 32) wm &= (1u << left) - 1u;
-            // 1) filter words, LK_FB in flight
-            uint32_t cand = 0;
+            // 1) minimizer of every window: hashes of the canonical m-mers ending at p0-KM..p0+31,
+            //    then a sliding minimum of width KM+1 (van Herk / Gil-Werman, blocks of KM+1)
+            constexpr int NM = LK_P + KM;
+            constexpr int NWF = Frame<LK_P>::NW;
+            const int m = k - KM;
+            const uint64_t mm = m >= 32 ? ~0ull : ((1ull << (2 * m)) - 1);
+            uint32_t mh[NM];
 #pragma unroll
-            for (int j0 = 0; j0 < LK_P; j0 += LK_FB) {
-                uint32_t bits[LK_FB];
-                uint64_t fw[LK_FB];
+            for (int t = 0; t < NM; ++t) {
+                const int pj = t - KM;   // m-mer ending at p0 + pj
+                const uint64_t fm = field64<NWF>(f.x, 2 * (16 * NWF - 33 - pj)) & mm;
+                const uint64_t rm = revcomp_code(fm, m);
+                mh[t] = mmer_hash(fm < rm ? fm : rm);
+            }
+            uint32_t wmin[LK_P];
+            if constexpr (KM == 0) {
 #pragma unroll
-                for (int j = 0; j < LK_FB; ++j) {
-                    const uint64_t h = tab_hash(lk_canon(f, j0 + j, mask));
-                    bits[j] = (uint32_t)(h >> 40);
-                    fw[j] = ((wm >> (j0 + j)) & 1u) ? tab.filt[h & tab.fmask] : 0ull;
+                for (int j = 0; j < LK_P; ++j) wmin[j] = mh[j];
+            } else {
+                constexpr int B = KM + 1;
+                uint32_t pre[NM], suf[NM];
+#pragma unroll
+                for (int t = 0; t < NM; ++t) pre[t] = (t % B == 0) ? mh[t] : min(pre[t - 1], mh[t]);
+#pragma unroll
+                for (int t = NM - 1; t >= 0; --t)
+                    suf[t] = (t % B == B - 1 || t == NM - 1) ? mh[t] : min(suf[t + 1], mh[t]);
+#pragma unroll
+                for (int j = 0; j < LK_P; ++j) wmin[j] = min(suf[j], pre[j + KM]);
+            }
+            // 2) filter blocks: a lane loads the 16-B block once per minimizer run (only the lanes
+            //    whose run changes issue the load, so L2 sees one request per run) and serves
+            //    the run's windows from registers.  Windows with a non-ACGT byte (REF codes are
+            //    not strand-consistent there, so their minimizer block is undefined) always pass.
+            //    Passing windows go to this wave's queue as (key, origin lane, window).
+            const uint4* __restrict__ filt4 = reinterpret_cast<const uint4*>(tab.filt);
+            const uint64_t bmask4 = tab.fmask >> 2;
+            const uint32_t force = ~acgt;
+            uint4 blk = make_uint4(0u, 0u, 0u, 0u);
+            uint32_t cur = 0;
+#pragma unroll
+            for (int j = 0; j < LK_P; ++j) {
+                const uint32_t bi = (uint32_t)(wmin[j] & bmask4);
+                if (j == 0 || bi != cur) {
+                    blk = filt4[bi];
+                    cur = bi;
                 }
-#pragma unroll
-                for (int j = 0; j < LK_FB; ++j) {
-                    const uint32_t x = bits[j];
-                    const uint64_t bb = (1ull << (x & 63)) | (1ull << ((x >> 6) & 63)) |
-                                        (1ull << ((x >> 12) & 63)) | (1ull << ((x >> 18) & 63));
-                    if ((fw[j] & bb) == bb && ((wm >> (j0 + j)) & 1u)) cand |= 1u << (j0 + j);
+                const uint64_t key = lk_canon(f, j, mask);
+                const uint64_t h = tab_hash(key);
+                const uint32_t sel = (uint32_t)(h >> 56) & 3u;
+                const uint32_t wv = sel == 0 ? blk.x : sel == 1 ? blk.y : sel == 2 ? blk.z : blk.w;
+                const uint32_t bb = bloom_bits(h);
+                const bool pass = (((wv & bb) == bb) || ((force >> j) & 1u)) && ((wm >> j) & 1u);
+                if (pass) {
+                    const uint32_t pos = atomicAdd(&qcnt[wave], 1u);
+                    if (pos < LK_QN) {
+                        qkey[wave][pos] = key;
+                        qorg[wave][pos] = (uint16_t)((lane << 5) | j);
+                    } else {
+                        ovf |= 1u << j;
+                    }
                 }
             }
-            // 2) table probes for the filter passes, LK_PB lines in flight
-            while (cand) {
-                uint64_t key[LK_PB];
-                int jj[LK_PB];
-                uint32_t live = 0;
-#pragma unroll
-                for (int q = 0; q < LK_PB; ++q) {
-                    jj[q] = cand ? __builtin_ctz(cand) : 0;
-                    if (cand) { live |= 1u << q; cand &= cand - 1u; }
-                    key[q] = lk_canon_rt(f, jj[q], mask);
-                }
-                int64_t id[LK_PB];
-                lk_probe_batch(tab, key, live, id);
-#pragma unroll
-                for (int q = 0; q < LK_PB; ++q)
-                    if (((live >> q) & 1u) && id[q] >= 0) hits |= 1u << jj[q];
-            }
-            hmask[gt] = hits;
         }
+        // 3) the wave's queue with every lane busy, two probes in flight per lane
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nq = min(qcnt[wave], (uint32_t)LK_QN);
+        const uint64_t gbase = (uint64_t)blockIdx.x * LK_T + (uint64_t)wave * 64;
+        for (uint32_t q0 = 0; q0 < nq; q0 += 128) {
+            const uint32_t i0 = q0 + lane, i1 = q0 + 64 + lane;
+            const bool l0 = i0 < nq, l1 = i1 < nq;
+            const uint64_t k0 = l0 ? qkey[wave][i0] : 0ull, k1 = l1 ? qkey[wave][i1] : 0ull;
+            const uint64_t b0 = bucket_of(tab_hash(k0), tab.nbk), b1 = bucket_of(tab_hash(k1), tab.nbk);
+            Line L0, L1;
+            if (l0) L0 = load_line(tab.t, b0);
+            if (l1) L1 = load_line(tab.t, b1);
+            if (l0) {
+                uint32_t id;
+                int r = line_find(L0, k0, id);
+                if (r < 0) {
+                    const int64_t x = lk_probe(tab.t, tab.nbk, k0, b0 + 1 == tab.nbk ? 0 : b0 + 1);
+                    r = x >= 0;
+                    id = (uint32_t)x;
+                }
+                if (r > 0) {
+                    const uint32_t o = qorg[wave][i0];
+                    atomicOr(&lhit[wave * 64 + (o >> 5)], 1u << (o & 31));
+                    win_kid[(gbase + (o >> 5)) * LK_P + (o & 31)] = id;
+                }
+            }
+            if (l1) {
+                uint32_t id;
+                int r = line_find(L1, k1, id);
+                if (r < 0) {
+                    const int64_t x = lk_probe(tab.t, tab.nbk, k1, b1 + 1 == tab.nbk ? 0 : b1 + 1);
+                    r = x >= 0;
+                    id = (uint32_t)x;
+                }
+                if (r > 0) {
+                    const uint32_t o = qorg[wave][i1];
+                    atomicOr(&lhit[wave * 64 + (o >> 5)], 1u << (o & 31));
+                    win_kid[(gbase + (o >> 5)) * LK_P + (o & 31)] = id;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        hits = lhit[threadIdx.x];
+        // 4) queue overflow (rare): this lane probes its own leftovers
+        while (ovf) {
+            const int j = __builtin_ctz(ovf);
+            ovf &= ovf - 1u;
+            const uint64_t key = lk_canon_rt(f, j, mask);
+            const int64_t x = lk_probe(tab.t, tab.nbk, key, bucket_of(tab_hash(key), tab.nbk));
+            if (x >= 0) {
+                hits |= 1u << j;
+                win_kid[gt * LK_P + j] = (uint32_t)x;
+            }
+        }
+        if (p0 < nbases) hmask[gt] = hits;
         uint32_t tot;
         (void)block_excl_scan<LK_T>((uint32_t)__popc(hits), ws, &tot);
         if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
@@ -239,37 +382,18 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
     const uint32_t ex = block_excl_scan<LK_T>((uint32_t)__popc(hits), ws, &tot);
     if (!hits) return;
     uint64_t o = tile_cnt[blockIdx.x] + ex;
-    Frame<LK_P> f;
-    (void)load_frame<LK_P, true>(pk, vd, PAD_WORDS + p0 / 16 - 2, k, f);
-    // read containing p0: last r with offs[r] <= p0
-    uint64_t lo = 0, hi = nreads;
-    while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (offs[mid] <= p0) lo = mid; else hi = mid;
-    }
-    uint64_t r = lo, re = offs[r + 1];
+    // read containing p0 (p0 is 32-aligned): precomputed per word, no search
+    uint64_t r = word_read[p0 / 32], re = offs[r + 1];
+    const uint32_t* __restrict__ wk = win_kid + gt * LK_P;
     while (hits) {
-        uint64_t key[LK_PB];
-        int jj[LK_PB];
-        uint32_t live = 0;
-#pragma unroll
-        for (int q = 0; q < LK_PB; ++q) {
-            jj[q] = hits ? __builtin_ctz(hits) : 0;
-            if (hits) { live |= 1u << q; hits &= hits - 1u; }
-            key[q] = lk_canon_rt(f, jj[q], mask);
-        }
-        int64_t id[LK_PB];
-        lk_probe_batch(tab, key, live, id);
-#pragma unroll
-        for (int q = 0; q < LK_PB; ++q) {
-            if (!((live >> q) & 1u)) continue;
-            const uint64_t e = p0 + jj[q];
-            while (re <= e) re = offs[++r + 1];
-            h_read[o] = (uint32_t)r;
-            h_kid[o] = (uint32_t)id[q];
-            h_pos[o] = (uint32_t)(e + 1 - offs[r]);
-            ++o;
-        }
+        const int j = __builtin_ctz(hits);
+        hits &= hits - 1u;
+        const uint64_t e = p0 + j;
+        while (re <= e) re = offs[++r + 1];
+        h_read[o] = (uint32_t)r;
+        h_kid[o] = wk[j];
+        h_pos[o] = (uint32_t)(e + 1 - offs[r]);
+        ++o;
     }
 }
 
@@ -283,15 +407,60 @@ __global__ void lk_ptr(const uint32_t* __restrict__ idx, uint64_t H, uint64_t ns
     for (uint64_t s = lo; s <= hi; ++s) ptr[s] = i;
 }
 
-// Number of non-empty CSR segments (one atomic per 1024 segments).
+// Number of non-empty CSR segments and the largest segment (one atomic each per 1024 segments).
 __global__ void __launch_bounds__(1024) lk_nonempty(const uint64_t* __restrict__ ptr, uint64_t nseg,
                                                     unsigned long long* __restrict__ out) {
     __shared__ uint32_t ws[1024 / 64 + 1];
+    __shared__ unsigned long long smax;
     const uint64_t s = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-    const uint32_t v = s < nseg && ptr[s + 1] > ptr[s] ? 1u : 0u;
+    const uint64_t len = s < nseg ? ptr[s + 1] - ptr[s] : 0;
+    if (threadIdx.x == 0) smax = 0;
+    __syncthreads();
+    if (len) atomicMax(&smax, (unsigned long long)len);
     uint32_t tot;
-    (void)block_excl_scan<1024>(v, ws, &tot);
-    if (threadIdx.x == 0 && tot) atomicAdd(out, (unsigned long long)tot);
+    (void)block_excl_scan<1024>(len ? 1u : 0u, ws, &tot);
+    if (threadIdx.x == 0) {
+        if (tot) atomicAdd(&out[0], (unsigned long long)tot);
+        if (smax) atomicMax(&out[1], smax);
+    }
+}
+
+// Per-read sort of the (read << kbits | KmerID, position) pairs: one workgroup per read with
+// 2 <= hits <= CAP, bitonic in LDS on (KmerID << 32 | position) — unique inside a read and
+// ordered like the stable (read, KmerID) sort with window order kept among equal ids
+// (ReadClusteringEngine.cpp:262-272: sorted ids; :267 first occurrence).
+template <int NT, int CAP>
+__global__ void __launch_bounds__(NT) lk_segsort(const uint64_t* __restrict__ hptr, uint64_t nreads, int kbits,
+                                                 uint64_t* __restrict__ sk, uint32_t* __restrict__ sv,
+                                                 uint32_t lo_excl) {
+    __shared__ uint64_t v[CAP];
+    const uint64_t r = blockIdx.x;
+    if (r >= nreads) return;
+    const uint64_t b = hptr[r], cnt = hptr[r + 1] - b;
+    if (cnt <= lo_excl || cnt > (uint64_t)CAP) return;
+    uint32_t P = 2;
+    while (P < cnt) P <<= 1;
+    const uint64_t kmask = (1ull << kbits) - 1;
+    for (uint32_t i = threadIdx.x; i < P; i += NT)
+        v[i] = i < cnt ? ((sk[b + i] & kmask) << 32) | sv[b + i] : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += NT) {
+                const uint32_t x = i ^ j;
+                if (x > i) {
+                    const uint64_t a = v[i], c = v[x];
+                    if ((a > c) == ((i & k) == 0)) { v[i] = c; v[x] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    const uint64_t rk = r << kbits;
+    for (uint32_t i = threadIdx.x; i < cnt; i += NT) {
+        const uint64_t x = v[i];
+        sk[b + i] = rk | (x >> 32);
+        sv[b + i] = (uint32_t)x;
+    }
 }
 
 __global__ void lk_compose(const uint32_t* __restrict__ rd, const uint32_t* __restrict__ kid,
@@ -337,27 +506,26 @@ inline int bits_for(uint64_t n) {   // bits to hold values in [0, n)
 void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n) {
     HGA_REQUIRE(k >= 1 && k <= 32, HGA_ERR_INVALID, "k must be in [1,32]");
     auto& L = c->lookup;
-    uint64_t nbk = 128;
-    while (nbk * BKT < 2ull * n) nbk <<= 1;            // <= 50 % slot load
+    const uint64_t nbk = std::max<uint64_t>(64, (2ull * n + BKT - 1) / BKT);   // <= 50 % slot load
     uint64_t fw = 1024;
-    while (fw * 64 < 11ull * n) fw <<= 1;               // >= 11 filter bits per key
-    L.slots = nbk * BKT;
+    while (fw * 64 < (uint64_t)HGA_FBITS2 * n) fw <<= 1;   // >= HGA_FBITS2/2 filter bits per key
+    L.slots = nbk;   // buckets
     L.fwords = fw;
     L.k = k;
+    L.km = k >= HGA_KM_MINK ? LK_KM : 0;
     L.n_sdk = n;
-    uint64_t* tk = static_cast<uint64_t*>(L.tab_key.ensure(L.slots * 8));
-    uint32_t* ti = static_cast<uint32_t*>(L.tab_id.ensure(L.slots * 4));
-    auto* filt = static_cast<unsigned long long*>(L.filter.ensure(fw * 8));
+    Bucket* tb = static_cast<Bucket*>(L.tab_key.ensure(nbk * sizeof(Bucket)));
+    auto* filt = static_cast<uint32_t*>(L.filter.ensure(fw * 4));
     DevBuf tmp;
     uint64_t* dk = static_cast<uint64_t*>(tmp.ensure(std::max<uint64_t>(n, 1) * 8));
     if (n) HGA_HIP(hipMemcpyAsync(dk, keys, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(lk_fill, dim3(blocks_for(L.slots, 256)), dim3(256), 0, c->stream, tk, L.slots);
+    hipLaunchKernelGGL(lk_fill, dim3(blocks_for(nbk * BKT, 256)), dim3(256), 0, c->stream, tb, nbk);
     c->check_launch("lk_fill");
-    HGA_HIP(hipMemsetAsync(filt, 0, fw * 8, c->stream));
+    HGA_HIP(hipMemsetAsync(filt, 0, fw * 4, c->stream));
     if (n) {
         c->launch("lk_build", [&] {
-            hipLaunchKernelGGL(lk_build, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, dk, n, tk, ti, nbk - 1,
-                               filt, fw - 1);
+            hipLaunchKernelGGL(lk_build, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, dk, n, tb, nbk, filt,
+                               fw - 1, k, L.km);
         });
         c->check_launch("lk_build");
     }
@@ -397,6 +565,11 @@ void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, ui
     if (n)
         hipLaunchKernelGGL(lk_starts, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            static_cast<const uint64_t*>(dof), n, nb, sb);
+    const uint64_t nwr = (nb + 31) / 32;
+    uint32_t* wr = static_cast<uint32_t*>(L.word_read.ensure(std::max<uint64_t>(nwr, 1) * 4));
+    if (n && nwr)
+        hipLaunchKernelGGL(lk_word_read, dim3(blocks_for(nwr, 256)), dim3(256), 0, c->stream,
+                           static_cast<const uint64_t*>(dof), n, nwr, wr);
     c->check_launch("lk_pack");
     c->sync();
     L.h_offsets.assign(offsets, offsets + n + 1);
@@ -420,19 +593,23 @@ void lookup_run(hga_ctx* c) {
     const uint64_t n_threads = (nb + LK_P - 1) / LK_P;
     const uint64_t n_tiles = (n_threads + LK_T - 1) / LK_T;
     uint32_t* hm = static_cast<uint32_t*>(L.scratch.ensure(std::max<uint64_t>(n_threads, 1) * 4 + 256));
+    uint32_t* wkid = static_cast<uint32_t*>(L.win_kid.ensure(std::max<uint64_t>(n_threads, 1) * LK_P * 4));
     auto* tile = static_cast<unsigned long long*>(L.tile_cnt.ensure((n_tiles + 1) * 8));
     const uint32_t* pk = L.packed.as<uint32_t>();
     const uint16_t* vd = L.valid.as<uint16_t>();
     const unsigned int* sb = L.starts.as<unsigned int>();
     const uint64_t* offs = L.offsets.as<uint64_t>();
-    LkTab tab{L.tab_key.as<uint64_t>(), L.tab_id.as<uint32_t>(), L.filter.as<unsigned long long>(),
-              L.slots / BKT - 1, L.fwords - 1};
+    LkTab tab{L.tab_key.as<Bucket>(), L.filter.as<uint32_t>(), L.slots, L.fwords - 1};
     uint64_t H = 0;
     if (n_tiles) {
         c->launch("lk_count", [&] {
-            hipLaunchKernelGGL(lk_scan<false>, dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, nb,
-                               offs, n, k, tab, hm, tile, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                               (uint32_t*)nullptr);
+#define HGA_LK_SCAN(KMV)                                                                                       \
+    hipLaunchKernelGGL((lk_scan<false, KMV>), dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, nb, \
+                       offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, (uint32_t*)nullptr,          \
+                       (uint32_t*)nullptr, (uint32_t*)nullptr)
+            if (L.km == LK_KM) HGA_LK_SCAN(LK_KM);
+            else HGA_LK_SCAN(0);
+#undef HGA_LK_SCAN
         });
         c->check_launch("lk_count");
         HGA_HIP(hipMemsetAsync(tile + n_tiles, 0, 8, c->stream));
@@ -446,8 +623,8 @@ void lookup_run(hga_ctx* c) {
     uint32_t* hp = static_cast<uint32_t*>(L.hit_pos.ensure(std::max<uint64_t>(H, 1) * 4));
     if (H) {
         c->launch("lk_emit", [&] {
-            hipLaunchKernelGGL(lk_scan<true>, dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, nb,
-                               offs, n, k, tab, hm, tile, hr, hk, hp);
+            hipLaunchKernelGGL((lk_scan<true, 0>), dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, nb,
+                               offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, hr, hk, hp);
         });
         c->check_launch("lk_emit");
     }
@@ -473,7 +650,21 @@ void lookup_run(hga_ctx* c) {
             hipLaunchKernelGGL(lk_compose, dim3(blocks_for(H, 256)), dim3(256), 0, c->stream, hr, hk, hp, H,
                                kbits, sk, sv);
         });
-        radix_sort_u64(c, sk, sv, H, kbits + rbits, L.scratch2);
+        unsigned long long mx[2];
+        HGA_HIP(hipMemcpyAsync(mx, ctr, 16, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        if (mx[1] <= 16384 && n < (1ull << 31)) {
+            c->launch("lk_sort", [&] {
+                hipLaunchKernelGGL((lk_segsort<256, 2048>), dim3((unsigned)n), dim3(256), 0, c->stream, hptr, n, kbits,
+                                   sk, sv, 1u);
+                if (mx[1] > 2048)
+                    hipLaunchKernelGGL((lk_segsort<1024, 16384>), dim3((unsigned)n), dim3(1024), 0, c->stream, hptr,
+                                       n, kbits, sk, sv, 2048u);
+            });
+            c->check_launch("lk_segsort");
+        } else {
+            radix_sort_u64(c, sk, sv, H, kbits + rbits, L.scratch2);   // a read with > 16384 hits
+        }
         uint64_t* flag = static_cast<uint64_t*>(L.s_key2.ensure((H + 1) * 8));
         uint32_t* skid = static_cast<uint32_t*>(L.s_val2.ensure(H * 4));
         c->launch("lk_post", [&] {

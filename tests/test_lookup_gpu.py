@@ -98,3 +98,24 @@ def test_lookup_c3_shape_property(gpu_ctx, hga_mod):
     o = oracle.construct_indices(r.bases[: int(r.offsets[200])], r.offsets[:201], 19, sdk)
     h = int(o["hit_ptr"][-1])
     assert np.array_equal(res["hit_kid"][:h], o["hit_kid"]) and np.array_equal(res["hit_pos"][:h], o["hit_pos"])
+
+
+@pytest.mark.parametrize("sizes", [(300, 5000, 40), (25000, 1500)])
+def test_lookup_hit_dense_reads(gpu_ctx, sizes):
+    """Reads whose every window is an SDK, with repeats: per-read sorts of 2..16384 hits (LDS
+    segment sorts) and of > 16384 hits (global radix path), duplicates kept in window order."""
+    rng = random.Random(sum(sizes))
+    k = 15
+    reads = []
+    for L in sizes:
+        unit = "".join(rng.choice("ACGT") for _ in range(max(L // 3, k + 1)))
+        reads.append((unit * 4)[:L].encode())
+    reads.append(b"ACGTN" * 10)
+    pool = set()
+    for r in reads:
+        c, _ = oracle.kmer_windows(r, k)
+        pool.update(c.tolist())
+    sdk = np.array(rng.sample(sorted(pool), len(pool)), np.uint64)
+    bases = b"".join(reads)
+    offsets = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 3), oracle.construct_indices(bases, offsets, k, sdk, 3))
