@@ -566,7 +566,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                     for (int t = 1; t < PF_C; ++t) pick = q == t ? rv[t] : pick;
                     myq[pos++] = pick;
                 }
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_sync();
                 // 2) the queue, 64 misses at a time with every lane busy, one probe step per
                 //    iteration; then the (rare) queue overflow, lane by lane
                 const uint32_t nq = qn < QN_C ? qn : QN_C;
@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                         count_occupancy(ins, s_occ, s_ovf, maxload);
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_sync();
                 E r = EMPTY;
                 uint32_t g = 0;
                 while (__any(miss != 0u || r != EMPTY)) {

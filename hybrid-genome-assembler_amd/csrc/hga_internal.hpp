@@ -123,7 +123,7 @@ struct LookupState {
     // results
     DevBuf tile_cnt, hit_read, hit_kid, hit_pos, hit_ptr, s_key, s_val, s_key2, s_val2,
         first_flag, first_kid, first_pos, first_read, first_ptr, kci_key, kci_val, kci_ptr, scratch,
-        scratch2, scratch3;
+        scratch2, scratch3, big_list;
     std::vector<uint64_t> h_offsets;
     uint64_t windows = 0, hits = 0, firsts = 0, reads_hit = 0;
 };

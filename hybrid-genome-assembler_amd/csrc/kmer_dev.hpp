@@ -207,6 +207,13 @@ __global__ void pack_kernel(const uint8_t* __restrict__ s, uint64_t n, uint32_t*
     vd[PAD_WORDS + w] = (uint16_t)valid;
 }
 
+// Hand-off of LDS data between lanes of ONE wave: a wave's LDS instructions execute in order,
+// so only the compiler must be kept from reordering or caching across this point.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // Wave / block scans (wave64).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll

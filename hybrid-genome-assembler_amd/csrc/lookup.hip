@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         if (lane == 0) qcnt[wave] = 0;
         lhit[threadIdx.x] = 0;
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         uint32_t hits = 0, ovf = 0;
         Frame<LK_P> f;
         if (p0 < nbases) {
@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
             }
         }
         // 3) the wave's queue with every lane busy, two probes in flight per lane
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         const uint32_t nq = min(qcnt[wave], (uint32_t)LK_QN);
         const uint64_t gbase = (uint64_t)blockIdx.x * LK_T + (uint64_t)wave * 64;
         for (uint32_t q0 = 0; q0 < nq; q0 += 128) {
@@ -358,7 +358,7 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
                 }
             }
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         hits = lhit[threadIdx.x];
         // 4) queue overflow (rare): this lane probes its own leftovers
         while (ovf) {
@@ -425,16 +425,26 @@ __global__ void __launch_bounds__(1024) lk_nonempty(const uint64_t* __restrict__
     }
 }
 
+// Reads with more than `lo` hits (order irrelevant).
+__global__ void lk_big_reads(const uint64_t* __restrict__ hptr, uint64_t n, uint64_t lo,
+                             uint32_t* __restrict__ list, unsigned long long* __restrict__ cnt) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n && hptr[r + 1] - hptr[r] > lo) list[atomicAdd(cnt, 1ull)] = (uint32_t)r;
+}
+
 // Per-read sort of the (read << kbits | KmerID, position) pairs: one workgroup per read with
 // 2 <= hits <= CAP, bitonic in LDS on (KmerID << 32 | position) — unique inside a read and
 // ordered like the stable (read, KmerID) sort with window order kept among equal ids
 // (ReadClusteringEngine.cpp:262-272: sorted ids; :267 first occurrence).
+// Element i lives with thread i % NT, so partners at distance j < 64 are in the same wave: those
+// stages need no workgroup barrier (a wave's LDS accesses are ordered).  `list` (optional)
+// names the reads to sort.
 template <int NT, int CAP>
 __global__ void __launch_bounds__(NT) lk_segsort(const uint64_t* __restrict__ hptr, uint64_t nreads, int kbits,
                                                  uint64_t* __restrict__ sk, uint32_t* __restrict__ sv,
-                                                 uint32_t lo_excl) {
+                                                 uint32_t lo_excl, const uint32_t* __restrict__ list) {
     __shared__ uint64_t v[CAP];
-    const uint64_t r = blockIdx.x;
+    const uint64_t r = list ? list[blockIdx.x] : blockIdx.x;
     if (r >= nreads) return;
     const uint64_t b = hptr[r], cnt = hptr[r + 1] - b;
     if (cnt <= lo_excl || cnt > (uint64_t)CAP) return;
@@ -444,8 +454,15 @@ __global__ void __launch_bounds__(NT) lk_segsort(const uint64_t* __restrict__ hp
     for (uint32_t i = threadIdx.x; i < P; i += NT)
         v[i] = i < cnt ? ((sk[b + i] & kmask) << 32) | sv[b + i] : ~0ull;
     __syncthreads();
+    bool cross = false;   // the previous stage wrote elements of other waves
     for (uint32_t k = 2; k <= P; k <<= 1)
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64 || cross) {
+                __syncthreads();
+            } else {
+                wave_lds_sync();
+            }
+            cross = j >= 64;
             for (uint32_t i = threadIdx.x; i < P; i += NT) {
                 const uint32_t x = i ^ j;
                 if (x > i) {
@@ -453,8 +470,9 @@ __global__ void __launch_bounds__(NT) lk_segsort(const uint64_t* __restrict__ hp
                     if ((a > c) == ((i & k) == 0)) { v[i] = c; v[x] = a; }
                 }
             }
-            __syncthreads();
         }
+    if (cross) __syncthreads();
+    wave_lds_sync();
     const uint64_t rk = r << kbits;
     for (uint32_t i = threadIdx.x; i < cnt; i += NT) {
         const uint64_t x = v[i];
@@ -654,12 +672,22 @@ void lookup_run(hga_ctx* c) {
         HGA_HIP(hipMemcpyAsync(mx, ctr, 16, hipMemcpyDeviceToHost, c->stream));
         c->sync();
         if (mx[1] <= 16384 && n < (1ull << 31)) {
+            uint32_t* big = nullptr;
+            unsigned long long nbig = 0;
+            if (mx[1] > 2048) {   // the few long reads: list them, one 1024-thread workgroup each
+                big = static_cast<uint32_t*>(L.big_list.ensure(n * 4 + 64));
+                auto* bc = reinterpret_cast<unsigned long long*>(ctr + 2);
+                hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, hptr, n, 2048ull,
+                                   big, bc);
+                HGA_HIP(hipMemcpyAsync(&nbig, bc, 8, hipMemcpyDeviceToHost, c->stream));
+                c->sync();
+            }
             c->launch("lk_sort", [&] {
                 hipLaunchKernelGGL((lk_segsort<256, 2048>), dim3((unsigned)n), dim3(256), 0, c->stream, hptr, n, kbits,
-                                   sk, sv, 1u);
-                if (mx[1] > 2048)
-                    hipLaunchKernelGGL((lk_segsort<1024, 16384>), dim3((unsigned)n), dim3(1024), 0, c->stream, hptr,
-                                       n, kbits, sk, sv, 2048u);
+                                   sk, sv, 1u, (const uint32_t*)nullptr);
+                if (nbig)
+                    hipLaunchKernelGGL((lk_segsort<1024, 16384>), dim3((unsigned)nbig), dim3(1024), 0, c->stream,
+                                       hptr, n, kbits, sk, sv, 2048u, (const uint32_t*)big);
             });
             c->check_launch("lk_segsort");
         } else {

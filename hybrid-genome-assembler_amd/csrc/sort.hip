@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
         if (ok) before = wcnt[wave][d];
         rank[j] = before + (uint32_t)__popcll(m & lt);
         if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
     }
     __syncthreads();
     // digit starts inside the tile, then per-wave starts

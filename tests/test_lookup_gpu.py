@@ -119,3 +119,27 @@ def test_lookup_hit_dense_reads(gpu_ctx, sizes):
     bases = b"".join(reads)
     offsets = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
     assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 3), oracle.construct_indices(bases, offsets, k, sdk, 3))
+
+
+def test_lookup_many_dense_reads(gpu_ctx):
+    """Hundreds of reads whose windows are mostly SDKs with repeats: many concurrent per-read
+    LDS sorts with cross-wave stages (sizes 50..2500 hits)."""
+    rng = random.Random(11)
+    k = 13
+    base = "".join(rng.choice("ACGT") for _ in range(3000))
+    reads = []
+    for _ in range(300):
+        L = rng.randint(50, 2500)
+        s = rng.randint(0, len(base) - L)
+        unit = base[s: s + max(L // 2, k)]
+        reads.append((unit * 3)[:L].encode())
+    pool = set()
+    for r in reads[:50]:
+        c, _ = oracle.kmer_windows(r, k)
+        pool.update(c.tolist())
+    sdk = np.array(rng.sample(sorted(pool), len(pool) * 3 // 4), np.uint64)
+    bases = b"".join(reads)
+    offsets = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    want = oracle.construct_indices(bases, offsets, k, sdk, 1)
+    for _ in range(3):
+        assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 1), want)
