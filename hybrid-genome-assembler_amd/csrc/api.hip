@@ -259,6 +259,23 @@ hga_status hga_profile_enable(hga_ctx* c, int on) {
     });
 }
 
+hga_status hga_profile_select(hga_ctx* c, const char* names) {
+    HGA_CTX_GUARD(c, {
+        c->prof.drain();
+        c->prof.only.clear();
+        std::string cur;
+        for (const char* p = names ? names : ""; ; ++p) {
+            if (*p == ',' || *p == 0) {
+                if (!cur.empty()) c->prof.only.push_back(cur);
+                cur.clear();
+                if (*p == 0) break;
+            } else {
+                cur += *p;
+            }
+        }
+    });
+}
+
 hga_status hga_profile_reset(hga_ctx* c) {
     HGA_CTX_GUARD(c, {
         c->prof.drain();

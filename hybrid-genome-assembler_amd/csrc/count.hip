@@ -22,6 +22,7 @@
 //                     (export_kmers, :110-135; numeric order == LC_ALL=C order).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 
 #include "hga_internal.hpp"
@@ -245,6 +246,29 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk_
     uint32_t tot;
     (void)block_excl_scan<NT_B>(inst, ws, &tot);
     if (tid == 0 && tot) atomicAdd(&gstat[4], (unsigned long long)tot);
+}
+
+// ---------------------------------------------------------------- pack
+// One launch packs every file into its [pad | words | tail] region of the shared buffers
+// (pad and tail zero = invalid) and initialises the pipeline counters.
+struct PackFile {
+    const uint8_t* seq;
+    uint64_t n, woff, nw;
+};
+__global__ void kc_pack_files(const PackFile* __restrict__ files, uint32_t F, uint64_t total_words,
+                              uint32_t* __restrict__ pk, uint16_t* __restrict__ vd,
+                              unsigned long long* __restrict__ gstat, uint64_t n_first) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < 8) gstat[g] = g == 3 ? (unsigned long long)n_first : 0ull;
+    if (g >= total_words) return;
+    uint32_t f = 0;
+    while (f + 1 < F && files[f + 1].woff <= g) ++f;
+    const PackFile pf = files[f];
+    const uint64_t wl = g - pf.woff;
+    uint32_t code = 0, valid = 0;
+    if (wl >= (uint64_t)PAD_WORDS && wl - PAD_WORDS < pf.nw) pack_word<false>(pf.seq, pf.n, wl - PAD_WORDS, code, valid);
+    pk[g] = code;
+    vd[g] = (uint16_t)valid;
 }
 
 // ---------------------------------------------------------------- layout
@@ -934,27 +958,23 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     for (uint32_t f = 0; f < F; ++f) woff[f + 1] = woff[f] + PAD_WORDS + (s.seq_len[f] + 15) / 16 + tail_words;
     uint32_t* pk_all = static_cast<uint32_t*>(s.pk_all.ensure(woff[F] * 4));
     uint16_t* vd_all = static_cast<uint16_t*>(s.vd_all.ensure(woff[F] * 2));
+    std::vector<PackFile> pf(F);
     for (uint32_t f = 0; f < F; ++f) {
-        const uint64_t n = s.seq_len[f];
-        const uint64_t nw = (n + 15) / 16;
-        uint32_t* pk = pk_all + woff[f];
-        uint16_t* vd = vd_all + woff[f];
-        HGA_HIP(hipMemsetAsync(vd, 0, PAD_WORDS * 2, c->stream));
-        HGA_HIP(hipMemsetAsync(vd + PAD_WORDS + nw, 0, tail_words * 2, c->stream));
-        HGA_HIP(hipMemsetAsync(pk, 0, PAD_WORDS * 4, c->stream));
-        HGA_HIP(hipMemsetAsync(pk + PAD_WORDS + nw, 0, tail_words * 4, c->stream));
-        if (nw) {
-            const uint8_t* sp = s.seq[f]->as<uint8_t>();
-            c->launch("kc_pack", [&] {
-                hipLaunchKernelGGL(pack_kernel<false>, dim3(blocks_for(nw, 256)), dim3(256), 0, c->stream, sp, n,
-                                   pk, vd, nw);
-            });
-            c->check_launch("kc_pack");
-        }
+        pf[f] = PackFile{s.seq[f]->as<uint8_t>(), s.seq_len[f], woff[f], (s.seq_len[f] + 15) / 16};
         bf[f].woff = woff[f];
     }
-    BinFile* d_bf = static_cast<BinFile*>(s.bin_files.ensure(sizeof(BinFile) * F));
-    HGA_HIP(hipMemcpyAsync(d_bf, bf.data(), sizeof(BinFile) * F, hipMemcpyHostToDevice, c->stream));
+    // per-file tables: uploaded only when they change (they are fixed for repeated runs)
+    const size_t tb = sizeof(BinFile) * F + sizeof(PackFile) * F;
+    std::vector<char> tab(tb);
+    std::memcpy(tab.data(), bf.data(), sizeof(BinFile) * F);
+    std::memcpy(tab.data() + sizeof(BinFile) * F, pf.data(), sizeof(PackFile) * F);
+    char* d_tab = static_cast<char*>(s.bin_files.ensure(tb));
+    if (s.tab_host != tab) {
+        HGA_HIP(hipMemcpy(d_tab, tab.data(), tb, hipMemcpyHostToDevice));
+        s.tab_host = tab;
+    }
+    BinFile* d_bf = reinterpret_cast<BinFile*>(d_tab);
+    const PackFile* d_pf = reinterpret_cast<const PackFile*>(d_tab + sizeof(BinFile) * F);
 
     const size_t esz1 = e1_32 ? 4 : 8, esz = e32 ? 4 : 8;
     const uint64_t cap = total_bytes / std::max<uint32_t>(1, min_per_file) + 1;
@@ -973,8 +993,12 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const uint64_t pool_cap = table_cap * BLK;
     void* binned1 = s.binned1.ensure(pool_cap * esz1);
     Blk* table = static_cast<Blk*>(s.regions.ensure(table_cap * sizeof(Blk)));
-    HGA_HIP(hipMemsetAsync(gstat, 0, 8 * 8, c->stream));
-    HGA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(gstat + 3), (int)n_first, 1, c->stream));
+    // P: pack all files + counter init, one launch
+    c->launch("kc_pack", [&] {
+        hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256)), dim3(256), 0,
+                           c->stream, d_pf, F, woff[F], pk_all, vd_all, gstat, n_first);
+    });
+    c->check_launch("kc_pack");
 
     // B1: level-1 binning of every file into pool blocks + per-workgroup fine histograms
     if (W) {
@@ -1054,9 +1078,16 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     auto* over = reinterpret_cast<unsigned long long*>(base + hbytes);
     auto* ctrl = reinterpret_cast<unsigned long long*>(base + hbytes + over_cap * 8);
     double* dthr = reinterpret_cast<double*>(ctrl + 4);
+    // pinned staging: [thresholds | ctrl readback (4 u64) | first SPEC_CHUNK compacted triples]
+    constexpr uint64_t SPEC_CHUNK = 1u << 12;
+    char* hp = static_cast<char*>(c->pinned.ensure(MAX_THR * 8 + 32 + SPEC_CHUNK * 16));
+    double* hthr = reinterpret_cast<double*>(hp);
+    auto* hc = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8);
+    auto* hcomp = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8 + 32);
+    std::memcpy(hthr, thr.data(), n_thr * 8);
     HGA_HIP(hipMemsetAsync(base, 0, hbytes, c->stream));
     HGA_HIP(hipMemsetAsync(ctrl, 0, 32, c->stream));
-    HGA_HIP(hipMemcpyAsync(dthr, thr.data(), n_thr * 8, hipMemcpyHostToDevice, c->stream));
+    HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_for(std::max<uint64_t>(s.rows, 1), NT_H),
                                                        (uint64_t)c->num_cu * 2);
     c->launch("kc_spec_hist", [&] {
@@ -1068,23 +1099,28 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     // compact the dense bins on the device: only (threshold, total, count) triples cross PCIe
     const uint64_t ncap = 1u << 20;
     auto* comp = static_cast<unsigned long long*>(s.hist_comp.ensure(ncap * 16 + 64));
-    HGA_HIP(hipMemsetAsync(ctrl + 2, 0, 8, c->stream));
     const uint64_t nd = (uint64_t)n_thr * TD;
     c->launch("kc_spec_hist", [&] {
         hipLaunchKernelGGL(kc_hist_compact, dim3(blocks_for(nd, 256)), dim3(256), 0, c->stream, hist, nd, comp,
                            ctrl + 2, ncap);
     });
     c->check_launch("kc_hist_compact");
-    unsigned long long hc[3];
+    // one synchronisation: counters and (speculatively) the first chunk of triples together
     HGA_HIP(hipMemcpyAsync(hc, ctrl, 24, hipMemcpyDeviceToHost, c->stream));
+    HGA_HIP(hipMemcpyAsync(hcomp, comp, SPEC_CHUNK * 16, hipMemcpyDeviceToHost, c->stream));
     c->sync();
     HGA_REQUIRE(!(hc[1] & 1ull), HGA_ERR_INVALID, "a row's specificity is above the last threshold");
     HGA_REQUIRE(!(hc[1] & 2ull), HGA_ERR_OOM, "histogram overflow list full");
     HGA_REQUIRE(hc[2] <= ncap, HGA_ERR_OOM, "histogram compaction buffer full");
     std::map<std::pair<uint32_t, uint64_t>, uint64_t> bins;
     if (hc[2]) {
-        std::vector<unsigned long long> cv(2 * hc[2]);
-        HGA_HIP(hipMemcpy(cv.data(), comp, hc[2] * 16, hipMemcpyDeviceToHost));
+        const unsigned long long* cv = hcomp;
+        std::vector<unsigned long long> rest;
+        if (hc[2] > SPEC_CHUNK) {
+            rest.resize(2 * hc[2]);
+            HGA_HIP(hipMemcpy(rest.data(), comp, hc[2] * 16, hipMemcpyDeviceToHost));
+            cv = rest.data();
+        }
         for (uint64_t i = 0; i < hc[2]; ++i)
             bins[{(uint32_t)(cv[2 * i] >> 56), cv[2 * i] & ((1ull << 56) - 1)}] += cv[2 * i + 1];
     }

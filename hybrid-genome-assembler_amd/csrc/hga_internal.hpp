@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -59,9 +60,31 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(p); }
 };
 
+// Grow-only pinned host buffer for small async transfers (one per ctx).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    void* ensure(size_t bytes) {
+        if (bytes <= cap && p) return p;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        HGA_HIP(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault));
+        cap = bytes ? bytes : 16;
+        return p;
+    }
+};
+
 // Per-kernel event timing on the ctx stream (hga_profile_*).
 struct Profiler {
     bool on = false;
+    std::vector<std::string> only;   // if non-empty: time only these launch names
     struct Rec { std::string name; hipEvent_t a, b; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
@@ -105,6 +128,7 @@ struct CountState {
         sel_keys, sel_tmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, pk_all, vd_all;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
+    std::vector<char> tab_host;   // last uploaded per-file tables
     uint32_t buckets = 0, fb = 0, max_split = 1;
     ~CountState() {
         for (auto* b : seq) delete b;
@@ -137,12 +161,16 @@ struct hga_ctx {
     hga::Profiler prof;
     hga::CountState count;
     hga::LookupState lookup;
-    hga::DevBuf pinned_dummy;
+    hga::PinnedBuf pinned;   // small host<->device staging (see count_spec_hist)
 
     // Launch helper: records events around the launch when profiling is on.
     template <class F>
     void launch(const char* name, F&& f) {
-        if (!prof.on) { f(); return; }
+        if (!prof.on || (!prof.only.empty() &&
+                         std::find(prof.only.begin(), prof.only.end(), name) == prof.only.end())) {
+            f();
+            return;
+        }
         hipEvent_t a = prof.get(), b = prof.get();
         HGA_HIP(hipEventRecord(a, stream));
         f();

@@ -185,14 +185,14 @@ __device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
 // ASCII -> packed frames (kc_pack / lk_pack).  REF = KmerIterator semantics (upper-case
 // ACGT only), otherwise jellyfish semantics (either case).
 // One thread per 16 bases: packed codes (first base in bits 31:30) and valid bits.
+// 16 bases starting at 16w -> 2-bit codes (MSB-first) + valid bits.
 template <bool REF>
-__global__ void pack_kernel(const uint8_t* __restrict__ s, uint64_t n, uint32_t* __restrict__ pk,
-                        uint16_t* __restrict__ vd, uint64_t nw) {
-    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nw) return;
+__device__ __forceinline__ void pack_word(const uint8_t* __restrict__ s, uint64_t n, uint64_t w, uint32_t& code,
+                                          uint32_t& valid) {
     const uint4 v = load16(s, (int64_t)(w * 16), n);
     const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-    uint32_t code = 0, valid = 0;
+    code = 0;
+    valid = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t b = (ws[j >> 2] >> (8 * (j & 3))) & 0xFFu;
@@ -203,6 +203,15 @@ __global__ void pack_kernel(const uint8_t* __restrict__ s, uint64_t n, uint32_t*
         code |= c << (30 - 2 * j);
         valid |= (ok ? 1u : 0u) << j;
     }
+}
+
+template <bool REF>
+__global__ void pack_kernel(const uint8_t* __restrict__ s, uint64_t n, uint32_t* __restrict__ pk,
+                            uint16_t* __restrict__ vd, uint64_t nw) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    uint32_t code, valid;
+    pack_word<REF>(s, n, w, code, valid);
     pk[PAD_WORDS + w] = code;
     vd[PAD_WORDS + w] = (uint16_t)valid;
 }

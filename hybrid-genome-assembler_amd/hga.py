@@ -76,6 +76,7 @@ HGA_SYMBOLS = {
     "hga_lookup_get_sizes": (C.c_int, [_vp, C.POINTER(LookupSizes)]),
     "hga_lookup_fetch": (C.c_int, [_vp, C.POINTER(LookupResult)]),
     "hga_profile_enable": (C.c_int, [_vp, C.c_int]),
+    "hga_profile_select": (C.c_int, [_vp, C.c_char_p]),
     "hga_profile_reset": (C.c_int, [_vp]),
     "hga_profile_get": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_double), _u64p]),
     "hga_sync": (C.c_int, [_vp]),
@@ -295,6 +296,10 @@ class Ctx:
     # ---- measurement
     def profile(self, on: bool = True):
         _ck(lib().hga_profile_enable(self._h, 1 if on else 0))
+
+    def profile_select(self, names=()):
+        """Time only these launch names (empty: all)."""
+        _ck(lib().hga_profile_select(self._h, ",".join(names).encode()))
 
     def profile_reset(self):
         _ck(lib().hga_profile_reset(self._h))

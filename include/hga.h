@@ -187,6 +187,9 @@ hga_status hga_lookup_fetch(hga_ctx* ctx, const hga_lookup_result* out);
  * Measurement: per-kernel device time, recorded with HIP events on the ctx stream.
  * ------------------------------------------------------------------------------ */
 hga_status hga_profile_enable(hga_ctx* ctx, int on);
+/* Restricts event timing to the comma-separated launch names ("" or NULL = all), so that
+ * the untimed launches carry no event overhead. */
+hga_status hga_profile_select(hga_ctx* ctx, const char* names);
 hga_status hga_profile_reset(hga_ctx* ctx);
 /* Total milliseconds and launch count recorded for kernel `name` since the reset. */
 hga_status hga_profile_get(hga_ctx* ctx, const char* name, double* ms, uint64_t* launches);
