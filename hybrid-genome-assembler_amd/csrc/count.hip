@@ -148,7 +148,6 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk_
     __shared__ uint32_t take_a[NB1_MAX];
     __shared__ uint32_t fhist[MAX_NB];
     __shared__ E1 stage[TP_B];
-    __shared__ uint8_t sd1[TP_B];
     __shared__ uint32_t ws[NT_B / 64 + 1];
     const int tid = threadIdx.x;
     const uint32_t nb1 = kp.nb1, nb = kp.nb;
@@ -222,18 +221,16 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk_
         lds_barrier();
 #pragma unroll
         for (int j = 0; j < P_B; ++j)
-            if ((wm >> j) & 1u) {
-                const uint32_t pos = off1[dd[j]] + rk[j];
-                stage[pos] = ee[j];
-                sd1[pos] = (uint8_t)dd[j];
-            }
+            if ((wm >> j) & 1u) stage[off1[dd[j]] + rk[j]] = ee[j];
         lds_barrier();
-        const uint32_t tot = off1[nb1];
-        for (uint32_t i = tid; i < tot; i += NT_B) {
-            const uint32_t d = sd1[i];
-            const uint32_t jj = i - off1[d];
-            const unsigned long long g = jj < take_a[d] ? base_a[d] + jj : base_b[d] + (jj - take_a[d]);
-            if (g < pool_cap) out1[g] = stage[i];
+        // flush: one wave per region run (region-uniform bases, lanes on consecutive elements)
+        for (uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6); d < nb1; d += NT_B / 64) {
+            const uint32_t o = off1[d], len = off1[d + 1] - o, ta = take_a[d];
+            const unsigned long long ba = base_a[d], bb = base_b[d];
+            for (uint32_t jj = (uint32_t)(tid & 63); jj < len; jj += 64) {
+                const unsigned long long g = jj < ta ? ba + jj : bb + (jj - ta);
+                if (g < pool_cap) out1[g] = stage[o + jj];
+            }
         }
         lds_barrier();
     }
@@ -318,7 +315,6 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
     __shared__ unsigned long long base2[NB2_MAX];
     __shared__ uint32_t s_w0;
     __shared__ E stage[CH_R];
-    __shared__ uint8_t sd2[CH_R];
     const int tid = threadIdx.x;
     const uint64_t blk = blockIdx.x;
     const uint32_t nb2 = kp.nb2;
@@ -376,17 +372,14 @@ __global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, con
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
         const uint32_t i = (uint32_t)j * NT_R + tid;
-        if (i < used) {
-            const uint32_t pos = off2[dd[j]] + rk[j];
-            stage[pos] = ee[j];
-            sd2[pos] = (uint8_t)dd[j];
-        }
+        if (i < used) stage[off2[dd[j]] + rk[j]] = ee[j];
     }
     __syncthreads();
-    const uint32_t tot = off2[nb2];
-    for (uint32_t i = tid; i < tot; i += NT_R) {
-        const uint32_t d = sd2[i];
-        out[base2[d] + (i - off2[d])] = stage[i];
+    // flush: one wave per digit run (digit-uniform base, lanes on consecutive elements)
+    for (uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6); d < nb2; d += NT_R / 64) {
+        const uint32_t o = off2[d], len = off2[d + 1] - o;
+        E* __restrict__ dst = out + base2[d];
+        for (uint32_t jj = (uint32_t)(tid & 63); jj < len; jj += 64) dst[jj] = stage[o + jj];
     }
 }
 

@@ -67,13 +67,19 @@ __device__ __forceinline__ uint32_t bloom_bits(uint64_t h) {
 #ifndef HGA_KM_MINK
 #define HGA_KM_MINK 15
 #endif
-constexpr int LK_KM = 7;   // m = k - 7 for k >= 15 (seven m-mers per window); k < 15: plain hashing
+#ifndef HGA_LK_KM
+#define HGA_LK_KM 7
+#endif
+constexpr int LK_KM = HGA_LK_KM;   // m = k - 7 for k >= 15 (eight m-mers per window); k < 15: plain hashing
 __device__ __forceinline__ uint64_t revcomp_code(uint64_t x, int m) {
     uint64_t y = ~x;                                           // complement: c -> 3 - c
     y = __builtin_bitreverse64(y);                             // reverse bits (and each pair)
     y = ((y >> 1) & 0x5555555555555555ull) | ((y & 0x5555555555555555ull) << 1);   // fix pairs
     return y >> (64 - 2 * m);
 }
+// Hash of a canonical m-mer: high half of one 64-bit product.  A multiplicative hash keeps
+// the hashes of overlapping m-mers correlated, which lengthens minimizer runs (fewer filter
+// blocks per thread); murmur-style mixing measured fewer false positives but 2x the scan time.
 __device__ __forceinline__ uint32_t mmer_hash(uint64_t canon_m) {
     return (uint32_t)((canon_m * 0x9E3779B97F4A7C15ull) >> 32);
 }
@@ -264,8 +270,11 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
 #pragma unroll
             for (int t = 0; t < NM; ++t) {
                 const int pj = t - KM;   // m-mer ending at p0 + pj
+                // fwd: the last m bases of the window frame; rc: the rc frame is pre-shifted so the
+                // k-window ending at p0+j is field64(r, 2j); its m-mer ending at the same base sits
+                // 2(k-m) bits higher, i.e. at field64(r, 2(pj + KM)) — both compile-time offsets
                 const uint64_t fm = field64<NWF>(f.x, 2 * (16 * NWF - 33 - pj)) & mm;
-                const uint64_t rm = revcomp_code(fm, m);
+                const uint64_t rm = field64<NWF>(f.r, 2 * (pj + KM)) & mm;
                 mh[t] = mmer_hash(fm < rm ? fm : rm);
             }
             uint32_t wmin[LK_P];
