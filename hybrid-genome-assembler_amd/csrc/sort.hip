@@ -8,6 +8,8 @@
 // linear exclusive scan gives every (digit, tile) output offset), scan, downsweep
 // (stable in-tile rank via 64-lane ballot matching, staged through LDS so the global
 // writes leave in digit runs).
+#include <algorithm>
+
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
 
@@ -114,6 +116,147 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
         const K kk = sk[i];
         const uint32_t d = (uint32_t)(kk >> shift) & 255u;
         const uint64_t g = (uint64_t)offs[(uint64_t)d * n_tiles + blockIdx.x] + (i - dstart[d]);
+        kout[g] = kk;
+        if (HAS_V) vout[g] = sv[i];
+    }
+}
+
+
+// ---- onesweep: one histogram kernel for all passes, then ONE kernel per pass ----------------
+// Each tile takes the next tile id (atomic), ranks its keys stably in LDS as above, publishes
+// its per-digit count, and looks back over earlier tiles (decoupled look-back) for its
+// exclusive prefix per digit.  Status words carry flag + value in one 32-bit granule: agent-
+// scope relaxed atomic stores/loads (sc1), the hand-off MI355X_MICROARCH.md lists for a flag
+// that is its own payload.  A tile only waits on tiles with smaller ids, which are running.
+constexpr uint32_t LB_A = 1u << 30, LB_P = 2u << 30, LB_M = (1u << 30) - 1;
+
+template <class K>
+__global__ void __launch_bounds__(RS_T) rs_hist_all(const K* __restrict__ keys, uint64_t n, int passes,
+                                                    uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[8][256];
+    for (int i = threadIdx.x; i < 8 * 256; i += RS_T) (&h[0][0])[i] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * RS_T + threadIdx.x; i < n; i += (uint64_t)gridDim.x * RS_T) {
+        const K k = keys[i];
+        for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
+    }
+    __syncthreads();
+    for (int p = 0; p < passes; ++p) {
+        const uint32_t v = h[p][threadIdx.x];
+        if (v) atomicAdd(&hist[p * 256 + threadIdx.x], v);
+    }
+}
+
+template <class K, bool HAS_V>
+__global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                    K* __restrict__ kout, uint32_t* __restrict__ vout, uint64_t n,
+                                                    int shift, const uint32_t* __restrict__ ghist,
+                                                    uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr) {
+    __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t gofs[256];
+    __shared__ uint32_t ws[8];
+    __shared__ uint32_t s_tile;
+    __shared__ K sk[RS_TILE];
+    __shared__ uint32_t sv[HAS_V ? RS_TILE : 1];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    for (int i = tid; i < 4 * 256; i += RS_T) (&wcnt[0][0])[i] = 0;
+    uint32_t gtot;
+    const uint32_t gstart = block_excl_scan<RS_T>(ghist[tid], ws, &gtot);   // digit tid's global start
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t base = (uint64_t)tile * RS_TILE;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    K key[RS_I];
+    uint32_t val[RS_I];
+    uint32_t dig[RS_I];
+    uint32_t rank[RS_I];
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        const uint64_t i = base + (uint64_t)wave * 1024 + (uint64_t)j * 64 + lane;
+        const bool ok = i < n;
+        key[j] = ok ? kin[i] : K(0);
+        if (HAS_V) val[j] = ok ? vin[i] : 0u;
+        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & 255u) : 256u;
+    }
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        const uint32_t d = dig[j];
+        const bool ok = d < 256u;
+        uint64_t m = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        uint32_t before = 0;
+        if (ok) before = wcnt[wave][d];
+        rank[j] = before + (uint32_t)__popcll(m & lt);
+        if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
+        wave_lds_sync();
+    }
+    __syncthreads();
+    {
+        const int d = tid;
+        const uint32_t c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
+        const uint32_t c = c0 + c1 + c2 + c3;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<RS_T>(c, ws, &tot);
+        wcnt[0][d] = ex;
+        wcnt[1][d] = ex + c0;
+        wcnt[2][d] = ex + c0 + c1;
+        wcnt[3][d] = ex + c0 + c1 + c2;
+        uint32_t* st = status + (uint64_t)tile * 256 + d;
+        uint32_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(st, LB_P | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st, LB_A | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // look back LBW tiles per step (independent loads), newest first; restart at the
+            // first tile that has not published yet
+            constexpr int LBW = 8;
+            int64_t t = (int64_t)tile - 1;
+            while (true) {
+                uint32_t v[LBW];
+#pragma unroll
+                for (int i = 0; i < LBW; ++i)
+                    v[i] = t - i >= 0 ? __hip_atomic_load(status + (uint64_t)(t - i) * 256 + d, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : LB_P;   // before tile 0: an empty inclusive prefix
+                int stop = LBW;   // 0..LBW-1: index of a P (done) or an unpublished tile (wait)
+                bool done = false;
+#pragma unroll
+                for (int i = LBW - 1; i >= 0; --i) {
+                    const uint32_t f = v[i] & ~LB_M;
+                    if (f == 0u || f == LB_P) { stop = i; done = f == LB_P; }
+                }
+                for (int i = 0; i < stop; ++i) excl += v[i] & LB_M;   // all A
+                if (stop < LBW && done) {
+                    excl += v[stop] & LB_M;
+                    break;
+                }
+                t -= stop;   // stop == LBW: all A, continue further back; else wait on tile t - stop
+            }
+            __hip_atomic_store(st, LB_P | (excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        gofs[d] = gstart + excl - ex;   // element at in-tile sorted index i, digit d -> gofs[d] + i
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        if (dig[j] < 256u) {
+            const uint32_t lp = wcnt[wave][dig[j]] + rank[j];
+            sk[lp] = key[j];
+            if (HAS_V) sv[lp] = val[j];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
+    for (uint32_t i = tid; i < cnt; i += RS_T) {
+        const K kk = sk[i];
+        const uint64_t g = (uint64_t)gofs[(uint32_t)(kk >> shift) & 255u] + i;
         kout[g] = kk;
         if (HAS_V) vout[g] = sv[i];
     }
@@ -228,6 +371,46 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
     K* kbuf = k2;
     uint32_t* va = vals;
     uint32_t* vbuf = v2;
+    const int npass = (bits + 7) / 8;
+    // onesweep where launch count dominates (small n); the classic pass is faster per byte
+    if (n < (4ull << 20) && npass <= 8) {
+        const size_t hb = (size_t)npass * 256 * 4, stb = (size_t)npass * n_tiles * 256 * 4, tcb = 64;
+        char* ob = static_cast<char*>(scratch.ensure(kb + vb + hb + stb + tcb));
+        K* k2o = reinterpret_cast<K*>(ob);
+        uint32_t* v2o = vals ? reinterpret_cast<uint32_t*>(ob + kb) : nullptr;
+        uint32_t* hist = reinterpret_cast<uint32_t*>(ob + kb + vb);
+        uint32_t* status = reinterpret_cast<uint32_t*>(ob + kb + vb + hb);
+        uint32_t* tctr = reinterpret_cast<uint32_t*>(ob + kb + vb + hb + stb);
+        HGA_HIP(hipMemsetAsync(hist, 0, hb + stb + tcb, c->stream));
+        const unsigned hgrid = (unsigned)std::min<uint64_t>(n_tiles, (uint64_t)c->num_cu * 2);
+        c->launch("radix_upsweep", [&] {
+            hipLaunchKernelGGL(rs_hist_all<K>, dim3(hgrid), dim3(RS_T), 0, c->stream, keys, n, npass, hist);
+        });
+        c->check_launch("rs_hist_all");
+        K* ka2 = keys;
+        K* kb2 = k2o;
+        uint32_t* va2 = vals;
+        uint32_t* vb2 = v2o;
+        for (int p = 0; p < npass; ++p) {
+            c->launch("radix_downsweep", [&] {
+                if (vals)
+                    hipLaunchKernelGGL((rs_onesweep<K, true>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka2, va2, kb2,
+                                       vb2, n, 8 * p, hist + p * 256, status + (size_t)p * n_tiles * 256, tctr + p);
+                else
+                    hipLaunchKernelGGL((rs_onesweep<K, false>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka2,
+                                       (const uint32_t*)nullptr, kb2, (uint32_t*)nullptr, n, 8 * p, hist + p * 256,
+                                       status + (size_t)p * n_tiles * 256, tctr + p);
+            });
+            c->check_launch("rs_onesweep");
+            std::swap(ka2, kb2);
+            std::swap(va2, vb2);
+        }
+        if (npass & 1) {
+            HGA_HIP(hipMemcpyAsync(keys, ka2, n * sizeof(K), hipMemcpyDeviceToDevice, c->stream));
+            if (vals) HGA_HIP(hipMemcpyAsync(vals, va2, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        }
+        return;
+    }
     int passes = 0;
     for (int shift = 0; shift < bits; shift += 8, ++passes) {
         c->launch("radix_upsweep", [&] {
