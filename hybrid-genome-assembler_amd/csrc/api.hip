@@ -195,6 +195,27 @@ hga_status hga_count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* cou
     HGA_CTX_GUARD(c, { hga::count_merge(c, keys, counts, n, min_per_file); });
 }
 
+hga_status hga_count_pack_bits(hga_ctx* c, int* bits) {
+    HGA_CTX_GUARD(c, {
+        HGA_REQUIRE(bits, HGA_ERR_INVALID, "null pointer");
+        HGA_REQUIRE(c->count.begun, HGA_ERR_STATE, "hga_count_begin not called");
+        *bits = hga::count_pack_bits(c);
+    });
+}
+
+hga_status hga_count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_owners, uint64_t* out,
+                                      uint64_t capacity, uint64_t* pieces_per_owner, uint64_t* total) {
+    HGA_CTX_GUARD(c, {
+        HGA_REQUIRE(pieces_per_owner && total && (n_owners <= 1 || splitters), HGA_ERR_INVALID, "null pointer");
+        *total = hga::count_partition_packed(c, splitters, n_owners, out, capacity, pieces_per_owner);
+        HGA_REQUIRE(*total <= capacity, HGA_ERR_OOM, "output capacity too small (see *total)");
+    });
+}
+
+hga_status hga_count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t min_per_file) {
+    HGA_CTX_GUARD(c, { hga::count_merge_packed(c, pieces, n, min_per_file); });
+}
+
 hga_status hga_count_rows(hga_ctx* c, uint64_t** keys, uint32_t** counts, uint64_t* rows) {
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(keys && counts && rows, HGA_ERR_INVALID, "null pointer");

@@ -197,6 +197,10 @@ void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<u
 void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* keys_out,
                      uint32_t* counts_out, uint64_t* rows_per_owner);
 void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min_c);
+int count_pack_bits(hga_ctx* c);
+uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,
+                                uint64_t cap_out, uint64_t* pieces_per_owner);
+void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t min_c);
 
 void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n);
 void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, uint64_t n,

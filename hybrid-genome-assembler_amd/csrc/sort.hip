@@ -9,6 +9,7 @@
 // (stable in-tile rank via 64-lane ballot matching, staged through LDS so the global
 // writes leave in digit runs).
 #include <algorithm>
+#include <cstdlib>
 
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
@@ -21,9 +22,11 @@ constexpr int RS_I = 16;               // items per thread
 constexpr int RS_TILE = RS_T * RS_I;   // 4096 keys per tile
 constexpr int SC_T = 1024, SC_I = 4, SC_TILE = SC_T * SC_I;
 
+// dmask: the pass's digit mask (the last pass may cover fewer than 8 bits: bits above the sort
+// width are payload and must not order the keys).
 template <class K>
 __global__ void __launch_bounds__(RS_T) rs_upsweep(const K* __restrict__ keys, uint64_t n,
-                                                   int shift, uint32_t* __restrict__ counts,
+                                                   int shift, uint32_t dmask, uint32_t* __restrict__ counts,
                                                    uint32_t n_tiles) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
@@ -32,7 +35,7 @@ __global__ void __launch_bounds__(RS_T) rs_upsweep(const K* __restrict__ keys, u
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
         uint64_t i = base + (uint64_t)j * RS_T + threadIdx.x;
-        if (i < n) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+        if (i < n) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & dmask], 1u);
     }
     __syncthreads();
     counts[(uint64_t)threadIdx.x * n_tiles + blockIdx.x] = h[threadIdx.x];
@@ -43,7 +46,7 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
                                                      const uint32_t* __restrict__ vin,
                                                      K* __restrict__ kout,
                                                      uint32_t* __restrict__ vout, uint64_t n,
-                                                     int shift,
+                                                     int shift, uint32_t dmask,
                                                      const uint32_t* __restrict__ offs,
                                                      uint32_t n_tiles) {
     __shared__ uint32_t wcnt[4][256];
@@ -68,7 +71,7 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
         const bool ok = i < n;
         key[j] = ok ? kin[i] : K(0);
         if (HAS_V) val[j] = ok ? vin[i] : 0u;
-        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & 255u) : 256u;
+        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & dmask) : 256u;
     }
     // Stable rank inside the wave: items in (j, lane) order.
 #pragma unroll
@@ -114,7 +117,7 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
     const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
     for (uint32_t i = tid; i < cnt; i += RS_T) {
         const K kk = sk[i];
-        const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+        const uint32_t d = (uint32_t)(kk >> shift) & dmask;
         const uint64_t g = (uint64_t)offs[(uint64_t)d * n_tiles + blockIdx.x] + (i - dstart[d]);
         kout[g] = kk;
         if (HAS_V) vout[g] = sv[i];
@@ -131,14 +134,17 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
 constexpr uint32_t LB_A = 1u << 30, LB_P = 2u << 30, LB_M = (1u << 30) - 1;
 
 template <class K>
-__global__ void __launch_bounds__(RS_T) rs_hist_all(const K* __restrict__ keys, uint64_t n, int passes,
+__global__ void __launch_bounds__(RS_T) rs_hist_all(const K* __restrict__ keys, uint64_t n, int passes, int bits,
                                                     uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[8][256];
     for (int i = threadIdx.x; i < 8 * 256; i += RS_T) (&h[0][0])[i] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * RS_T + threadIdx.x; i < n; i += (uint64_t)gridDim.x * RS_T) {
         const K k = keys[i];
-        for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
+        for (int p = 0; p < passes; ++p) {
+            const int w = bits - 8 * p < 8 ? bits - 8 * p : 8;
+            atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & ((1u << w) - 1u)], 1u);
+        }
     }
     __syncthreads();
     for (int p = 0; p < passes; ++p) {
@@ -150,7 +156,7 @@ __global__ void __launch_bounds__(RS_T) rs_hist_all(const K* __restrict__ keys, 
 template <class K, bool HAS_V>
 __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     K* __restrict__ kout, uint32_t* __restrict__ vout, uint64_t n,
-                                                    int shift, const uint32_t* __restrict__ ghist,
+                                                    int shift, uint32_t dmask, const uint32_t* __restrict__ ghist,
                                                     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr) {
     __shared__ uint32_t wcnt[4][256];
     __shared__ uint32_t gofs[256];
@@ -178,7 +184,7 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
         const bool ok = i < n;
         key[j] = ok ? kin[i] : K(0);
         if (HAS_V) val[j] = ok ? vin[i] : 0u;
-        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & 255u) : 256u;
+        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & dmask) : 256u;
     }
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
@@ -256,7 +262,7 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
     const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
     for (uint32_t i = tid; i < cnt; i += RS_T) {
         const K kk = sk[i];
-        const uint64_t g = (uint64_t)gofs[(uint32_t)(kk >> shift) & 255u] + i;
+        const uint64_t g = (uint64_t)gofs[(uint32_t)(kk >> shift) & dmask] + i;
         kout[g] = kk;
         if (HAS_V) vout[g] = sv[i];
     }
@@ -353,6 +359,15 @@ size_t scan_scratch_bytes(uint64_t n) {
     return b + 256;
 }
 
+// n below which the onesweep path is used (env HGA_ONESWEEP_MAX overrides; 0 disables).
+inline uint64_t hga_onesweep_max() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("HGA_ONESWEEP_MAX");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)(4ull << 20);
+    }();
+    return v;
+}
+
 template <class K>
 void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, DevBuf& scratch) {
     if (n <= 1 || bits <= 0) return;
@@ -373,7 +388,7 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
     uint32_t* vbuf = v2;
     const int npass = (bits + 7) / 8;
     // onesweep where launch count dominates (small n); the classic pass is faster per byte
-    if (n < (4ull << 20) && npass <= 8) {
+    if (n < (uint64_t)hga_onesweep_max() && npass <= 8) {
         const size_t hb = (size_t)npass * 256 * 4, stb = (size_t)npass * n_tiles * 256 * 4, tcb = 64;
         char* ob = static_cast<char*>(scratch.ensure(kb + vb + hb + stb + tcb));
         K* k2o = reinterpret_cast<K*>(ob);
@@ -384,7 +399,7 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
         HGA_HIP(hipMemsetAsync(hist, 0, hb + stb + tcb, c->stream));
         const unsigned hgrid = (unsigned)std::min<uint64_t>(n_tiles, (uint64_t)c->num_cu * 2);
         c->launch("radix_upsweep", [&] {
-            hipLaunchKernelGGL(rs_hist_all<K>, dim3(hgrid), dim3(RS_T), 0, c->stream, keys, n, npass, hist);
+            hipLaunchKernelGGL(rs_hist_all<K>, dim3(hgrid), dim3(RS_T), 0, c->stream, keys, n, npass, bits, hist);
         });
         c->check_launch("rs_hist_all");
         K* ka2 = keys;
@@ -392,13 +407,14 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
         uint32_t* va2 = vals;
         uint32_t* vb2 = v2o;
         for (int p = 0; p < npass; ++p) {
+            const uint32_t dm = bits - 8 * p >= 8 ? 255u : ((1u << (bits - 8 * p)) - 1u);
             c->launch("radix_downsweep", [&] {
                 if (vals)
                     hipLaunchKernelGGL((rs_onesweep<K, true>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka2, va2, kb2,
-                                       vb2, n, 8 * p, hist + p * 256, status + (size_t)p * n_tiles * 256, tctr + p);
+                                       vb2, n, 8 * p, dm, hist + p * 256, status + (size_t)p * n_tiles * 256, tctr + p);
                 else
                     hipLaunchKernelGGL((rs_onesweep<K, false>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka2,
-                                       (const uint32_t*)nullptr, kb2, (uint32_t*)nullptr, n, 8 * p, hist + p * 256,
+                                       (const uint32_t*)nullptr, kb2, (uint32_t*)nullptr, n, 8 * p, dm, hist + p * 256,
                                        status + (size_t)p * n_tiles * 256, tctr + p);
             });
             c->check_launch("rs_onesweep");
@@ -413,22 +429,23 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
     }
     int passes = 0;
     for (int shift = 0; shift < bits; shift += 8, ++passes) {
+        const uint32_t dm = bits - shift >= 8 ? 255u : ((1u << (bits - shift)) - 1u);
         c->launch("radix_upsweep", [&] {
             hipLaunchKernelGGL(rs_upsweep<K>, dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n,
-                               shift, cnt, n_tiles);
+                               shift, dm, cnt, n_tiles);
         });
         c->check_launch("rs_upsweep");
         excl_scan_impl<uint32_t>(c, cnt, n_cnt, scratch, kb + vb + cb);
         if (vals) {
             c->launch("radix_downsweep", [&] {
                 hipLaunchKernelGGL((rs_downsweep<K, true>), dim3(n_tiles), dim3(RS_T), 0, c->stream,
-                                   ka, va, kbuf, vbuf, n, shift, cnt, n_tiles);
+                                   ka, va, kbuf, vbuf, n, shift, dm, cnt, n_tiles);
             });
         } else {
             c->launch("radix_downsweep", [&] {
                 hipLaunchKernelGGL((rs_downsweep<K, false>), dim3(n_tiles), dim3(RS_T), 0,
                                    c->stream, ka, (const uint32_t*)nullptr, kbuf,
-                                   (uint32_t*)nullptr, n, shift, cnt, n_tiles);
+                                   (uint32_t*)nullptr, n, shift, dm, cnt, n_tiles);
             });
         }
         c->check_launch("rs_downsweep");

@@ -68,6 +68,9 @@ HGA_SYMBOLS = {
     "hga_count_select_device": (C.c_int, [_vp, C.c_int64, C.c_int64, _u64p, _u64p]),
     "hga_count_partition": (C.c_int, [_vp, _u64p, C.c_uint32, C.c_void_p, C.c_void_p, _u64p]),
     "hga_count_merge": (C.c_int, [_vp, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]),
+    "hga_count_pack_bits": (C.c_int, [_vp, C.POINTER(C.c_int)]),
+    "hga_count_partition_packed": (C.c_int, [_vp, _u64p, C.c_uint32, C.c_void_p, C.c_uint64, _u64p, _u64p]),
+    "hga_count_merge_packed": (C.c_int, [_vp, C.c_void_p, C.c_uint64, C.c_uint32]),
     "hga_count_rows": (C.c_int, [_vp, C.POINTER(_u64p), C.POINTER(_u32p), _u64p]),
     "hga_count_dump": (C.c_int, [_vp, C.c_uint32, C.POINTER(_u64p), C.POINTER(_u32p), _u64p]),
     "hga_lookup_load": (C.c_int, [_vp, C.c_int, _u64p, C.c_uint32]),
@@ -243,6 +246,28 @@ class Ctx:
     def count_merge(self, keys_ptr: int, counts_ptr: int, n: int, min_per_file: int = 2):
         """Owner-side merge of received rows (device pointers); they become the ctx rows."""
         _ck(lib().hga_count_merge(self._h, C.c_void_p(keys_ptr), C.c_void_p(counts_ptr), n, min_per_file))
+
+    def count_pack_bits(self) -> int:
+        b = C.c_int()
+        _ck(lib().hga_count_pack_bits(self._h, C.byref(b)))
+        return b.value
+
+    def count_partition_packed(self, splitters, out_ptr: int, capacity: int):
+        """Packed pieces grouped by owner into a device buffer.  Returns (pieces per owner, total);
+        total > capacity means nothing was written (retry with more room)."""
+        spl = np.ascontiguousarray(splitters, dtype=np.uint64)
+        n_own = len(spl) + 1
+        per = np.zeros(n_own, np.uint64)
+        tot = C.c_uint64()
+        st = lib().hga_count_partition_packed(self._h, _p(spl, C.c_uint64), n_own, C.c_void_p(out_ptr), capacity,
+                                               _p(per, C.c_uint64), C.byref(tot))
+        if st == 3 and tot.value > capacity:   # HGA_ERR_OOM: caller retries
+            return per, tot.value
+        _ck(st)
+        return per, tot.value
+
+    def count_merge_packed(self, pieces_ptr: int, n: int, min_per_file: int = 2):
+        _ck(lib().hga_count_merge_packed(self._h, C.c_void_p(pieces_ptr), n, min_per_file))
 
     def rows(self):
         k = _u64p()

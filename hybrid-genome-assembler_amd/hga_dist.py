@@ -14,6 +14,9 @@ world_size 2) drive exactly this code:
     engine.count_local()                 -> rows   (count of this rank's shard, no drop)
     engine.partition(splitters, keys_buf, counts_buf) -> rows per owner (np.uint64)
     engine.merge(keys, counts, n, min_per_file)
+    engine.pack_bits()                   -> bits per file count in the packed form (0: wide only)
+    engine.partition_packed(splitters, buf, capacity) -> (pieces per owner, total)
+    engine.merge_packed(buf, n, min_per_file)
     engine.spec_hist(thresholds)         -> int64 [m, 3] (threshold index, total, count)
     engine.select(lower, upper)          -> (keys np.uint64 ascending, flags np.uint8)
     engine.select_device(lower, upper)   -> (n, n_discriminative)
@@ -59,6 +62,15 @@ class HgaEngine:
     def merge(self, keys: torch.Tensor, counts: torch.Tensor, n: int, min_per_file: int):
         self.ctx.count_merge(keys.data_ptr(), counts.data_ptr(), n, min_per_file)
 
+    def pack_bits(self) -> int:
+        return self.ctx.count_pack_bits()
+
+    def partition_packed(self, splitters, buf: torch.Tensor, capacity: int):
+        return self.ctx.count_partition_packed(splitters, buf.data_ptr(), capacity)
+
+    def merge_packed(self, buf: torch.Tensor, n: int, min_per_file: int):
+        self.ctx.count_merge_packed(buf.data_ptr(), n, min_per_file)
+
     def spec_hist(self, thresholds):
         return self.ctx.spec_hist(thresholds)
 
@@ -95,10 +107,41 @@ class OwnerExchange:
                                group=self.group)
 
     def count(self, min_per_file: int = 2) -> int:
-        """Local count, owner exchange, owner merge.  Returns the owner's merged row count."""
-        e, F = self.e, self.e.n_files
+        """Local count, owner exchange, owner merge.  Returns the rows/pieces this owner received."""
+        e = self.e
         rows = e.count_local()
         self.local_rows = rows
+        if e.pack_bits() > 0:
+            return self._count_packed(rows, min_per_file)
+        return self._count_wide(rows, min_per_file)
+
+    def _count_packed(self, rows: int, min_per_file: int) -> int:
+        """One u64 per row piece: half the all-to-all bytes of the wide form."""
+        e = self.e
+        cap = rows + rows // 64 + 1024
+        buf = torch.empty(cap, dtype=torch.int64, device=e.device)
+        per, total = e.partition_packed(self.splitters, buf, cap)
+        if total > cap:   # many rows with huge counts: retry with room for every piece
+            cap = total
+            buf = torch.empty(cap, dtype=torch.int64, device=e.device)
+            per, total = e.partition_packed(self.splitters, buf, cap)
+        per = np.asarray(per, dtype=np.int64)
+        send_n = torch.from_numpy(per).to(self.comm_dev)
+        recv_n = torch.empty_like(send_n)
+        self._a2a(recv_n, send_n, None, None)
+        rn = recv_n.cpu().numpy().astype(np.int64)
+        n = int(rn.sum())
+        rbuf = torch.empty(n, dtype=torch.int64, device=self.comm_dev)
+        self._a2a(rbuf, buf[:total].to(self.comm_dev), rn.tolist(), per.tolist())
+        rbuf = rbuf.to(e.device)
+        if e.device.type == "cuda":
+            torch.cuda.synchronize(e.device)
+        e.merge_packed(rbuf, n, min_per_file)
+        self.received_rows = n
+        return n
+
+    def _count_wide(self, rows: int, min_per_file: int) -> int:
+        e, F = self.e, self.e.n_files
         keys = torch.empty(rows, dtype=torch.int64, device=e.device)
         cnts = torch.empty(rows * F, dtype=torch.int32, device=e.device)
         per = np.asarray(e.partition(self.splitters, keys, cnts), dtype=np.int64)

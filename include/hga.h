@@ -132,6 +132,21 @@ hga_status hga_count_partition(hga_ctx* ctx, const uint64_t* splitters, uint32_t
 hga_status hga_count_merge(hga_ctx* ctx, const uint64_t* keys, const uint32_t* counts, uint64_t n,
                            uint32_t min_per_file);
 
+/* Packed form of the same exchange (half the bytes): one u64 per row piece, key in the low 2k
+ * bits, file f's count in the `bits` bits above it (bits = (64 - 2k) / n_files, 0 when below 4
+ * or n_files > 8: use the wide form).  A row whose count exceeds 2^bits - 1 is sent as several
+ * pieces with the same key; the owner's merge sums them.
+ *   hga_count_partition_packed: pieces grouped by owner into DEVICE buffer out[capacity];
+ *     pieces_per_owner[n_owners] and *total (host).  If *total > capacity nothing is written
+ *     and HGA_ERR_OOM is returned (call again with room for *total).
+ *   hga_count_merge_packed: the pieces this owner received (DEVICE pointer, any order). */
+hga_status hga_count_pack_bits(hga_ctx* ctx, int* bits);
+hga_status hga_count_partition_packed(hga_ctx* ctx, const uint64_t* splitters, uint32_t n_owners,
+                                      uint64_t* out, uint64_t capacity, uint64_t* pieces_per_owner,
+                                      uint64_t* total);
+hga_status hga_count_merge_packed(hga_ctx* ctx, const uint64_t* pieces, uint64_t n,
+                                  uint32_t min_per_file);
+
 /* ------------------------------------------------------------------------------
  * SDK lookup — replaces the per-read loop of ReadClusteringEngine::construct_indices
  * (src/clustering/ReadClusteringEngine.cpp:234-299).  The host keeps SDK loading

@@ -46,13 +46,13 @@ def make_streams(seed=7, n_reads=600, L=3000):
     return out
 
 
-def _worker(rank, world, port, lower, upper, out_path):
+def _worker(rank, world, port, lower, upper, out_path, packed=True):
     from dist_engine_oracle import OracleEngine
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         streams = make_streams()
         shards = [hga_dist.shard_reads(s, rank, world) for s in streams]
-        ex = hga_dist.OwnerExchange(OracleEngine(shards, K))
+        ex = hga_dist.OwnerExchange(OracleEngine(shards, K, packed))
         ex.count(2)
         hist = ex.spec_hist(THR)
         keys, flags = ex.select(lower, upper)
@@ -63,15 +63,16 @@ def _worker(rank, world, port, lower, upper, out_path):
         dist.destroy_process_group()
 
 
-def _run(world, tmp_path, lower=3, upper=40):
-    out = str(tmp_path / f"dist_{world}.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), lower, upper, out), nprocs=world, start_method="spawn")
+def _run(world, tmp_path, lower=3, upper=40, packed=True):
+    out = str(tmp_path / f"dist_{world}_{packed}.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), lower, upper, out, packed), nprocs=world,
+                       start_method="spawn")
     return np.load(out)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_owner_exchange_matches_single_process(world, tmp_path):
-    r = _run(world, tmp_path)
+@pytest.mark.parametrize("world,packed", [(2, True), (3, True), (2, False)])
+def test_owner_exchange_matches_single_process(world, packed, tmp_path):
+    r = _run(world, tmp_path, packed=packed)
     ref = oracle.count_pipeline(make_streams(), K, 3, 40)
     assert np.array_equal(r["hist"], ref["hist"])
     assert np.array_equal(r["keys"], ref["selected"])

@@ -126,3 +126,52 @@ def test_owner_exchange_two_processes(tmp_path):
     assert np.array_equal(r["hist"], ref["hist"])
     assert np.array_equal(r["keys"], ref["selected"])
     assert int(r["n"]) == len(ref["selected"]) and int(r["d"]) == ref["n_discr"]
+
+
+def _sim_packed(streams, k, G, min_c):
+    """Packed exchange simulated in one process: pieces per owner, owner merges its slices."""
+    F = len(streams)
+    dev = torch.device("cuda:0")
+    ctxs = [hga.Ctx(0) for _ in range(G)]
+    spl = hga_dist.owner_splitters(k, G)
+    sends = []
+    for r, c in enumerate(ctxs):
+        c.count_begin(k, F)
+        for f, s in enumerate(streams):
+            c.count_add(f, hga_dist.shard_reads(s, r, G))
+        c.count_run(1)
+        assert c.count_pack_bits() > 0
+        rows = c.count_stats().distinct_rows
+        cap = max(rows // 4, 1)   # deliberately small: exercises the retry
+        buf = torch.empty(cap, dtype=torch.int64, device=dev)
+        per, tot = c.count_partition_packed(spl, buf.data_ptr(), cap)
+        if tot > cap:
+            buf = torch.empty(tot, dtype=torch.int64, device=dev)
+            per, tot = c.count_partition_packed(spl, buf.data_ptr(), tot)
+        per = per.astype(np.int64)
+        assert int(per.sum()) == tot >= rows
+        sends.append((buf, np.concatenate([[0], np.cumsum(per)])))
+    keys, counts = [], []
+    for o, c in enumerate(ctxs):
+        rb = torch.cat([b[off[o]:off[o + 1]] for b, off in sends])
+        torch.cuda.synchronize()
+        c.count_merge_packed(rb.data_ptr(), len(rb), min_c)
+        kk, cc = c.rows()
+        keys.append(kk)
+        counts.append(cc)
+    for c in ctxs:
+        c.close()
+    return np.concatenate(keys), np.concatenate(counts)
+
+
+@pytest.mark.parametrize("k,G,min_c", [(11, 3, 2), (13, 2, 2), (19, 4, 2), (27, 2, 1), (27, 5, 3)])
+def test_packed_partition_merge_equals_oracle(k, G, min_c):
+    base = make_streams(seed=k, n_reads=300)
+    # repeated reads push counts past 2^5 - 1 at k = 27 (5 count bits per file): rows split into pieces
+    streams = [s * 40 for s in base] if k == 27 else base
+    keys, counts = _sim_packed(streams, k, G, min_c)
+    rk, rc = oracle.merge([oracle.count_stream(s, k, min_c) for s in streams])
+    assert np.array_equal(keys, rk)
+    assert np.array_equal(counts, rc)
+    if k == 27:
+        assert int(counts.max()) > 31
