@@ -85,10 +85,20 @@ class Dist:
             if backend != "nccl":
                 self.local %= max(1, torch.cuda.device_count())
             torch.cuda.set_device(self.local)
-            if backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local}"))
-            else:
-                dist.init_process_group(backend)
+            # the communication libraries may print to fd 1; stdout must carry only the JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                if backend == "nccl":
+                    dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local}"))
+                else:
+                    dist.init_process_group(backend)
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.comm_dev = f"cuda:{self.local}" if backend == "nccl" else "cpu"
             self.torch, self.dist = torch, dist
             self.pg = True
@@ -253,8 +263,9 @@ def main():
                    "k": K, "reads": ra.n + rb.n, "bases": st.bytes, "instances_per_gpu": st.instances,
                    "distinct_rows": st.distinct_rows, "selected": n_sel, "discriminative": n_disc,
                    "buckets": st.buckets, "max_split": st.max_split, "parallelism": f"dp{D.world}",
-                   "exchange": ("owner all-to-all of (key, counts) rows over RCCL, "
-                                f"{ex.local_rows} local rows -> {ex.received_rows} owned rows on rank 0")
+                   "exchange": (f"owner all-to-all over {os.environ.get('HGA_BENCH_BACKEND', 'nccl (RCCL)')} of "
+                                f"{'packed u64 row pieces' if ctx.count_pack_bits() else '(key, counts[F]) rows'}: "
+                                f"{ex.local_rows} local rows -> {ex.received_rows} owned pieces on rank 0")
                    if ex else None},
         "roofline": roofline,
         "pipeline_roofline": {"model": "16.25 B per k-mer instance (SURVEY.md §8(d))",
