@@ -112,6 +112,11 @@ hga_status hga_count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n_
     });
 }
 
+hga_status hga_count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts,
+                              uint64_t n) {
+    HGA_CTX_GUARD(c, hga::count_add_rows(c, file, keys, counts, n));
+}
+
 hga_status hga_count_run(hga_ctx* c, uint32_t min_per_file) {
     HGA_CTX_GUARD(c, hga::count_run(c, min_per_file));
 }

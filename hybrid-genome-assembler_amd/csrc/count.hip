@@ -850,6 +850,8 @@ inline unsigned blocks_for(uint64_t n, int t) { return (unsigned)((n + t - 1) / 
 
 // ================================================================ host side
 
+void merge_dump_rows(hga_ctx* c);
+
 void count_begin(hga_ctx* c, int k, uint32_t n_files) {
     HGA_REQUIRE(k >= 1 && k <= 32, HGA_ERR_INVALID, "k must be in [1,32]");
     HGA_REQUIRE(n_files >= 1 && n_files <= 64, HGA_ERR_INVALID, "n_files must be in [1,64]");
@@ -858,6 +860,8 @@ void count_begin(hga_ctx* c, int k, uint32_t n_files) {
     s.seq.clear();
     s.seq_len.assign(n_files, 0);
     for (uint32_t i = 0; i < n_files; ++i) s.seq.push_back(new DevBuf());
+    s.dump_keys.assign(n_files, {});
+    s.dump_cnt.assign(n_files, {});
     s.k = k;
     s.n_files = n_files;
     s.begun = true;
@@ -1054,6 +1058,63 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     s.rows_cap = cap;
     s.ran = true;
     s.n_sel = 0;
+    merge_dump_rows(c);
+}
+
+// Pre-counted rows of a file whose `<reads>_<k>-mers_sorted` cache exists
+// (JellyfishOccurrenceReader.cpp:19-24 skips jellyfish for it and reads the dump verbatim).
+void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts, uint64_t n) {
+    auto& s = c->count;
+    HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
+    HGA_REQUIRE(file < s.n_files, HGA_ERR_INVALID, "file index out of range");
+    HGA_REQUIRE(n == 0 || (keys && counts), HGA_ERR_INVALID, "null rows pointer");
+    const uint64_t lim = s.k >= 32 ? ~0ull : (1ull << (2 * s.k)) - 1;
+    auto& dk = s.dump_keys[file];
+    auto& dc = s.dump_cnt[file];
+    for (uint64_t i = 0; i < n; ++i) {
+        HGA_REQUIRE(keys[i] <= lim, HGA_ERR_INVALID, "dump key exceeds 4^k - 1");
+        if (!counts[i]) continue;
+        dk.push_back(keys[i]);
+        dc.push_back(counts[i]);
+    }
+    s.ran = false;
+}
+
+// Folds the staged dump rows into the counted rows: one merge (sum per key, no drop: the
+// reference reads cached dumps as they are), leaving the rows ascending.
+void merge_dump_rows(hga_ctx* c) {
+    auto& s = c->count;
+    const uint32_t F = s.n_files;
+    uint64_t nd = 0;
+    for (auto& v : s.dump_keys) nd += v.size();
+    if (!nd) return;
+    const uint64_t n = s.rows + nd;
+    std::vector<uint64_t> hk;
+    std::vector<uint32_t> hc;
+    hk.reserve(nd);
+    hc.assign(nd * F, 0);
+    for (uint32_t f = 0; f < F; ++f)
+        for (uint64_t i = 0; i < s.dump_keys[f].size(); ++i) {
+            hc[hk.size() * F + f] = s.dump_cnt[f][i];
+            hk.push_back(s.dump_keys[f][i]);
+        }
+    DevBuf tk, tc, ti;
+    uint64_t* k = static_cast<uint64_t*>(tk.ensure(n * 8));
+    uint32_t* cc = static_cast<uint32_t*>(tc.ensure(n * 4 * F));
+    if (s.rows) {
+        uint32_t* v = static_cast<uint32_t*>(ti.ensure(s.rows * 4));
+        HGA_HIP(hipMemcpyAsync(k, s.rows_key.p, s.rows * 8, hipMemcpyDeviceToDevice, c->stream));
+        hipLaunchKernelGGL(kc_iota, dim3(blocks_for(s.rows, 256)), dim3(256), 0, c->stream, v, s.rows);
+        c->check_launch("kc_iota");
+        hipLaunchKernelGGL(kc_gather_rows, dim3(blocks_for(s.rows, 256)), dim3(256), 0, c->stream, v,
+                           s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, F, cc);
+        c->check_launch("kc_gather_rows");
+    }
+    HGA_HIP(hipMemcpyAsync(k + s.rows, hk.data(), nd * 8, hipMemcpyHostToDevice, c->stream));
+    HGA_HIP(hipMemcpyAsync(cc + s.rows * F, hc.data(), nd * 4 * F, hipMemcpyHostToDevice, c->stream));
+    const uint32_t min_c = s.min_per_file;
+    count_merge(c, k, cc, n, 1);   // synchronises before the host staging goes out of scope
+    s.min_per_file = min_c;
 }
 
 void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::vector<int64_t>& out) {

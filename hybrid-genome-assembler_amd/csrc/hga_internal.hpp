@@ -129,6 +129,9 @@ struct CountState {
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     std::vector<char> tab_host;   // last uploaded per-file tables
+    // pre-counted dump rows per file (hga_count_add_rows), merged verbatim at the end of count_run
+    std::vector<std::vector<uint64_t>> dump_keys;
+    std::vector<std::vector<uint32_t>> dump_cnt;
     uint32_t buckets = 0, fb = 0, max_split = 1;
     ~CountState() {
         for (auto* b : seq) delete b;
@@ -197,6 +200,7 @@ void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<u
 void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* keys_out,
                      uint32_t* counts_out, uint64_t* rows_per_owner);
 void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min_c);
+void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts, uint64_t n);
 int count_pack_bits(hga_ctx* c);
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,
                                 uint64_t cap_out, uint64_t* pieces_per_owner);

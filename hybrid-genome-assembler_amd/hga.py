@@ -59,6 +59,7 @@ HGA_SYMBOLS = {
     "hga_ctx_destroy": (C.c_int, [_vp]),
     "hga_count_begin": (C.c_int, [_vp, C.c_int, C.c_uint32]),
     "hga_count_add": (C.c_int, [_vp, C.c_uint32, C.c_char_p, C.c_uint64]),
+    "hga_count_add_rows": (C.c_int, [_vp, C.c_uint32, _u64p, _u32p, C.c_uint64]),
     "hga_count_run": (C.c_int, [_vp, C.c_uint32]),
     "hga_count_get_stats": (C.c_int, [_vp, C.POINTER(CountStats)]),
     "hga_count_spec_hist": (C.c_int, [_vp, C.POINTER(C.c_double), C.c_uint32, C.POINTER(_i64p), _u64p]),
@@ -201,6 +202,14 @@ class Ctx:
 
     def count_add(self, file: int, seq: bytes):
         _ck(lib().hga_count_add(self._h, file, seq, len(seq)))
+
+    def count_add_rows(self, file: int, keys, counts):
+        """Rows of a cached `<reads>_<k>-mers_sorted` dump for `file` (summed in verbatim)."""
+        k = np.ascontiguousarray(keys, dtype=np.uint64)
+        c = np.ascontiguousarray(counts, dtype=np.uint32)
+        if len(k) != len(c):
+            raise ValueError("keys and counts differ in length")
+        _ck(lib().hga_count_add_rows(self._h, file, k.ctypes.data_as(_u64p), c.ctypes.data_as(_u32p), len(k)))
 
     def count_run(self, min_per_file: int = 2):
         _ck(lib().hga_count_run(self._h, min_per_file))

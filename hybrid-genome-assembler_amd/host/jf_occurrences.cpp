@@ -12,10 +12,16 @@
 // (:57), one k-mer per line in ascending order, and the final
 // "{d} out of {e} exported kmers are discriminative" line without newline (:133).
 //
+// Dump cache (JellyfishOccurrenceReader.cpp:19-24): a file whose "<reads>_<k>-mers_sorted"
+// exists is not read at all, its dump rows are merged verbatim (hga_count_add_rows); for every
+// other file the GPU count is written back as that dump, "KMER COUNT" lines in LC_ALL=C order,
+// as run_jellyfish.sh:5-6 would leave it.  HGA_DUMP_CACHE=0 skips writing.
+//
 // HGA_DEVICE selects the GPU (default 0); HGA_PLOT_CMD overrides the plot command.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <filesystem>
 #include <iostream>
 #include <map>
 #include <random>
@@ -105,11 +111,31 @@ int main(int argc, char* argv[]) {
     hga_ctx* ctx = nullptr;
     check(hga_ctx_create(&ctx, dev_env ? std::atoi(dev_env) : 0), "hga_ctx_create");
     check(hga_count_begin(ctx, k, (uint32_t)read_paths.size()), "hga_count_begin");
+    std::vector<uint32_t> counted;
     for (uint32_t f = 0; f < read_paths.size(); ++f) {
+        const std::string cache = hgah::dump_cache_path(read_paths[f], k);
+        if (std::filesystem::exists(cache)) {
+            std::vector<uint64_t> dk;
+            std::vector<uint32_t> dc;
+            hgah::read_kmer_dump(cache, k, dk, dc);
+            check(hga_count_add_rows(ctx, f, dk.data(), dc.data(), dk.size()), "hga_count_add_rows");
+            continue;
+        }
         const std::string s = hgah::jf_stream(read_paths[f]);
         check(hga_count_add(ctx, f, s.data(), s.size()), "hga_count_add");
+        counted.push_back(f);
     }
     check(hga_count_run(ctx, 2), "hga_count_run");   // jellyfish --bc: per-file singletons dropped
+    const char* cache_env = std::getenv("HGA_DUMP_CACHE");
+    if (!(cache_env && std::string(cache_env) == "0"))
+        for (uint32_t f : counted) {
+            uint64_t *dk = nullptr, n_d = 0;
+            uint32_t* dc = nullptr;
+            check(hga_count_dump(ctx, f, &dk, &dc, &n_d), "hga_count_dump");
+            hgah::write_kmer_dump(hgah::dump_cache_path(read_paths[f], k), k, dk, dc, n_d);
+            hga_free(dk);
+            hga_free(dc);
+        }
 
     const std::set<double> thresholds = {70, 85, 90, 95, 99, 100, 100.01};
     const std::vector<double> thr(thresholds.begin(), thresholds.end());

@@ -318,4 +318,82 @@ uint64_t line_canonical(const char* s, size_t len) {
     return fwd < rc ? fwd : rc;
 }
 
+std::string dump_cache_path(const std::string& reads, int k) {
+    return reads + "_" + std::to_string(k) + "-mers_sorted";
+}
+
+void read_kmer_dump(const std::string& path, int k, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
+    std::FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) throw std::invalid_argument("cannot open k-mer dump " + path);
+    std::string data;
+    std::fseek(f, 0, SEEK_END);
+    const long sz = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    data.resize(sz > 0 ? (size_t)sz : 0);
+    const bool ok = sz <= 0 || std::fread(&data[0], 1, (size_t)sz, f) == (size_t)sz;
+    std::fclose(f);
+    if (!ok) throw std::runtime_error("short read on " + path);
+    keys.clear();
+    counts.clear();
+    const char* p = data.data();
+    const char* end = p + data.size();
+    uint64_t line_no = 0;
+    while (p < end) {
+        const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
+        const char* e = nl ? nl : end;
+        ++line_no;
+        if (e > p) {
+            const char* sp = static_cast<const char*>(std::memchr(p, ' ', (size_t)(e - p)));
+            if (!sp || sp - p != k)
+                throw std::invalid_argument(path + ":" + std::to_string(line_no) + ": expected \"<" +
+                                            std::to_string(k) + "-mer> <count>\"");
+            uint64_t code = 0;
+            for (const char* q = p; q < sp; ++q) {
+                uint64_t v;
+                switch (*q) {
+                    case 'A': v = 0; break;
+                    case 'C': v = 1; break;
+                    case 'G': v = 2; break;
+                    case 'T': v = 3; break;
+                    default:
+                        throw std::invalid_argument(path + ":" + std::to_string(line_no) + ": non-ACGT k-mer");
+                }
+                code = (code << 2) | v;
+            }
+            const char* c = sp;
+            while (c < e && *c == ' ') ++c;
+            uint32_t cnt = 0;
+            auto r = std::from_chars(c, e, cnt);
+            if (r.ec != std::errc() || c == e)
+                throw std::invalid_argument(path + ":" + std::to_string(line_no) + ": bad count");
+            keys.push_back(code);
+            counts.push_back(cnt);
+        }
+        p = nl ? nl + 1 : end;
+    }
+}
+
+void write_kmer_dump(const std::string& path, int k, const uint64_t* keys, const uint32_t* counts, uint64_t n) {
+    std::FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + path);
+    std::vector<char> buf;
+    buf.reserve(1 << 20);
+    char num[16];
+    for (uint64_t i = 0; i < n; ++i) {
+        const size_t at = buf.size();
+        buf.resize(at + (size_t)k);
+        kmer_to_chars(keys[i], k, buf.data() + at);
+        buf.push_back(' ');
+        auto r = std::to_chars(num, num + sizeof(num), counts[i]);
+        buf.insert(buf.end(), num, r.ptr);
+        buf.push_back('\n');
+        if (buf.size() > (1u << 20)) {
+            std::fwrite(buf.data(), 1, buf.size(), f);
+            buf.clear();
+        }
+    }
+    std::fwrite(buf.data(), 1, buf.size(), f);
+    if (std::fclose(f) != 0) throw std::runtime_error("cannot write " + path);
+}
+
 }  // namespace hgah

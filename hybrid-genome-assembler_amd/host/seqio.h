@@ -59,4 +59,13 @@ void kmer_to_chars(uint64_t code, int k, char* out);
 // KmerIterator canonical code of a whole line (load_text_file_kmers, read_clustering.cpp:18-33).
 uint64_t line_canonical(const char* s, size_t len);
 
+// "<reads>_<k>-mers_sorted" dump cache (JellyfishOccurrenceReader.cpp:19-24; written by
+// run_jellyfish.sh:5-6 as `jellyfish dump -c` + LC_ALL=C sort): one "KMER COUNT" line per
+// k-mer.  read_kmer_dump parses it like parse_line (JellyfishOccurrenceReader.cpp:9-14); the
+// k-mer string is kept as it is (its forward 2-bit code, not re-canonicalised), and a line
+// whose k-mer is not k bases of ACGT throws.  write_kmer_dump writes rows in the given order.
+void read_kmer_dump(const std::string& path, int k, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);
+void write_kmer_dump(const std::string& path, int k, const uint64_t* keys, const uint32_t* counts, uint64_t n);
+std::string dump_cache_path(const std::string& reads, int k);   // "{reads}_{k}-mers_sorted"
+
 }  // namespace hgah

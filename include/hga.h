@@ -63,6 +63,16 @@ hga_status hga_count_begin(hga_ctx* ctx, int k, uint32_t n_files);
  * several times per file; a read must not straddle two calls. */
 hga_status hga_count_add(hga_ctx* ctx, uint32_t file, const char* seq, uint64_t n_bytes);
 
+/* Adds file `file`'s rows from an existing "<reads>_<k>-mers_sorted" dump instead of its
+ * reads: the reference skips jellyfish for a file whose dump exists and merges the dump
+ * verbatim (src/occurrences/JellyfishOccurrenceReader.cpp:19-24 and the reader's
+ * get_next_kmer, :63-86).  keys = canonical codes (< 4^k, any order), counts >= 1
+ * (rows with count 0 are ignored); copied, may be freed on return.  hga_count_run then
+ * counts the files given by reads (with the per-file drop) and sums in the dump rows
+ * without dropping any.  A file may have both reads and rows; their counts add. */
+hga_status hga_count_add_rows(hga_ctx* ctx, uint32_t file, const uint64_t* keys, const uint32_t* counts,
+                              uint64_t n);
+
 /* Runs the device pipeline on everything added: canonical k-mers, per-file exact
  * counts, per-file drop of k-mers whose count is < min_per_file (2 = jellyfish
  * `--bc`), merge across files.  May be re-run (bench). */

@@ -1,5 +1,6 @@
 """End-to-end runs of the drop-in CLIs (bin/jf_occurrences, bin/categorization) on the GPU."""
 import os
+import shutil
 import subprocess
 
 import numpy as np
@@ -27,11 +28,24 @@ def expected_wire(hist, k):
     return f"1 200\n({k}, [{', '.join(bounds)}])"
 
 
+def stage_reads(tmp_path, names=("reads_a.fq", "reads_b.fq")):
+    """Copies of the golden reads: jf_occurrences writes its dump caches next to them."""
+    out = []
+    for n in names:
+        shutil.copy(os.path.join(GOLD, n), tmp_path / n)
+        out.append(str(tmp_path / n))
+    return out
+
+
+def dump_text(keys, counts, k):
+    return "".join(f"{kmer_str(c, k)} {int(n)}\n" for c, n in zip(keys, counts))
+
+
 @pytest.mark.parametrize("k,stdin,fname", [(19, "3 12 1\n", "19-mers_3_12_100%.txt"),
                                            (15, "2 40 1.0\n", "15-mers_2_40_100%.txt")])
 def test_jf_occurrences_end_to_end(tmp_path, hga_mod, k, stdin, fname):
     lower, upper = int(stdin.split()[0]), int(stdin.split()[1])
-    paths = [os.path.join(GOLD, p) for p in ("reads_a.fq", "reads_b.fq")]
+    paths = stage_reads(tmp_path)
     env = dict(os.environ, HGA_PLOT_CMD=f"cat > {tmp_path}/wire.txt")
     out = subprocess.run([os.path.join(BIN, "jf_occurrences"), *paths, "-k", str(k)], input=stdin, text=True,
                          capture_output=True, cwd=tmp_path, env=env, timeout=300)
@@ -46,7 +60,7 @@ def test_jf_occurrences_end_to_end(tmp_path, hga_mod, k, stdin, fname):
 
 
 def test_jf_occurrences_output_option_and_sampling(tmp_path, hga_mod):
-    paths = [os.path.join(GOLD, p) for p in ("reads_a.fq", "reads_b.fq")]
+    paths = stage_reads(tmp_path)
     env = dict(os.environ, HGA_PLOT_CMD="cat > /dev/null")
     out = subprocess.run([os.path.join(BIN, "jf_occurrences"), *paths, "--k-size=19", "-o", "sel.txt"],
                          input="3 12 0.5", text=True, capture_output=True, cwd=tmp_path, env=env, timeout=300)
@@ -56,6 +70,63 @@ def test_jf_occurrences_output_option_and_sampling(tmp_path, hga_mod):
     allk = {kmer_str(c, 19) for c in full["selected"]}
     assert set(got) <= allk and got == sorted(got)
     assert 0 < len(got) < len(allk)
+
+
+def test_jf_occurrences_writes_dump_cache(tmp_path, hga_mod):
+    """Every counted file leaves "<reads>_<k>-mers_sorted" as run_jellyfish.sh:5-6 would."""
+    paths = stage_reads(tmp_path)
+    env = dict(os.environ, HGA_PLOT_CMD="cat > /dev/null")
+    out = subprocess.run([os.path.join(BIN, "jf_occurrences"), *paths, "-k", "17"], input="3 12 1",
+                         text=True, capture_output=True, cwd=tmp_path, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr
+    for p in paths:
+        keys, counts = oracle.count_stream(hga_mod.jf_stream(p), 17, 2)
+        assert open(p + "_17-mers_sorted").read() == dump_text(keys, counts, 17)
+
+
+def test_jf_occurrences_reads_dump_cache(tmp_path, hga_mod):
+    """A file with an existing dump is not read; its rows (even count 1) are merged verbatim
+    (JellyfishOccurrenceReader.cpp:19-24, 63-86)."""
+    k = 19
+    paths = stage_reads(tmp_path)
+    stream_b = hga_mod.jf_stream(paths[1])
+    ka, ca = oracle.count_stream(hga_mod.jf_stream(paths[0]), k, 2)
+    rng = np.random.default_rng(5)
+    ca = ca.copy()
+    ca[rng.integers(0, len(ca), 200)] = 1                      # counts the GPU drop would remove
+    extra = rng.integers(0, 1 << (2 * k), 300, dtype=np.uint64)  # k-mers absent from the reads
+    ka2 = np.concatenate([ka, extra])
+    ca2 = np.concatenate([ca, rng.integers(1, 40, 300).astype(np.uint32)])
+    keep = np.unique(ka2, return_index=True)[1]
+    ka2, ca2 = ka2[keep], ca2[keep]
+    open(paths[0] + f"_{k}-mers_sorted", "w").write(dump_text(ka2, ca2, k))
+    open(paths[0], "w").write("not a read file\n")          # must not be opened
+    env = dict(os.environ, HGA_PLOT_CMD=f"cat > {tmp_path}/wire.txt")
+    out = subprocess.run([os.path.join(BIN, "jf_occurrences"), *paths, "-k", str(k)], input="2 30 1",
+                         text=True, capture_output=True, cwd=tmp_path, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr
+    kb, cb = oracle.count_stream(stream_b, k, 2)
+    keys, counts = oracle.merge([(ka2, ca2), (kb, cb)])
+    hist = oracle.specificity(counts, oracle.THRESHOLDS)
+    sel, disc = oracle.select(keys, counts, 2, 30)
+    assert out.stdout.endswith(f"{disc} out of {len(sel)} exported kmers are discriminative")
+    assert open(tmp_path / "wire.txt").read() == expected_wire(hist, k)
+    assert open(tmp_path / "19-mers_2_30_100%.txt").read() == "".join(kmer_str(c, k) + "\n" for c in sel)
+    assert open(paths[1] + f"_{k}-mers_sorted").read() == dump_text(kb, cb, k)
+
+
+@pytest.mark.parametrize("tool", ["bin", "script"])
+def test_run_jellyfish_dump(tmp_path, hga_mod, tool):
+    """run_jellyfish(.sh) <reads> <k> <sorted>: the dump contract of run_jellyfish.sh:3-6."""
+    reads = stage_reads(tmp_path, ("reads_c.fa",))[0]
+    exe = (os.path.join(BIN, "run_jellyfish") if tool == "bin" else
+           os.path.join(ROOT, "hybrid-genome-assembler_amd", "scripts", "run_jellyfish.sh"))
+    out = subprocess.run([exe, reads, "15", str(tmp_path / "sorted")], capture_output=True, text=True,
+                         cwd=tmp_path, timeout=300)
+    assert out.returncode == 0, out.stderr
+    keys, counts = oracle.count_stream(hga_mod.jf_stream(reads), 15, 2)
+    assert len(keys) > 0
+    assert open(tmp_path / "sorted").read() == dump_text(keys, counts, 15)
 
 
 def test_categorization_end_to_end(tmp_path):

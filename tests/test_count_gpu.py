@@ -166,3 +166,62 @@ def test_count_level1_overflow_retry(gpu_ctx, hga_mod):
     streams = [b"A" * 3_000_000 + b"\n" + g, b"C" * 1_000_000 + b"\n" + g[:200_000]]
     o = oracle.count_pipeline(streams, 21, 1, 10 ** 9, min_count=1)
     assert_same(run_gpu(gpu_ctx, streams, 21, 1, 10 ** 9, min_count=1), o)
+
+
+@pytest.mark.parametrize("k,F", [(19, 2), (13, 3), (32, 2)])
+def test_count_add_rows_merges_dumps_verbatim(gpu_ctx, hga_mod, k, F):
+    """hga_count_add_rows: a cached dump's rows are summed in without the per-file drop
+    (JellyfishOccurrenceReader.cpp:19-24 reads an existing dump instead of counting)."""
+    rng = np.random.default_rng(k * 10 + F)
+    streams = golden_streams(hga_mod) + [b""] * (F - 2)
+    lim = (1 << (2 * k)) - 1
+    extra = []
+    for f in range(F):
+        n = 400 + 100 * f
+        ks = np.unique(rng.integers(0, lim, n, dtype=np.uint64, endpoint=True))
+        if f == 0:   # overlap with counted k-mers of file 0 so sums happen
+            k0, _ = oracle.count_stream(streams[0], k, 1)
+            ks = np.unique(np.concatenate([ks, k0[::7]]))
+        extra.append((ks, rng.integers(1, 5, len(ks)).astype(np.uint32)))
+    gpu_ctx.count_begin(k, F)
+    for f in range(F):
+        if streams[f]:
+            gpu_ctx.count_add(f, streams[f])
+        gpu_ctx.count_add_rows(f, extra[f][0][::-1], extra[f][1][::-1])   # any order
+    gpu_ctx.count_run(2)
+    keys, counts = gpu_ctx.rows()
+    dumps = []
+    for f in range(F):
+        d = {}
+        if streams[f]:
+            kk, cc = oracle.count_stream(streams[f], k, 2)
+            d = dict(zip(kk.tolist(), cc.tolist()))
+        for kk, cc in zip(*extra[f]):
+            d[int(kk)] = d.get(int(kk), 0) + int(cc)
+        ks = np.array(sorted(d), np.uint64)
+        dumps.append((ks, np.array([d[x] for x in ks.tolist()], np.uint32)))
+    ok, oc = oracle.merge(dumps)
+    assert np.array_equal(keys, ok) and np.array_equal(counts, oc)
+    for f in range(F):
+        dk, dc = gpu_ctx.dump(f)
+        assert np.array_equal(dk, dumps[f][0]) and np.array_equal(dc, dumps[f][1])
+    hist = gpu_ctx.spec_hist(oracle.THRESHOLDS)
+    assert np.array_equal(hist, oracle.specificity(oc, oracle.THRESHOLDS))
+
+
+def test_count_add_rows_only(gpu_ctx):
+    """All files cached: no reads at all, rows come from the dumps alone."""
+    gpu_ctx.count_begin(11, 2)
+    gpu_ctx.count_add_rows(0, np.array([5, 1, 9], np.uint64), np.array([3, 1, 0], np.uint32))
+    gpu_ctx.count_add_rows(1, np.array([9, 4], np.uint64), np.array([2, 7], np.uint32))
+    gpu_ctx.count_run(2)
+    keys, counts = gpu_ctx.rows()
+    assert keys.tolist() == [1, 4, 5, 9]
+    assert counts.tolist() == [[1, 0], [0, 7], [3, 0], [0, 2]]
+    with pytest.raises(hga_err()):
+        gpu_ctx.count_add_rows(0, np.array([1 << 22], np.uint64), np.array([1], np.uint32))
+
+
+def hga_err():
+    import hga
+    return hga.HgaError
