@@ -183,6 +183,57 @@ def cpu_lookup_baseline(bases, offsets, sdk, threads):
             "seconds": round(dt, 3)}
 
 
+def connections_leg(ctx2, D, reps, args):
+    """get_all_connections(1) (ReadClusteringEngine.cpp:335-339, the default first clustering
+    stage, :754) on the C3 indices left on the device by the lookup."""
+    ctx2.connections_run(min_score=1)
+    ctx2.profile(True)
+    ctx2.profile_reset()
+    for _ in range(reps):
+        ctx2.connections_run(min_score=1)
+    kern = {}
+    for name in ("cn_local", "cn_global", "cn_sort", "radix_upsweep", "radix_downsweep", "scan"):
+        ms, n = ctx2.profile_get(name)
+        if n:
+            kern[name] = round(ms / reps, 4)
+    ctx2.profile(False)
+    D.barrier()
+    ctx2.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        n_conn = ctx2.connections_run(min_score=1)
+    ctx2.sync()
+    D.barrier()
+    dt = D.max((time.perf_counter() - t0) / reps)
+    idx = ctx2.lookup_fetch()
+    lens = np.diff(idx["kci_ptr"]).astype(np.float64)
+    pairs_walked = float((lens * lens).sum())    # (id, candidate) pairs over all pivots
+    H = float(len(idx["sorted_kid"]))
+    # per pivot hit: KmerID 4 B + kci_ptr pair 16 B; per walked pair: candidate 4 B; per kept pair 12 B
+    cn_bytes = 20 * H + 4 * pairs_walked + 12 * n_conn
+    cn_ms = kern.get("cn_local", 0) + kern.get("cn_global", 0)
+    out = {"call": "get_all_connections(min_score=1) on the C3 indices", "ms": round(dt * 1e3, 3),
+           "connections": int(n_conn), "pairs_walked": int(pairs_walked),
+           "pivots_per_s": round(D.sum(float(len(idx["hit_ptr"]) - 1)) / dt, 1), "kernels_ms": kern,
+           "roofline": {"bound": "hbm", "kernel": "cn_local", "model": "20 B per hit + 4 B per walked "
+                        "(id, candidate) pair + 12 B per kept pair",
+                        "achieved": round(cn_bytes / (cn_ms * 1e-3) / 1e9, 1) if cn_ms else None,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s"}}
+    if not args.no_cpu and D.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        n_p = 2000
+        piv = np.arange(1, n_p + 1, dtype=np.uint32)
+        t0 = time.perf_counter()
+        oracle.connections(idx, pivots=piv, min_score=1)
+        dtc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n_p / dtc, 1), "unit": "pivots/s", "cores": 1, "kind": "port",
+                               "sample": f"first {n_p} C3 reads as pivots, oracle get_connections "
+                                         "(unordered_map per pivot, 1 thread, like the reference's default -t 1)",
+                               "seconds": round(dtc, 3)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -317,6 +368,7 @@ def main():
             "lookup_roofline": {"model": "12.25 B per window per walk + 12 B per hit (SURVEY.md §8(d))",
                                 "achieved": round(lk_bytes / (lk_ms * 1e-3) / 1e9, 1) if lk_ms else None},
         }
+        result["categorize"]["connections"] = connections_leg(ctx2, D, reps, args)
         ctx2.close()
         if not args.no_cpu and D.rank == 0:
             result["categorize"]["cpu_baseline"] = cpu_lookup_baseline(bases, offsets, sdk, args.cpu_threads)

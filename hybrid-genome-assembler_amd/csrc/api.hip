@@ -112,6 +112,19 @@ hga_status hga_count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n_
     });
 }
 
+hga_status hga_connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_pivots, uint32_t min_kmers,
+                               uint64_t min_score, const int32_t* categories, uint64_t* n) {
+    HGA_CTX_GUARD(c, {
+        HGA_REQUIRE(n, HGA_ERR_INVALID, "null out pointer");
+        HGA_REQUIRE(pivots || n_pivots == 0, HGA_ERR_INVALID, "null pivots with n_pivots > 0");
+        hga::connections_run(c, pivots, n_pivots, min_kmers, min_score, categories, n);
+    });
+}
+
+hga_status hga_connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good) {
+    HGA_CTX_GUARD(c, hga::connections_fetch(c, x, y, score, is_good));
+}
+
 hga_status hga_count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts,
                               uint64_t n) {
     HGA_CTX_GUARD(c, hga::count_add_rows(c, file, keys, counts, n));

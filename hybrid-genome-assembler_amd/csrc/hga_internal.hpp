@@ -155,6 +155,12 @@ struct LookupState {
     uint64_t windows = 0, hits = 0, firsts = 0, reads_hit = 0;
 };
 
+struct ConnState {
+    bool ready = false;
+    uint64_t n = 0, cap_hint = 0;
+    DevBuf piv, cat, ctr, ovf, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og;
+};
+
 }  // namespace hga
 
 struct hga_ctx {
@@ -164,6 +170,7 @@ struct hga_ctx {
     hga::Profiler prof;
     hga::CountState count;
     hga::LookupState lookup;
+    hga::ConnState conn;
     hga::PinnedBuf pinned;   // small host<->device staging (see count_spec_hist)
 
     // Launch helper: records events around the launch when profiling is on.
@@ -200,6 +207,9 @@ void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<u
 void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* keys_out,
                      uint32_t* counts_out, uint64_t* rows_per_owner);
 void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min_c);
+void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_t min_kmers, uint64_t min_score,
+                     const int32_t* categories, uint64_t* n_out);
+void connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good);
 void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts, uint64_t n);
 int count_pack_bits(hga_ctx* c);
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,

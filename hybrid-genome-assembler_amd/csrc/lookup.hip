@@ -608,6 +608,7 @@ void lookup_run(hga_ctx* c) {
     auto& L = c->lookup;
     HGA_REQUIRE(L.loaded, HGA_ERR_STATE, "hga_lookup_load not called");
     HGA_REQUIRE(L.have_reads, HGA_ERR_STATE, "hga_lookup_set_reads not called");
+    c->conn.ready = false;
     const uint64_t n = L.n_reads, nb = L.n_bases;
     const int k = L.k;
     uint64_t w = 0;

@@ -79,6 +79,8 @@ HGA_SYMBOLS = {
     "hga_lookup_run": (C.c_int, [_vp]),
     "hga_lookup_get_sizes": (C.c_int, [_vp, C.POINTER(LookupSizes)]),
     "hga_lookup_fetch": (C.c_int, [_vp, C.POINTER(LookupResult)]),
+    "hga_connections_run": (C.c_int, [_vp, _u32p, C.c_uint64, C.c_uint32, C.c_uint64, _i32p, _u64p]),
+    "hga_connections_fetch": (C.c_int, [_vp, _u32p, _u32p, _u64p, _u8p]),
     "hga_profile_enable": (C.c_int, [_vp, C.c_int]),
     "hga_profile_select": (C.c_int, [_vp, C.c_char_p]),
     "hga_profile_reset": (C.c_int, [_vp]),
@@ -326,6 +328,26 @@ class Ctx:
             setattr(r, name, _p(arr, C.c_uint64 if arr.dtype == np.uint64 else C.c_uint32))
         _ck(lib().hga_lookup_fetch(self._h, C.byref(r)))
         return out
+
+    # ---- connections (get_connections / get_all_connections on the lookup's indices)
+    def connections_run(self, pivots=None, min_kmers: int = 1, min_score: int = 1, categories=None) -> int:
+        n = C.c_uint64()
+        pv = None if pivots is None else np.ascontiguousarray(pivots, np.uint32)
+        cat = None if categories is None else np.ascontiguousarray(categories, np.int32)
+        self._keep = (pv, cat)
+        _ck(lib().hga_connections_run(self._h, None if pv is None else _p(pv, C.c_uint32),
+                                      0 if pv is None else len(pv), min_kmers, min_score,
+                                      None if cat is None else _p(cat, C.c_int32), C.byref(n)))
+        return n.value
+
+    def connections(self, pivots=None, min_kmers: int = 1, min_score: int = 1, categories=None):
+        """(x, y, score, is_good) ordered by score descending, then (x, y) ascending."""
+        m = self.connections_run(pivots, min_kmers, min_score, categories)
+        x, y = np.zeros(m, np.uint32), np.zeros(m, np.uint32)
+        sc, g = np.zeros(m, np.uint64), np.zeros(m, np.uint8)
+        _ck(lib().hga_connections_fetch(self._h, _p(x, C.c_uint32), _p(y, C.c_uint32), _p(sc, C.c_uint64),
+                                        _p(g, C.c_uint8)))
+        return x, y, sc, g
 
     # ---- measurement
     def profile(self, on: bool = True):

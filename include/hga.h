@@ -209,6 +209,30 @@ typedef struct hga_lookup_result {
 hga_status hga_lookup_fetch(hga_ctx* ctx, const hga_lookup_result* out);
 
 /* ------------------------------------------------------------------------------
+ * Connections — ReadClusteringEngine::get_connections / get_all_connections
+ * (src/clustering/ReadClusteringEngine.cpp:301-339) on the one-read components that
+ * construct_indices leaves (run after hga_lookup_run, on its device-resident indices).
+ * For pivot p and every other read c: score = sum over KmerIDs of (occurrences in p) x
+ * (occurrences in c), i.e. the robin_map count of :311-315; pairs with score >= min_score
+ * are kept (:318-325), the pivot itself never (:316).
+ * ------------------------------------------------------------------------------ */
+
+/* pivots: ReadIDs (the reference's component_ids), or NULL for every read with at least
+ *   min_kmers hits (min_kmers = 1: get_all_connections, :335-339; min_kmers = s with
+ *   min_score = s: the filter_components(... discriminative_kmer_ids.size() >= s) call
+ *   site, :750-751).  A pivot without hits yields nothing.
+ * categories: per read of the lookup (read order, n_reads), or NULL.  is_good =
+ *   categories[p] == categories[c] when given (the reference's debug mode, :319), else 0.
+ * Result order: score descending (std::sort(rbegin, rend), :331); ties, unordered in the
+ *   reference, by (pivot, candidate) ascending.  *n = number of connections. */
+hga_status hga_connections_run(hga_ctx* ctx, const uint32_t* pivots, uint64_t n_pivots, uint32_t min_kmers,
+                               uint64_t min_score, const int32_t* categories, uint64_t* n);
+/* Copies the result (caller-allocated, n entries each; any may be NULL): ComponentConnection
+ * {component_x_id = x, component_y_id = y, score, is_good}
+ * (src/clustering/ReadClusteringEngine.h:127-136). */
+hga_status hga_connections_fetch(hga_ctx* ctx, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good);
+
+/* ------------------------------------------------------------------------------
  * Measurement: per-kernel device time, recorded with HIP events on the ctx stream.
  * ------------------------------------------------------------------------------ */
 hga_status hga_profile_enable(hga_ctx* ctx, int on);

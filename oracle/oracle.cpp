@@ -419,6 +419,71 @@ int64_t or_construct_indices(const char* bases, const uint64_t* offsets, uint64_
     return (int64_t)hk.size();
 }
 
+// get_connections (src/clustering/ReadClusteringEngine.cpp:301-333) on the state that
+// construct_indices leaves: component r = read r (ReadID read_ids[r]) with
+// discriminative_kmer_ids = its sorted KmerIDs with duplicates, kmer_component_index =
+// kci_ptr/kci_read (ReadIDs).  Per pivot: count every candidate over the KmerID lists
+// (:311-315, robin_map -> unordered_map), erase the pivot (:316), keep count >= min_score
+// (:318-325); is_good = equal categories when given (debug, :319).  pivots == nullptr means
+// every read with >= min_kmers hits (get_all_connections :335-339 for min_kmers = 1, the
+// filter_components call site :750-751 otherwise); an explicit pivot list is also filtered by
+// min_kmers.  Order: score descending (:331), ties by (x, y) ascending (unordered in the
+// reference).  Returns the number of connections; arrays malloc'ed.
+int64_t or_connections(uint64_t n, const uint64_t* hit_ptr, const uint32_t* sorted_kid,
+                       const uint64_t* kci_ptr, const uint32_t* kci_read, const uint32_t* read_ids,
+                       const uint32_t* pivots, uint64_t n_piv, uint32_t min_kmers, uint64_t min_score,
+                       const int32_t* categories, uint32_t** ox, uint32_t** oy, uint64_t** os,
+                       uint8_t** og) {
+    std::unordered_map<uint32_t, uint64_t> row_of;   // ReadID -> read index (component_index)
+    for (uint64_t r = 0; r < n; ++r)
+        if (hit_ptr[r + 1] > hit_ptr[r]) row_of[read_ids[r]] = r;
+    std::vector<uint32_t> piv;
+    if (pivots) {
+        piv.assign(pivots, pivots + n_piv);
+    } else {
+        for (uint64_t r = 0; r < n; ++r) piv.push_back(read_ids[r]);
+    }
+    struct Conn { uint32_t x, y; uint64_t s; uint8_t g; };
+    std::vector<Conn> conns;
+    for (uint32_t p : piv) {
+        auto it = row_of.find(p);
+        if (it == row_of.end()) continue;
+        const uint64_t r = it->second;
+        if (hit_ptr[r + 1] - hit_ptr[r] < min_kmers) continue;
+        std::unordered_map<uint32_t, uint64_t> shared;
+        for (uint64_t i = hit_ptr[r]; i < hit_ptr[r + 1]; ++i) {
+            const uint32_t kid = sorted_kid[i];
+            for (uint64_t j = kci_ptr[kid]; j < kci_ptr[kid + 1]; ++j) shared[kci_read[j]]++;
+        }
+        shared.erase(p);
+        for (auto& kv : shared) {
+            if (kv.second < min_score) continue;
+            uint8_t g = 0;
+            if (categories) g = categories[r] == categories[row_of.at(kv.first)];
+            conns.push_back({p, kv.first, kv.second, g});
+        }
+    }
+    std::sort(conns.begin(), conns.end(), [](const Conn& a, const Conn& b) {
+        if (a.s != b.s) return a.s > b.s;
+        if (a.x != b.x) return a.x < b.x;
+        return a.y < b.y;
+    });
+    std::vector<uint32_t> x, y;
+    std::vector<uint64_t> sc;
+    std::vector<uint8_t> g;
+    for (auto& c : conns) {
+        x.push_back(c.x);
+        y.push_back(c.y);
+        sc.push_back(c.s);
+        g.push_back(c.g);
+    }
+    *ox = dup_vec(x);
+    *oy = dup_vec(y);
+    *os = dup_vec(sc);
+    *og = dup_vec(g);
+    return (int64_t)conns.size();
+}
+
 // Multi-threaded lookup-only timing kernel for the cpu_baseline leg: counts SDK hits
 // over all windows of all reads with a std::unordered_set, reads split over threads.
 uint64_t or_lookup_hits_mt(const char* bases, const uint64_t* offsets, uint64_t n, int k,

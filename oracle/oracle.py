@@ -18,6 +18,8 @@ SO = os.path.join(HERE, "_build", "liboracle.so")
 _u32p = C.POINTER(C.c_uint32)
 _u64p = C.POINTER(C.c_uint64)
 _i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
 _lib = None
 
 
@@ -57,6 +59,10 @@ def lib():
         L.or_construct_indices.argtypes = [C.c_char_p, _u64p, C.c_uint64, _u32p, C.c_int, _u64p, C.c_uint32] + \
             [C.POINTER(_u64p), C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u64p),
              C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u64p), C.POINTER(_u32p), _u64p]
+        L.or_connections.restype = C.c_int64
+        L.or_connections.argtypes = [C.c_uint64, _u64p, _u32p, _u64p, _u32p, _u32p, _u32p, C.c_uint64, C.c_uint32,
+                                     C.c_uint64, _i32p, C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u64p),
+                                     C.POINTER(_u8p)]
         L.or_lookup_hits_mt.restype = C.c_uint64
         L.or_lookup_hits_mt.argtypes = [C.c_char_p, _u64p, C.c_uint64, C.c_int, _u64p, C.c_uint32, C.c_int]
         _lib = L
@@ -168,6 +174,27 @@ def construct_indices(bases: bytes, offsets, k: int, sdk_keys, first_read_id: in
         "first_pos": _take(ptrs[6], U, np.uint32), "kci_ptr": _take(ptrs[7], K + 1, np.uint64),
         "kci_read": _take(ptrs[8], H, np.uint32),
     }
+
+
+def connections(idx, pivots=None, min_kmers: int = 1, min_score: int = 1, categories=None,
+                first_read_id: int = 1):
+    """get_connections on construct_indices output `idx` (dict of construct_indices()).
+    Returns (x, y, score, is_good), score descending then (x, y) ascending."""
+    hp = np.ascontiguousarray(idx["hit_ptr"], np.uint64)
+    n = len(hp) - 1
+    sk = np.ascontiguousarray(idx["sorted_kid"], np.uint32)
+    kp = np.ascontiguousarray(idx["kci_ptr"], np.uint64)
+    kr = np.ascontiguousarray(idx["kci_read"], np.uint32)
+    ids = np.arange(first_read_id, first_read_id + n, dtype=np.uint32)
+    pv = None if pivots is None else np.ascontiguousarray(pivots, np.uint32)
+    cat = None if categories is None else np.ascontiguousarray(categories, np.int32)
+    px, py, ps, pg = _u32p(), _u32p(), _u64p(), _u8p()
+    m = lib().or_connections(n, _p(hp, C.c_uint64), _p(sk, C.c_uint32), _p(kp, C.c_uint64), _p(kr, C.c_uint32),
+                             _p(ids, C.c_uint32), None if pv is None else _p(pv, C.c_uint32),
+                             0 if pv is None else len(pv), min_kmers, min_score,
+                             None if cat is None else _p(cat, C.c_int32),
+                             C.byref(px), C.byref(py), C.byref(ps), C.byref(pg))
+    return _take(px, m, np.uint32), _take(py, m, np.uint32), _take(ps, m, np.uint64), _take(pg, m, np.uint8)
 
 
 def lookup_hits_mt(bases: bytes, offsets, k: int, sdk_keys, threads: int) -> int:

@@ -75,3 +75,52 @@ def test_construct_indices_vs_pyref():
     for i, lst in enumerate(kci):
         a, b = int(got["kci_ptr"][i]), int(got["kci_ptr"][i + 1])
         assert got["kci_read"][a:b].tolist() == lst
+
+
+def py_connections(idx, pivots, min_kmers, min_score, categories, first_id):
+    """Pure-Python get_connections (ReadClusteringEngine.cpp:301-333) over construct_indices output."""
+    hp, sk, kp, kr = idx["hit_ptr"], idx["sorted_kid"], idx["kci_ptr"], idx["kci_read"]
+    n = len(hp) - 1
+    has = {first_id + r: r for r in range(n) if hp[r + 1] > hp[r]}
+    piv = list(range(first_id, first_id + n)) if pivots is None else [int(p) for p in pivots]
+    out = []
+    for p in piv:
+        if p not in has:
+            continue
+        r = has[p]
+        if hp[r + 1] - hp[r] < min_kmers:
+            continue
+        cnt = {}
+        for kid in sk[hp[r]:hp[r + 1]]:
+            for c in kr[kp[kid]:kp[kid + 1]]:
+                cnt[int(c)] = cnt.get(int(c), 0) + 1
+        cnt.pop(p, None)
+        for c, s in cnt.items():
+            if s >= min_score:
+                g = int(categories[r] == categories[has[c]]) if categories is not None else 0
+                out.append((p, c, s, g))
+    out.sort(key=lambda t: (-t[2], t[0], t[1]))
+    return out
+
+
+@pytest.mark.parametrize("min_kmers,min_score,use_piv", [(1, 1, False), (1, 3, False), (4, 4, False), (1, 1, True)])
+def test_oracle_connections_vs_python(min_kmers, min_score, use_piv):
+    rng = np.random.default_rng(7)
+    gnm = bytes(rng.choice(list(b"ACGT"), 4000).tolist())
+    reads = []
+    for _ in range(150):
+        s = int(rng.integers(0, 3800))
+        reads.append(gnm[s:s + int(rng.integers(20, 300))])
+    reads.append(b"A" * 40)
+    reads.append(b"A" * 25 + b"T" * 30)
+    bases = b"".join(reads)
+    offs = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    c, _ = oracle.kmer_windows(gnm, 13)
+    sdk = np.concatenate([np.unique(c)[::4], np.array([0], np.uint64)])
+    idx = oracle.construct_indices(bases, offs, 13, sdk, 5)
+    cat = (np.arange(len(reads)) % 2).astype(np.int32)
+    piv = np.arange(5, 5 + len(reads), 2, dtype=np.uint32) if use_piv else None
+    x, y, s, g = oracle.connections(idx, piv, min_kmers, min_score, cat, first_read_id=5)
+    exp = py_connections(idx, piv, min_kmers, min_score, cat, 5)
+    assert len(exp) > 10
+    assert list(zip(x.tolist(), y.tolist(), s.tolist(), g.tolist())) == exp
