@@ -234,6 +234,48 @@ def connections_leg(ctx2, D, reps, args):
     return out
 
 
+def hll_leg(ctx2, D, n_bases, bases, offsets, args):
+    """HyperLogLog k sweep of jf_occurrences' automatic k selection (KmerAnalysis.cpp:26-56):
+    registers for k = 11, 13, ..., 31 over the C3 reads already resident on the device."""
+    ks = list(range(11, 33, 2))
+    for kk in ks[:2]:
+        ctx2.hll_registers(kk)
+    ctx2.profile(True)
+    ctx2.profile_reset()
+    for kk in ks:
+        ctx2.hll_registers(kk)
+    scan_ms, _ = ctx2.profile_get("hll_scan")
+    ctx2.profile(False)
+    D.barrier()
+    t0 = time.perf_counter()
+    for kk in ks:
+        ctx2.hll_registers(kk)
+    D.barrier()
+    dt = D.max(time.perf_counter() - t0)
+    per_k = scan_ms / len(ks)
+    win = sum(max(int(l) - 19 + 1, 0) for l in np.diff(offsets))   # windows at k = 19
+    out = {"call": "hga_hll_registers(k, b=10) for k = 11..31 step 2 on the C3 reads",
+           "ms_per_k": round(dt * 1e3 / len(ks), 3), "windows_per_s": round(D.sum(win) / (dt / len(ks)), 1),
+           "kernel_ms_per_k": {"hll_scan": round(per_k, 4)},
+           "roofline": {"bound": "hbm", "kernel": "hll_scan", "model": "0.5 B per base (packed codes + valid + "
+                        "read-start bits)", "achieved": round(0.5 * n_bases / (per_k * 1e-3) / 1e9, 1) if per_k
+                        else None, "peak": HBM_PEAK_GBS, "unit": "GB/s"}}
+    if not args.no_cpu and D.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        n = min(len(offsets) - 1, 8000)
+        sub_off = offsets[: n + 1]
+        sub = bases[: int(sub_off[-1])]
+        w = sum(max(int(l) - 19 + 1, 0) for l in np.diff(sub_off))
+        t0 = time.perf_counter()
+        oracle.hll_registers(sub, sub_off, 19)
+        dtc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(w / dtc, 1), "unit": "windows/s", "cores": 1, "kind": "port",
+                               "sample": f"first {n} C3 reads at k=19, oracle HyperLogLog add (1 thread)",
+                               "seconds": round(dtc, 3)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -369,6 +411,7 @@ def main():
                                 "achieved": round(lk_bytes / (lk_ms * 1e-3) / 1e9, 1) if lk_ms else None},
         }
         result["categorize"]["connections"] = connections_leg(ctx2, D, reps, args)
+        result["categorize"]["hll_auto_k"] = hll_leg(ctx2, D, len(bases), bases, offsets, args)
         ctx2.close()
         if not args.no_cpu and D.rank == 0:
             result["categorize"]["cpu_baseline"] = cpu_lookup_baseline(bases, offsets, sdk, args.cpu_threads)

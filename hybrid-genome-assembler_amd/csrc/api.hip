@@ -291,6 +291,13 @@ hga_status hga_lookup_fetch(hga_ctx* c, const hga_lookup_result* out) {
     });
 }
 
+hga_status hga_hll_registers(hga_ctx* c, int k, uint32_t b, uint8_t* registers) {
+    HGA_CTX_GUARD(c, {
+        HGA_REQUIRE(registers, HGA_ERR_INVALID, "null registers");
+        hga::hll_registers(c, k, (int)b, registers);
+    });
+}
+
 hga_status hga_profile_enable(hga_ctx* c, int on) {
     HGA_CTX_GUARD(c, {
         c->prof.drain();

@@ -150,7 +150,7 @@ struct LookupState {
     // results
     DevBuf tile_cnt, hit_read, hit_kid, hit_pos, hit_ptr, s_key, s_val, s_key2, s_val2,
         first_flag, first_kid, first_pos, first_read, first_ptr, kci_key, kci_val, kci_ptr, scratch,
-        scratch2, scratch3, big_list;
+        scratch2, scratch3, big_list, hll_part;
     std::vector<uint64_t> h_offsets;
     uint64_t windows = 0, hits = 0, firsts = 0, reads_hit = 0;
 };
@@ -222,6 +222,7 @@ void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, ui
 void lookup_run(hga_ctx* c);
 void lookup_sizes(hga_ctx* c, hga_lookup_sizes* out);
 void lookup_fetch(hga_ctx* c, const hga_lookup_result* out);
+void hll_registers(hga_ctx* c, int k, int b, uint8_t* regs);
 
 // radix sort (sort.hip): stable LSD sort of `n` keys by their low `bits` bits, with an
 // optional u32 payload.  Result ends in keys/vals (scratch used as ping-pong).

@@ -81,6 +81,7 @@ HGA_SYMBOLS = {
     "hga_lookup_fetch": (C.c_int, [_vp, C.POINTER(LookupResult)]),
     "hga_connections_run": (C.c_int, [_vp, _u32p, C.c_uint64, C.c_uint32, C.c_uint64, _i32p, _u64p]),
     "hga_connections_fetch": (C.c_int, [_vp, _u32p, _u32p, _u64p, _u8p]),
+    "hga_hll_registers": (C.c_int, [_vp, C.c_int, C.c_uint32, _u8p]),
     "hga_profile_enable": (C.c_int, [_vp, C.c_int]),
     "hga_profile_select": (C.c_int, [_vp, C.c_char_p]),
     "hga_profile_reset": (C.c_int, [_vp]),
@@ -107,6 +108,7 @@ HOST_SYMBOLS = {
                                    C.POINTER(_u64p), C.POINTER(_vp)]),
     "hgh_jf_stream": (C.c_int, [C.c_char_p, C.POINTER(_vp), _u64p, _u64p]),
     "hgh_fmt_double": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
+    "hgh_hll_estimate": (C.c_double, [_u8p, C.c_int]),
 }
 
 
@@ -349,6 +351,32 @@ class Ctx:
                                         _p(g, C.c_uint8)))
         return x, y, sc, g
 
+    # ---- HyperLogLog auto-k (KmerAnalysis.cpp:15-56) on the reads of lookup_set_reads
+    def hll_registers(self, k: int, b: int = 10):
+        """hll::HyperLogLog(b) registers over every KmerIterator window (HyperLogLog.hpp:96-106)."""
+        regs = np.zeros(1 << b, np.uint8)
+        _ck(lib().hga_hll_registers(self._h, k, b, _p(regs, C.c_uint8)))
+        return regs
+
+    def approximate_kmer_count(self, k: int) -> int:
+        """get_approximate_kmer_count (KmerAnalysis.cpp:26-38): the estimate truncated to uint64."""
+        return int(hll_estimate(self.hll_registers(k, 10), 10))
+
+    def unique_k_length(self):
+        """get_unique_k_length (KmerAnalysis.cpp:41-56): ((k, count), the printed lines)."""
+        lines = []
+        k = 11
+        prev = self.approximate_kmer_count(k)
+        lines.append(f"k=11 : ~{prev} kmers")
+        while k < 33:
+            cnt = self.approximate_kmer_count(k + 2)
+            lines.append(f"k={k + 2} : ~{cnt} kmers")
+            if cnt + prev and abs(cnt - prev) / ((cnt + prev) / 2.0) < 0.1:
+                return (k, prev), lines
+            k += 2
+            prev = cnt
+        return (k, prev), lines
+
     # ---- measurement
     def profile(self, on: bool = True):
         _ck(lib().hga_profile_enable(self._h, 1 if on else 0))
@@ -456,6 +484,12 @@ def jf_stream(path: str) -> bytes:
     _hck(host().hgh_jf_stream(path.encode(), C.byref(p), C.byref(n), C.byref(r)))
     return bytes(_take(p.value, n.value, np.uint8, host().hgh_free)) if n.value else (
         host().hgh_free(p.value) or b"")
+
+
+def hll_estimate(regs, b: int = 10) -> float:
+    """hll::HyperLogLog::estimate (src/lib/HyperLogLog.hpp:113-132), host C++ (host/hll.cpp)."""
+    r = np.ascontiguousarray(regs, np.uint8)
+    return float(host().hgh_hll_estimate(_p(r, C.c_uint8), b))
 
 
 def fmt_double(v: float) -> str:

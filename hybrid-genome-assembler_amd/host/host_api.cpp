@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "gen.h"
+#include "kmer_analysis.h"
 #include "seqio.h"
 
 namespace {
@@ -151,5 +152,8 @@ int hgh_fmt_double(double v, char* buf, int cap) {
     std::memcpy(buf, s.c_str(), s.size() + 1);
     return (int)s.size();
 }
+
+// hll::HyperLogLog::estimate of 2^b registers (kmer_analysis.h).
+double hgh_hll_estimate(const uint8_t* regs, int b) { return hgah::hll_estimate(regs, b); }
 
 }  // extern "C"

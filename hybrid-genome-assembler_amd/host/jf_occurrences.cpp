@@ -17,6 +17,9 @@
 // other file the GPU count is written back as that dump, "KMER COUNT" lines in LC_ALL=C order,
 // as run_jellyfish.sh:5-6 would leave it.  HGA_DUMP_CACHE=0 skips writing.
 //
+// Without -k, k is chosen as the reference does (:40-44, KmerAnalysis.cpp:41-56): HyperLogLog
+// estimates for k = 11, 13, ... filled on the GPU (hga_hll_registers), printed per k.
+//
 // HGA_DEVICE selects the GPU (default 0); HGA_PLOT_CMD overrides the plot command.
 #include <chrono>
 #include <cstdio>
@@ -32,6 +35,7 @@
 
 #include "args.h"
 #include "hga.h"
+#include "kmer_analysis.h"
 #include "seqio.h"
 
 namespace {
@@ -103,13 +107,15 @@ int main(int argc, char* argv[]) {
         return 0;
     }
     if (read_paths.empty()) throw std::invalid_argument("You need to specify paths to read files");
-    if (!ap.has("k-size"))
-        throw std::invalid_argument(
-            "automatic k selection (HyperLogLog, src/occurrences/KmerAnalysis.cpp) is not part of this build; pass -k");
 
     const char* dev_env = std::getenv("HGA_DEVICE");
     hga_ctx* ctx = nullptr;
     check(hga_ctx_create(&ctx, dev_env ? std::atoi(dev_env) : 0), "hga_ctx_create");
+    if (!ap.has("k-size")) {   // :40-44 — SequenceRecordIterator(read_paths, true) + get_unique_k_length
+        const hgah::RecordSet rs = hgah::load_records(read_paths, true, false);
+        check(hga_lookup_set_reads(ctx, rs.bases.data(), rs.offsets.data(), rs.size(), 1), "hga_lookup_set_reads");
+        k = hgah::unique_k_length(ctx, std::cout).first;
+    }
     check(hga_count_begin(ctx, k, (uint32_t)read_paths.size()), "hga_count_begin");
     std::vector<uint32_t> counted;
     for (uint32_t f = 0; f < read_paths.size(); ++f) {

@@ -209,6 +209,20 @@ typedef struct hga_lookup_result {
 hga_status hga_lookup_fetch(hga_ctx* ctx, const hga_lookup_result* out);
 
 /* ------------------------------------------------------------------------------
+ * HyperLogLog k-mer cardinality — replaces get_approximate_kmer_count
+ * (src/occurrences/KmerAnalysis.cpp:15-38), the estimator behind jf_occurrences' automatic
+ * k selection (get_unique_k_length, KmerAnalysis.cpp:41-56; src/jellyfish_occurrences.cpp:40-44).
+ * ------------------------------------------------------------------------------ */
+
+/* Registers of hll::HyperLogLog(b) (src/lib/HyperLogLog.hpp:96-106) after add() of the
+ * canonical code (8 little-endian bytes, MurmurHash3_x86_32 seed 313) of every KmerIterator
+ * window of the reads uploaded with hga_lookup_set_reads.  registers[2^b] (caller-allocated)
+ * receive M[index] = max rank; order-independent, so bit-identical to the reference.
+ * b in [4, 14] (the reference uses 10); k in [1, 32] ("Kmer size is too big" above 32,
+ * KmerIterator.cpp:24-26).  The estimate itself is host arithmetic on these registers. */
+hga_status hga_hll_registers(hga_ctx* ctx, int k, uint32_t b, uint8_t* registers);
+
+/* ------------------------------------------------------------------------------
  * Connections — ReadClusteringEngine::get_connections / get_all_connections
  * (src/clustering/ReadClusteringEngine.cpp:301-339) on the one-read components that
  * construct_indices leaves (run after hga_lookup_run, on its device-resident indices).

@@ -18,6 +18,7 @@
 // std::sort).  The multi-threaded *_mt variants exist for bench.py's cpu_baseline
 // and are checked against the plain ones in tests/test_oracle.py.
 
+#include <cmath>
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -506,6 +507,81 @@ uint64_t or_lookup_hits_mt(const char* bases, const uint64_t* offsets, uint64_t 
         });
     for (auto& x : th) x.join();
     return hits.load();
+}
+
+// --- HLL auto-k (src/occurrences/KmerAnalysis.cpp:15-56, src/lib/HyperLogLog.hpp) ------
+// MurmurHash3_x86_32 (src/lib/MurmurHash3.cpp:94-140), any length, byte-wise tail.
+uint32_t or_murmur3_x86_32(const void* key, int len, uint32_t seed) {
+    const uint8_t* data = (const uint8_t*)key;
+    const int nblocks = len / 4;
+    uint32_t h1 = seed;
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+    for (int i = 0; i < nblocks; ++i) {
+        uint32_t k1;
+        std::memcpy(&k1, data + 4 * i, 4);
+        k1 *= c1; k1 = rotl(k1, 15); k1 *= c2;
+        h1 ^= k1; h1 = rotl(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+    }
+    const uint8_t* tail = data + nblocks * 4;
+    uint32_t k1 = 0;
+    switch (len & 3) {
+        case 3: k1 ^= (uint32_t)tail[2] << 16; [[fallthrough]];
+        case 2: k1 ^= (uint32_t)tail[1] << 8; [[fallthrough]];
+        case 1: k1 ^= tail[0]; k1 *= c1; k1 = rotl(k1, 15); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint32_t)len;
+    h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+    return h1;
+}
+
+// HyperLogLog(b)::add of every KmerIterator window's canonical code (8 bytes, seed 313) of
+// every read (KmerAnalysis.cpp:15-23; HyperLogLog.hpp:96-106).  clz(0) is taken as 32.
+// Returns 0, or -1 when k is outside [1, 32] (KmerIterator.cpp:24-26) and reads exist.
+int or_hll_registers(const char* bases, const uint64_t* offsets, uint64_t n, int k, int b, uint8_t* regs) {
+    const uint32_t m = 1u << b;
+    std::memset(regs, 0, m);
+    std::vector<uint64_t> wk;
+    for (uint64_t r = 0; r < n; ++r) {
+        const uint64_t len = offsets[r + 1] - offsets[r];
+        wk.resize(len + 1);
+        const int64_t w = or_kmer_windows(bases + offsets[r], len, k, wk.data(), nullptr);
+        if (w < 0) return -1;
+        for (int64_t i = 0; i < w; ++i) {
+            const uint64_t kmer = wk[i];   // little-endian bytes of the u64 (x86)
+            const uint32_t h = or_murmur3_x86_32(&kmer, 8, 313);
+            const uint32_t idx = h >> (32 - b);
+            const uint32_t x = h << b;
+            const int clz = x ? __builtin_clz(x) : 32;
+            const uint8_t rank = (uint8_t)(std::min(32 - b, clz) + 1);
+            if (rank > regs[idx]) regs[idx] = rank;
+        }
+    }
+    return 0;
+}
+
+// hll::HyperLogLog::estimate (HyperLogLog.hpp:66-87 alpha, :113-132).
+double or_hll_estimate(const uint8_t* regs, int b) {
+    const uint32_t m = 1u << b;
+    double alpha;
+    switch (m) {
+        case 16: alpha = 0.673; break;
+        case 32: alpha = 0.697; break;
+        case 64: alpha = 0.709; break;
+        default: alpha = 0.7213 / (1.0 + 1.079 / m); break;
+    }
+    const double alphaMM = alpha * m * m;
+    double sum = 0.0;
+    for (uint32_t i = 0; i < m; i++) sum += 1.0 / (1 << regs[i]);
+    double estimate = alphaMM / sum;
+    if (estimate <= 2.5 * m) {
+        uint32_t zeros = 0;
+        for (uint32_t i = 0; i < m; i++) zeros += regs[i] == 0;
+        if (zeros != 0) estimate = m * std::log(static_cast<double>(m) / zeros);
+    } else if (estimate > (1.0 / 30.0) * 4294967296.0) {
+        estimate = -4294967296.0 * std::log(1.0 - (estimate / 4294967296.0));
+    }
+    return estimate;
 }
 
 }  // extern "C"

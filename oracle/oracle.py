@@ -65,6 +65,12 @@ def lib():
                                      C.POINTER(_u8p)]
         L.or_lookup_hits_mt.restype = C.c_uint64
         L.or_lookup_hits_mt.argtypes = [C.c_char_p, _u64p, C.c_uint64, C.c_int, _u64p, C.c_uint32, C.c_int]
+        L.or_murmur3_x86_32.restype = C.c_uint32
+        L.or_murmur3_x86_32.argtypes = [C.c_char_p, C.c_int, C.c_uint32]
+        L.or_hll_registers.restype = C.c_int
+        L.or_hll_registers.argtypes = [C.c_char_p, _u64p, C.c_uint64, C.c_int, C.c_int, _u8p]
+        L.or_hll_estimate.restype = C.c_double
+        L.or_hll_estimate.argtypes = [_u8p, C.c_int]
         _lib = L
     return _lib
 
@@ -215,3 +221,42 @@ def count_pipeline(streams, k, lower, upper, thresholds=THRESHOLDS, min_count=2)
     hist = specificity(counts, thresholds) if len(keys) else np.zeros((0, 3), np.int64)
     sel, disc = select(keys, counts, lower, upper)
     return {"dumps": dumps, "keys": keys, "counts": counts, "hist": hist, "selected": sel, "n_discr": disc}
+
+
+def murmur3_x86_32(data: bytes, seed: int) -> int:
+    """MurmurHash3_x86_32 (src/lib/MurmurHash3.cpp:94-140)."""
+    return int(lib().or_murmur3_x86_32(data, len(data), seed))
+
+
+def hll_registers(bases: bytes, offsets, k: int, b: int = 10):
+    """HyperLogLog(b) registers over every KmerIterator window (KmerAnalysis.cpp:15-23)."""
+    offs = np.ascontiguousarray(offsets, np.uint64)
+    regs = np.zeros(1 << b, np.uint8)
+    if lib().or_hll_registers(bases, _p(offs, C.c_uint64), len(offs) - 1, k, b, _p(regs, C.c_uint8)) < 0:
+        raise ValueError("Kmer size is too big")
+    return regs
+
+
+def hll_estimate(regs, b: int = 10) -> float:
+    """hll::HyperLogLog::estimate (src/lib/HyperLogLog.hpp:113-132)."""
+    r = np.ascontiguousarray(regs, np.uint8)
+    return float(lib().or_hll_estimate(_p(r, C.c_uint8), b))
+
+
+def unique_k_length(bases: bytes, offsets, registers=None):
+    """get_unique_k_length (KmerAnalysis.cpp:41-56): ((k, count), printed lines).
+    `registers(k)` may supply the registers (e.g. from the GPU); default = the oracle's."""
+    reg = registers or (lambda kk: hll_registers(bases, offsets, kk))
+    count_of = lambda kk: int(hll_estimate(reg(kk)))   # double -> uint64_t, truncation
+    lines = []
+    k = 11
+    prev = count_of(k)
+    lines.append(f"k=11 : ~{prev} kmers")
+    while k < 33:
+        cnt = count_of(k + 2)
+        lines.append(f"k={k + 2} : ~{cnt} kmers")
+        if cnt + prev and abs(cnt - prev) / ((cnt + prev) / 2.0) < 0.1:
+            return (k, prev), lines
+        k += 2
+        prev = cnt
+    return (k, prev), lines

@@ -86,3 +86,56 @@ def construct_indices(reads, k, sdk_keys_in_id_order, first_id=1):
         per_read.append({"hits": hits, "sorted": sorted(kid for kid, _ in hits),
                          "first": sorted(first.items())})
     return per_read, [sorted(x) for x in kci]
+
+
+# --- HyperLogLog auto-k: src/lib/MurmurHash3.cpp:94-140, src/lib/HyperLogLog.hpp:96-132,
+#     src/occurrences/KmerAnalysis.cpp:15-56
+def murmur3_x86_32(data: bytes, seed: int) -> int:
+    M = 0xFFFFFFFF
+    rotl = lambda x, r: ((x << r) | (x >> (32 - r))) & M
+    h = seed & M
+    n = len(data) // 4
+    for i in range(n):
+        k1 = int.from_bytes(data[4 * i:4 * i + 4], "little")
+        k1 = rotl((k1 * 0xcc9e2d51) & M, 15) * 0x1b873593 & M
+        h = (rotl(h ^ k1, 13) * 5 + 0xe6546b64) & M
+    tail = data[4 * n:]
+    k1 = 0
+    for j in reversed(range(len(tail))):
+        k1 ^= tail[j] << (8 * j)
+    if tail:
+        k1 = rotl((k1 * 0xcc9e2d51) & M, 15) * 0x1b873593 & M
+        h ^= k1
+    h ^= len(data)
+    h ^= h >> 16
+    h = (h * 0x85ebca6b) & M
+    h ^= h >> 13
+    h = (h * 0xc2b2ae35) & M
+    return h ^ (h >> 16)
+
+
+def hll_registers(reads, k: int, b: int = 10):
+    regs = [0] * (1 << b)
+    for seq in reads:
+        for code, _ in kmer_iterator(seq, k):
+            h = murmur3_x86_32(code.to_bytes(8, "little"), 313)
+            x = (h << b) & 0xFFFFFFFF
+            clz = 32 - x.bit_length()          # clz(0) = 32
+            rank = min(32 - b, clz) + 1
+            idx = h >> (32 - b)
+            regs[idx] = max(regs[idx], rank)
+    return regs
+
+
+def hll_estimate(regs, b: int = 10) -> float:
+    import math
+    m = 1 << b
+    alpha = {16: 0.673, 32: 0.697, 64: 0.709}.get(m, 0.7213 / (1.0 + 1.079 / m))
+    e = alpha * m * m / sum(1.0 / (1 << r) for r in regs)
+    if e <= 2.5 * m:
+        z = regs.count(0)
+        if z:
+            e = m * math.log(m / z)
+    elif e > (1.0 / 30.0) * 4294967296.0:
+        e = -4294967296.0 * math.log(1.0 - e / 4294967296.0)
+    return e
