@@ -192,7 +192,7 @@ def connections_leg(ctx2, D, reps, args):
     for _ in range(reps):
         ctx2.connections_run(min_score=1)
     kern = {}
-    for name in ("cn_local", "cn_global", "cn_sort", "radix_upsweep", "radix_downsweep", "scan"):
+    for name in ("cn_wave", "cn_local", "cn_global", "cn_sort", "radix_upsweep", "radix_downsweep", "scan"):
         ms, n = ctx2.profile_get(name)
         if n:
             kern[name] = round(ms / reps, 4)
@@ -211,11 +211,11 @@ def connections_leg(ctx2, D, reps, args):
     H = float(len(idx["sorted_kid"]))
     # per pivot hit: KmerID 4 B + kci_ptr pair 16 B; per walked pair: candidate 4 B; per kept pair 12 B
     cn_bytes = 20 * H + 4 * pairs_walked + 12 * n_conn
-    cn_ms = kern.get("cn_local", 0) + kern.get("cn_global", 0)
+    cn_ms = kern.get("cn_wave", 0) + kern.get("cn_local", 0) + kern.get("cn_global", 0)
     out = {"call": "get_all_connections(min_score=1) on the C3 indices", "ms": round(dt * 1e3, 3),
            "connections": int(n_conn), "pairs_walked": int(pairs_walked),
            "pivots_per_s": round(D.sum(float(len(idx["hit_ptr"]) - 1)) / dt, 1), "kernels_ms": kern,
-           "roofline": {"bound": "hbm", "kernel": "cn_local", "model": "20 B per hit + 4 B per walked "
+           "roofline": {"bound": "hbm", "kernel": "cn_wave+cn_local+cn_global", "model": "20 B per hit + 4 B per walked "
                         "(id, candidate) pair + 12 B per kept pair",
                         "achieved": round(cn_bytes / (cn_ms * 1e-3) / 1e9, 1) if cn_ms else None,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s"}}

@@ -30,7 +30,6 @@ namespace hga {
 namespace {
 
 constexpr int CN_T = 256;
-constexpr uint32_t CN_CAP = 4096;          // LDS table entries (32 KB)
 constexpr uint32_t CN_EMPTY = 0xFFFFFFFFu;
 
 inline unsigned cn_blocks(uint64_t n, uint64_t t) { return (unsigned)((n + t - 1) / t); }
@@ -73,11 +72,32 @@ struct CnIn {
     uint32_t min_kmers, min_score;
 };
 
+// Output: CN_R regions of rcap entries, each with its own cursor in its own 128-B line, so the
+// per-pivot reservations spread over CN_R addresses instead of serialising on one.  Pivot p
+// writes to region p % CN_R, so the region sizes do not depend on scheduling (an overflowing
+// first attempt gives the exact size for the retry).
+constexpr int CN_R = 64;
+constexpr int CN_RSTRIDE = 16;             // u64 words between region cursors
 struct CnOut {
     uint32_t *x, *y, *s;
-    uint64_t cap;
-    unsigned long long* ctr;   // [0] cursor, [1] max score, [2] overflow pivots
+    uint64_t rcap;                 // entries per region
+    unsigned long long* ctr;       // [1] max score, [2] / [3] tier-2 / tier-3 pivots, [5] work
+    unsigned long long* rcur;      // region cursors, stride CN_RSTRIDE
 };
+
+// Reserves n entries in region r; returns the region-local offset (entries past rcap are
+// counted but not written, and the host retries with the exact size).
+__device__ __forceinline__ uint64_t cn_reserve(const CnOut& out, uint32_t r, uint32_t n) {
+    return atomicAdd(&out.rcur[(uint64_t)r * CN_RSTRIDE], (unsigned long long)n);
+}
+__device__ __forceinline__ void cn_put(const CnOut& out, uint32_t r, uint64_t w, uint32_t x, uint32_t y, uint32_t sc) {
+    if (w < out.rcap) {
+        const uint64_t g = (uint64_t)r * out.rcap + w;
+        out.x[g] = x;
+        out.y[g] = y;
+        out.s[g] = sc;
+    }
+}
 
 // Walks pivot p's hit list into the table.  Returns false (uniformly) on overflow.
 __device__ bool cn_walk(const CnIn& in, uint32_t p, uint64_t b, uint64_t e, uint32_t* tk, uint32_t* tv,
@@ -136,7 +156,8 @@ __device__ void cn_emit(const CnIn& in, const CnOut& out, uint32_t p, const uint
     const uint32_t pre = block_excl_scan<CN_T>(cnt, ws, &total);
     if (total == 0) return;
     __shared__ unsigned long long base_s;
-    if (threadIdx.x == 0) base_s = atomicAdd(&out.ctr[0], (unsigned long long)total);
+    const uint32_t reg = p % CN_R;
+    if (threadIdx.x == 0) base_s = cn_reserve(out, reg, total);
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(&out.ctr[1], (unsigned long long)mx);
     __syncthreads();
     uint64_t w = base_s + pre;
@@ -144,36 +165,336 @@ __device__ void cn_emit(const CnIn& in, const CnOut& out, uint32_t p, const uint
         const uint32_t v = cn_ld(&tv[s]);
         const uint32_t key = cn_ld(&tk[s]);
         if (key != CN_EMPTY && v >= in.min_score) {
-            if (w < out.cap) {
-                out.x[w] = p;
-                out.y[w] = key;
-                out.s[w] = v;
-            }
+            cn_put(out, reg, w, p, key, v);
             ++w;
             --cnt;
         }
     }
 }
 
+// ---- cn_local: the LDS path (every pivot whose distinct candidates fit 3/4 of CN_CAP).
+// Table entries are one u64 (candidate in the low word, count in the high word), so a repeat
+// is one ds_add_u64 and a new candidate one ds_cmpst_b64.  The table is sized per pivot from
+// its (id, candidate) pair count (an upper bound of its distinct candidates), so short pivots
+// clear and scan a small table.  Pairs of a chunk of 256 KmerIDs are assigned lane-strided
+// (neighbouring lanes read neighbouring kmer_component_index words); the owner KmerID of each
+// pair comes from an LDS owner map (segment starts + a block max-scan) instead of a per-pair
+// binary search, and every lane issues its CN_U candidate loads before its inserts.
+constexpr uint32_t CN_CAP = 2048;          // LDS table entries (16 KB)
+constexpr uint32_t CN_W = 2048;            // pairs per owner-map window
+constexpr int CN_U = CN_W / CN_T;          // pairs per lane per window
+constexpr uint64_t CN_EMPTY64 = 0x00000000FFFFFFFFull;
+
+__device__ __forceinline__ bool cn_insert64(uint64_t* t, uint32_t mask, uint32_t cand, uint32_t* fill, uint32_t limit,
+                                            uint32_t* ovf) {
+    uint32_t s = cn_hash(cand) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+        uint64_t v = __atomic_load_n(&t[s], __ATOMIC_RELAXED);
+        if ((uint32_t)v == CN_EMPTY) {
+            v = atomicCAS((unsigned long long*)&t[s], (unsigned long long)CN_EMPTY64,
+                          (unsigned long long)((1ull << 32) | cand));
+            if (v == CN_EMPTY64) {
+                if (atomicAdd(fill, 1u) + 1 >= limit) __atomic_store_n(ovf, 1u, __ATOMIC_RELAXED);
+                return true;
+            }
+        }
+        if ((uint32_t)v == cand) {
+            atomicAdd((unsigned long long*)&t[s], 1ull << 32);
+            return true;
+        }
+        s = (s + 1) & mask;
+    }
+    __atomic_store_n(ovf, 1u, __ATOMIC_RELAXED);
+    return false;
+}
+
+// Inclusive max-scan of own[0..CN_W) in place (CN_U consecutive entries per thread).
+__device__ __forceinline__ void cn_owner_scan(uint8_t* own, uint32_t* ws) {
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t v[CN_U];
+    uint32_t m = 0;
+#pragma unroll
+    for (int u = 0; u < CN_U; ++u) {
+        m = max(m, (uint32_t)own[t * CN_U + u]);
+        v[u] = m;
+    }
+    uint32_t x = m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x = max(x, y);
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    uint32_t pre = __shfl_up(x, 1, 64);
+    if (lane == 0) pre = 0;
+    for (uint32_t w = 0; w < wave; ++w) pre = max(pre, ws[w]);
+#pragma unroll
+    for (int u = 0; u < CN_U; ++u) own[t * CN_U + u] = (uint8_t)max(pre, v[u]);
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint32_t* __restrict__ piv,
-                                                 uint32_t* __restrict__ ovf_list, uint32_t limit) {
-    __shared__ uint32_t tk[CN_CAP], tv[CN_CAP];
-    __shared__ uint64_t sh64[(8 + 2 * CN_T + CN_T + 2) / 2];
-    uint32_t* sh = reinterpret_cast<uint32_t*>(sh64);
+                                                 uint32_t* __restrict__ ovf_list, unsigned long long* __restrict__ ovf_n,
+                                                 uint32_t limit) {
+    __shared__ uint64_t tab[CN_CAP];
+    __shared__ uint64_t lo[CN_T];
+    __shared__ uint32_t off[CN_T + 1];
+    __shared__ uint8_t own[CN_W];
+    __shared__ uint32_t sh[12];   // [0] fill, [1] ovf, [2..] scan scratch
+    const uint32_t t = threadIdx.x;
     const uint32_t p = piv ? piv[blockIdx.x] : blockIdx.x;
     const uint64_t b = in.hit_ptr[p], e = in.hit_ptr[p + 1];
     if (e - b < (uint64_t)in.min_kmers || e == b) return;
-    for (uint32_t s = threadIdx.x; s < CN_CAP; s += CN_T) {
-        tk[s] = CN_EMPTY;
-        tv[s] = 0;
+    // pair count -> table size (>= 2 x distinct candidates when it fits)
+    uint64_t acc = 0;
+    for (uint64_t i = b + t; i < e; i += CN_T) {
+        const uint32_t kid = in.skid[i];
+        acc += in.kci_ptr[kid + 1] - in.kci_ptr[kid];
     }
-    if (threadIdx.x < 2) sh[threadIdx.x] = 0;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((t & 63) == 0) sh[4 + (t >> 6)] = (uint32_t)min<uint64_t>(acc, 1u << 30);
+    if (t < 2) sh[t] = 0;
     __syncthreads();
-    if (!cn_walk(in, p, b, e, tk, tv, CN_CAP - 1, limit, sh)) {
-        if (threadIdx.x == 0) ovf_list[atomicAdd(&out.ctr[2], 1ull)] = p;
+    const uint64_t pairs = (uint64_t)sh[4] + sh[5] + sh[6] + sh[7];
+    uint32_t size = 256;
+    while (size < CN_CAP && size < 2 * pairs) size <<= 1;
+    const uint32_t mask = size - 1;
+    const uint32_t lim = min(limit, size * 3 / 4 + (size < CN_CAP ? size : 0u));   // small tables cannot fill
+    for (uint32_t s2 = t; s2 < size; s2 += CN_T) tab[s2] = CN_EMPTY64;
+    __syncthreads();
+    bool ok = true;
+    for (uint64_t cb = b; cb < e && ok; cb += CN_T) {
+        const uint64_t i = cb + t;
+        uint32_t len = 0;
+        uint64_t l0 = 0;
+        if (i < e) {
+            const uint32_t kid = in.skid[i];
+            l0 = in.kci_ptr[kid];
+            len = (uint32_t)(in.kci_ptr[kid + 1] - l0);
+        }
+        uint32_t T;
+        const uint32_t o = block_excl_scan<CN_T>(len, sh + 2, &T);
+        lo[t] = l0;
+        off[t] = o;
+        if (t == 0) off[CN_T] = T;
+        for (uint32_t w0 = 0; w0 < T && ok; w0 += CN_W) {
+            // owner map of pairs [w0, w0 + CN_W): segment starts, then a max-scan
+#pragma unroll
+            for (int u = 0; u < CN_U; ++u) own[t * CN_U + u] = 0;
+            __syncthreads();
+            if (len && o >= w0 && o < w0 + CN_W) own[o - w0] = (uint8_t)t;
+            if (w0 && o < w0 && o + len > w0) own[0] = (uint8_t)t;   // segment straddling the window start
+            __syncthreads();
+            cn_owner_scan(own, sh + 2);
+            uint32_t cand[CN_U];
+#pragma unroll
+            for (int u = 0; u < CN_U; ++u) {
+                const uint32_t j = w0 + t + CN_T * u;
+                cand[u] = CN_EMPTY;
+                if (j < T) {
+                    const uint32_t a = own[j - w0];
+                    cand[u] = in.kci[lo[a] + (j - off[a])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < CN_U; ++u)
+                if (cand[u] != CN_EMPTY && cand[u] != p) (void)cn_insert64(tab, mask, cand[u], &sh[0], lim, &sh[1]);
+            __syncthreads();
+            ok = __atomic_load_n(&sh[1], __ATOMIC_RELAXED) == 0;
+        }
+        __syncthreads();
+    }
+    if (!ok) {
+        if (t == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = p;
         return;
     }
-    cn_emit(in, out, p, tk, tv, CN_CAP, sh + 2);
+    // emit: survivors compacted with one global atomic per workgroup
+    const uint32_t per = size / CN_T ? size / CN_T : 1;
+    const uint32_t s0 = t * per;
+    uint32_t cnt = 0, mx = 0;
+    for (uint32_t s2 = s0; s2 < s0 + per && s2 < size; ++s2) {
+        const uint64_t v = tab[s2];
+        const uint32_t c = (uint32_t)(v >> 32);
+        if ((uint32_t)v != CN_EMPTY && c >= in.min_score) {
+            ++cnt;
+            mx = max(mx, c);
+        }
+    }
+#pragma unroll
+    for (int o2 = 32; o2; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o2, 64));
+    uint32_t total;
+    const uint32_t pre = block_excl_scan<CN_T>(cnt, sh + 2, &total);
+    if (total == 0) return;
+    __shared__ unsigned long long base_s;
+    const uint32_t reg = p % CN_R;
+    if (t == 0) base_s = cn_reserve(out, reg, total);
+    if ((t & 63) == 0 && mx) atomicMax(&out.ctr[1], (unsigned long long)mx);
+    __syncthreads();
+    uint64_t w = base_s + pre;
+    for (uint32_t s2 = s0; s2 < s0 + per && s2 < size && cnt; ++s2) {
+        const uint64_t v = tab[s2];
+        const uint32_t c = (uint32_t)(v >> 32);
+        if ((uint32_t)v != CN_EMPTY && c >= in.min_score) {
+            cn_put(out, reg, w, p, (uint32_t)v, c);
+            ++w;
+            --cnt;
+        }
+    }
+}
+
+// ---- cn_wave: the first tier — one wave per pivot, pivots taken from a work counter.
+// Every wave owns a CNW_CAP-entry LDS table (u64 entries as in cn_local) and its own chunk /
+// owner-map state, so a workgroup walks four pivots at once without workgroup barriers (a
+// wave's LDS accesses are ordered) and a CU keeps ~28 pivots' dependent load chains in flight.
+// A pivot whose distinct candidates pass 3/4 of the table goes to the cn_local list.
+constexpr uint32_t CNW_CAP = 512;
+constexpr uint32_t CNW_W = 512;            // pairs per owner-map window
+constexpr int CNW_U = CNW_W / 64;
+constexpr int CNW_WAVES = 4;
+constexpr uint32_t CNW_GRAB = 8;         // pivots per work-counter atomic
+
+struct CnWaveLds {
+    uint64_t tab[CNW_CAP];
+    uint64_t lo[64];
+    uint32_t off[64];
+    uint8_t own[CNW_W];
+    uint32_t fill, ovf;
+};
+
+__global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, const uint32_t* __restrict__ piv,
+                                                          uint64_t n_piv, uint32_t* __restrict__ ovf_list,
+                                                          uint32_t limit) {
+    __shared__ CnWaveLds S[CNW_WAVES];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    CnWaveLds& W = S[wave];
+    for (uint32_t s2 = lane; s2 < CNW_CAP; s2 += 64) W.tab[s2] = CN_EMPTY64;
+    // pivots are taken CNW_GRAB at a time (device-wide same-address atomics serialise) and the
+    // largest score is kept per wave until the end
+    unsigned long long* work = out.ctr + 5;
+    uint32_t wmax = 0;
+    unsigned long long q = 0, q_end = 0;
+    while (true) {
+        if (q == q_end) {
+            if (lane == 0) q = atomicAdd(work, (unsigned long long)CNW_GRAB);
+            q = __shfl(q, 0, 64);
+            q_end = q + CNW_GRAB;
+        }
+        if (q >= n_piv) break;
+        const uint32_t p = piv ? piv[q] : (uint32_t)q;
+        ++q;
+        const uint64_t b = in.hit_ptr[p], e = in.hit_ptr[p + 1];
+        if (e - b < (uint64_t)in.min_kmers || e == b) continue;
+        if (lane == 0) {
+            W.fill = 0;
+            W.ovf = 0;
+        }
+        wave_lds_sync();
+        bool ok = true;
+        for (uint64_t cb = b; cb < e && ok; cb += 64) {
+            const uint64_t i = cb + lane;
+            uint32_t len = 0;
+            uint64_t l0 = 0;
+            if (i < e) {
+                const uint32_t kid = in.skid[i];
+                l0 = in.kci_ptr[kid];
+                len = (uint32_t)(in.kci_ptr[kid + 1] - l0);
+            }
+            const uint32_t inc = wave_incl_scan(len, (int)lane);
+            const uint32_t o = inc - len;
+            const uint32_t T = __shfl(inc, 63, 64);
+            W.lo[lane] = l0;
+            W.off[lane] = o;
+            for (uint32_t w0 = 0; w0 < T && ok; w0 += CNW_W) {
+                // owner map of pairs [w0, w0 + CNW_W): segment starts, then a wave max-scan
+#pragma unroll
+                for (int u = 0; u < CNW_U; ++u) W.own[lane * CNW_U + u] = 0;
+                wave_lds_sync();
+                if (len && o >= w0 && o < w0 + CNW_W) W.own[o - w0] = (uint8_t)lane;
+                if (w0 && o < w0 && o + len > w0) W.own[0] = (uint8_t)lane;
+                wave_lds_sync();
+                uint32_t v[CNW_U];
+                uint32_t m = 0;
+#pragma unroll
+                for (int u = 0; u < CNW_U; ++u) {
+                    m = max(m, (uint32_t)W.own[lane * CNW_U + u]);
+                    v[u] = m;
+                }
+                uint32_t x = m;
+#pragma unroll
+                for (int o2 = 1; o2 < 64; o2 <<= 1) {
+                    const uint32_t y = __shfl_up(x, o2, 64);
+                    if (lane >= (uint32_t)o2) x = max(x, y);
+                }
+                uint32_t pre = __shfl_up(x, 1, 64);
+                if (lane == 0) pre = 0;
+                wave_lds_sync();
+#pragma unroll
+                for (int u = 0; u < CNW_U; ++u) W.own[lane * CNW_U + u] = (uint8_t)max(pre, v[u]);
+                wave_lds_sync();
+                uint32_t cand[CNW_U];
+#pragma unroll
+                for (int u = 0; u < CNW_U; ++u) {
+                    const uint32_t j = w0 + lane + 64 * u;
+                    cand[u] = CN_EMPTY;
+                    if (j < T) {
+                        const uint32_t a = W.own[j - w0];
+                        cand[u] = in.kci[W.lo[a] + (j - W.off[a])];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < CNW_U; ++u)
+                    if (cand[u] != CN_EMPTY && cand[u] != p)
+                        (void)cn_insert64(W.tab, CNW_CAP - 1, cand[u], &W.fill, limit, &W.ovf);
+                wave_lds_sync();
+                ok = __atomic_load_n(&W.ovf, __ATOMIC_RELAXED) == 0;
+            }
+            wave_lds_sync();
+        }
+        if (!ok) {
+            if (lane == 0) ovf_list[atomicAdd(&out.ctr[2], 1ull)] = p;
+            for (uint32_t s2 = lane; s2 < CNW_CAP; s2 += 64) W.tab[s2] = CN_EMPTY64;
+            wave_lds_sync();
+            continue;
+        }
+        // emit (and reset the table for the next pivot)
+        constexpr int PER = CNW_CAP / 64;
+        uint64_t ent[PER];
+        uint32_t cnt = 0, mx = 0;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            ent[u] = W.tab[lane * PER + u];
+            W.tab[lane * PER + u] = CN_EMPTY64;
+            const uint32_t c = (uint32_t)(ent[u] >> 32);
+            if ((uint32_t)ent[u] != CN_EMPTY && c >= in.min_score) {
+                ++cnt;
+                mx = max(mx, c);
+            } else {
+                ent[u] = CN_EMPTY64;
+            }
+        }
+        wave_lds_sync();
+        const uint32_t inc = wave_incl_scan(cnt, (int)lane);
+        const uint32_t tot = __shfl(inc, 63, 64);
+        if (!tot) continue;
+#pragma unroll
+        for (int o2 = 32; o2; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o2, 64));
+        wmax = max(wmax, mx);
+        unsigned long long base = 0;
+        const uint32_t reg = p % CN_R;
+        if (lane == 0) base = cn_reserve(out, reg, tot);
+        base = __shfl(base, 0, 64);
+        uint64_t w = base + inc - cnt;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            if ((uint32_t)ent[u] != CN_EMPTY) {
+                cn_put(out, reg, w, p, (uint32_t)ent[u], (uint32_t)(ent[u] >> 32));
+                ++w;
+            }
+        }
+    }
+    if (lane == 0 && wmax) atomicMax(&out.ctr[1], (unsigned long long)wmax);
 }
 
 // Upper bound of a pivot's distinct candidates: its (id, candidate) pair count.
@@ -214,12 +535,25 @@ __global__ void __launch_bounds__(CN_T) cn_global(CnIn in, CnOut out, const uint
     cn_emit(in, out, p, tk, tv, size, sh + 2);
 }
 
+// Dense index i -> output slot: region r with rpre[r] <= i < rpre[r + 1] (rpre: CN_R + 1 prefix
+// counts of the regions), slot r * rcap + (i - rpre[r]).
+__device__ __forceinline__ uint64_t cn_slot(const uint64_t* __restrict__ rpre, uint64_t rcap, uint64_t i) {
+    uint32_t a = 0, z = CN_R;
+    while (z - a > 1) {
+        const uint32_t m = (a + z) >> 1;
+        if (rpre[m] <= i) a = m; else z = m;
+    }
+    return (uint64_t)a * rcap + (i - rpre[a]);
+}
+
 // key = (max - score) << 2*ib | pivot << ib | candidate  (ascending = score desc, then ids)
 __global__ void cn_keys(const uint32_t* __restrict__ x, const uint32_t* __restrict__ y, const uint32_t* __restrict__ s,
-                        uint64_t n, uint32_t mxs, int ib, uint64_t* __restrict__ key) {
+                        const uint64_t* __restrict__ rpre, uint64_t rcap, uint64_t n, uint32_t mxs, int ib,
+                        uint64_t* __restrict__ key) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    key[i] = ((uint64_t)(mxs - s[i]) << (2 * ib)) | ((uint64_t)x[i] << ib) | y[i];
+    const uint64_t g = cn_slot(rpre, rcap, i);
+    key[i] = ((uint64_t)(mxs - s[g]) << (2 * ib)) | ((uint64_t)x[g] << ib) | y[g];
 }
 
 __global__ void cn_decode(const uint64_t* __restrict__ key, uint64_t n, uint32_t mxs, int ib,
@@ -238,12 +572,14 @@ __global__ void cn_decode(const uint64_t* __restrict__ key, uint64_t n, uint32_t
 
 // Two-stage order when the composite key does not fit 64 bits: sort (pivot, candidate) first,
 // then stably by (max - score).
-__global__ void cn_pair_keys(const uint32_t* __restrict__ x, const uint32_t* __restrict__ y, uint64_t n, int ib,
+__global__ void cn_pair_keys(const uint32_t* __restrict__ x, const uint32_t* __restrict__ y,
+                             const uint64_t* __restrict__ rpre, uint64_t rcap, uint64_t n, int ib,
                              uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    key[i] = ((uint64_t)x[i] << ib) | y[i];
-    idx[i] = (uint32_t)i;
+    const uint64_t g = cn_slot(rpre, rcap, i);
+    key[i] = ((uint64_t)x[g] << ib) | y[g];
+    idx[i] = (uint32_t)g;   // slots < 2^32 (checked on the host)
 }
 
 __global__ void cn_score_keys(const uint32_t* __restrict__ s, const uint32_t* __restrict__ idx, uint64_t n,
@@ -320,28 +656,46 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     }
     CnIn in{L.hit_ptr.as<uint64_t>(), L.s_val2.as<uint32_t>(), L.kci_ptr.as<uint64_t>(), L.kci_val.as<uint32_t>(),
             min_kmers, ms};
-    auto* ctr = static_cast<unsigned long long*>(S.ctr.ensure(64));
+    const size_t ctr_bytes = 64 + (size_t)CN_R * CN_RSTRIDE * 8;
+    auto* ctr = static_cast<unsigned long long*>(S.ctr.ensure(ctr_bytes));
+    unsigned long long* rcur = ctr + 8;
     uint32_t* ovf = static_cast<uint32_t*>(S.ovf.ensure(P * 4));
-    uint64_t cap = std::max<uint64_t>(S.cap_hint, 2 * L.hits + (1u << 20));
-    // test hooks: every pivot through the HBM-table path / the two-stage sort
+    uint32_t* ovf2 = static_cast<uint32_t*>(S.ovf2.ensure(P * 4));
+    uint64_t rcap = (std::max<uint64_t>(S.cap_hint, 2 * L.hits + (1u << 20)) + CN_R - 1) / CN_R;
+    // test hooks: every pivot through the workgroup tier / the HBM-table tier / the two-stage sort
     const bool force_global = std::getenv("HGA_CN_FORCE_GLOBAL") != nullptr;
+    const bool force_block = force_global || std::getenv("HGA_CN_FORCE_BLOCK") != nullptr;
     const bool force_two = std::getenv("HGA_CN_TWO_STAGE") != nullptr;
-    unsigned long long h[3];
+    if (const char* rc = std::getenv("HGA_CN_RCAP")) rcap = std::max<uint64_t>(1, std::strtoull(rc, nullptr, 10));
+    unsigned long long h[4];
+    std::vector<unsigned long long> hc(ctr_bytes / 8);
+    std::vector<uint64_t> rpre(CN_R + 1, 0);
     for (int attempt = 0; attempt < 2; ++attempt) {
+        const uint64_t cap = rcap * CN_R;
         CnOut out{static_cast<uint32_t*>(S.x.ensure(cap * 4)), static_cast<uint32_t*>(S.y.ensure(cap * 4)),
-                  static_cast<uint32_t*>(S.s.ensure(cap * 4)), cap, ctr};
-        HGA_HIP(hipMemsetAsync(ctr, 0, 64, c->stream));
-        c->launch("cn_local", [&] {
-            hipLaunchKernelGGL(cn_local, dim3((unsigned)P), dim3(CN_T), 0, c->stream, in, out, d_piv, ovf,
-                               force_global ? 1u : CN_CAP * 3 / 4);
+                  static_cast<uint32_t*>(S.s.ensure(cap * 4)), rcap, ctr, rcur};
+        HGA_HIP(hipMemsetAsync(ctr, 0, ctr_bytes, c->stream));
+        const uint64_t wblk = std::min<uint64_t>((P + CNW_WAVES - 1) / CNW_WAVES, (uint64_t)c->num_cu * 7);
+        c->launch("cn_wave", [&] {
+            hipLaunchKernelGGL(cn_wave, dim3((unsigned)wblk), dim3(64 * CNW_WAVES), 0, c->stream, in, out, d_piv, P,
+                               ovf, force_block ? 1u : CNW_CAP * 3 / 4);
         });
-        c->check_launch("cn_local");
-        HGA_HIP(hipMemcpyAsync(h, ctr, 24, hipMemcpyDeviceToHost, c->stream));
+        c->check_launch("cn_wave");
+        HGA_HIP(hipMemcpyAsync(h, ctr, 32, hipMemcpyDeviceToHost, c->stream));
         c->sync();
-        if (h[2]) {   // overflow pivots: HBM tables of 2 x (largest pair count), in batches of <= 1 GiB
+        if (h[2]) {   // pivots with more distinct candidates than a wave table: one workgroup each
+            c->launch("cn_local", [&] {
+                hipLaunchKernelGGL(cn_local, dim3((unsigned)h[2]), dim3(CN_T), 0, c->stream, in, out, ovf, ovf2,
+                                   ctr + 3, force_global ? 1u : CN_CAP * 3 / 4);
+            });
+            c->check_launch("cn_local");
+            HGA_HIP(hipMemcpyAsync(h, ctr, 32, hipMemcpyDeviceToHost, c->stream));
+            c->sync();
+        }
+        if (h[3]) {   // overflow pivots: HBM tables of 2 x (largest pair count), in batches of <= 1 GiB
             auto* mx = ctr + 4;
             c->launch("cn_global", [&] {
-                hipLaunchKernelGGL(cn_contrib, dim3((unsigned)h[2]), dim3(CN_T), 0, c->stream, in, ovf, mx);
+                hipLaunchKernelGGL(cn_contrib, dim3((unsigned)h[3]), dim3(CN_T), 0, c->stream, in, ovf2, mx);
             });
             c->check_launch("cn_contrib");
             unsigned long long mc = 0;
@@ -352,28 +706,38 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
             while (size < 2 * distinct) size <<= 1;
             HGA_REQUIRE(size <= (1ull << 31), HGA_ERR_OOM, "connection table too large");
             const uint64_t batch = std::max<uint64_t>(1, (1ull << 27) / size);
-            for (uint64_t b0 = 0; b0 < h[2]; b0 += batch) {
-                const uint64_t nb = std::min<uint64_t>(batch, h[2] - b0);
+            for (uint64_t b0 = 0; b0 < h[3]; b0 += batch) {
+                const uint64_t nb = std::min<uint64_t>(batch, h[3] - b0);
                 uint32_t* gk = static_cast<uint32_t*>(S.gk.ensure(nb * size * 4));
                 uint32_t* gv = static_cast<uint32_t*>(S.gv.ensure(nb * size * 4));
                 HGA_HIP(hipMemsetAsync(gk, 0xFF, nb * size * 4, c->stream));
                 HGA_HIP(hipMemsetAsync(gv, 0, nb * size * 4, c->stream));
                 c->launch("cn_global", [&] {
-                    hipLaunchKernelGGL(cn_global, dim3((unsigned)nb), dim3(CN_T), 0, c->stream, in, out, ovf + b0, gk,
-                                       gv, (uint32_t)size);
+                    hipLaunchKernelGGL(cn_global, dim3((unsigned)nb), dim3(CN_T), 0, c->stream, in, out, ovf2 + b0,
+                                       gk, gv, (uint32_t)size);
                 });
                 c->check_launch("cn_global");
             }
-            HGA_HIP(hipMemcpyAsync(h, ctr, 24, hipMemcpyDeviceToHost, c->stream));
+            HGA_HIP(hipMemcpyAsync(h, ctr, 32, hipMemcpyDeviceToHost, c->stream));
             c->sync();
         }
-        if (h[0] <= cap) break;
-        cap = h[0];   // exact now: run again with room for every pair
+        HGA_HIP(hipMemcpyAsync(hc.data(), ctr, ctr_bytes, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        uint64_t mx_region = 0;
+        for (int r = 0; r < CN_R; ++r) {
+            const uint64_t cnt = hc[8 + (size_t)r * CN_RSTRIDE];
+            rpre[r + 1] = rpre[r] + cnt;
+            mx_region = std::max<uint64_t>(mx_region, cnt);
+        }
+        if (mx_region <= rcap) break;
+        HGA_REQUIRE(attempt == 0, HGA_ERR_OOM, "connection output grew between attempts");
+        rcap = mx_region;   // exact now: run again with room for every pair
     }
-    const uint64_t n = h[0];
-    HGA_REQUIRE(n <= cap, HGA_ERR_OOM, "connection output grew between attempts");
+    const uint64_t n = rpre[CN_R];
     HGA_REQUIRE(n < (1ull << 32), HGA_ERR_OOM, "too many connections for one sort");
-    S.cap_hint = cap;
+    S.cap_hint = rcap * CN_R;
+    uint64_t* d_rpre = static_cast<uint64_t*>(S.rpre.ensure((CN_R + 1) * 8));
+    HGA_HIP(hipMemcpyAsync(d_rpre, rpre.data(), (CN_R + 1) * 8, hipMemcpyHostToDevice, c->stream));
     const uint32_t mxs = (uint32_t)h[1];
     const int ib = std::max(1, bits_for(nr - 1));
     const int sb = bits_for(mxs - ms);
@@ -386,7 +750,7 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
         if (sb + 2 * ib <= 64 && !force_two) {
             c->launch("cn_sort", [&] {
                 hipLaunchKernelGGL(cn_keys, dim3(cn_blocks(n, 256)), dim3(256), 0, c->stream, S.x.as<uint32_t>(),
-                                   S.y.as<uint32_t>(), S.s.as<uint32_t>(), n, mxs, ib, key);
+                                   S.y.as<uint32_t>(), S.s.as<uint32_t>(), d_rpre, rcap, n, mxs, ib, key);
             });
             c->check_launch("cn_keys");
             radix_sort_u64(c, key, nullptr, n, sb + 2 * ib, L.scratch);
@@ -396,12 +760,13 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
             });
             c->check_launch("cn_decode");
         } else {
+            HGA_REQUIRE(rcap * CN_R < (1ull << 32), HGA_ERR_OOM, "too many connection slots for one sort");
             uint32_t* idx = static_cast<uint32_t*>(S.idx.ensure(n * 4));
             uint32_t* sk = static_cast<uint32_t*>(S.skey.ensure(n * 4));
             uint32_t* pos = static_cast<uint32_t*>(S.pos.ensure(n * 4));
             c->launch("cn_sort", [&] {
                 hipLaunchKernelGGL(cn_pair_keys, dim3(cn_blocks(n, 256)), dim3(256), 0, c->stream, S.x.as<uint32_t>(),
-                                   S.y.as<uint32_t>(), n, ib, key, idx);
+                                   S.y.as<uint32_t>(), d_rpre, rcap, n, ib, key, idx);
             });
             radix_sort_u64(c, key, idx, n, 2 * ib, L.scratch);
             c->launch("cn_sort", [&] {

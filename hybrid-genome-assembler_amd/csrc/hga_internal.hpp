@@ -158,7 +158,7 @@ struct LookupState {
 struct ConnState {
     bool ready = false;
     uint64_t n = 0, cap_hint = 0;
-    DevBuf piv, cat, ctr, ovf, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og;
+    DevBuf piv, cat, ctr, rpre, ovf, ovf2, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og;
 };
 
 }  // namespace hga

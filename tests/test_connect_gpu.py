@@ -56,7 +56,7 @@ def test_connections_filters_and_pivots(gpu_ctx, golden_case):
     assert gpu_ctx.connections(pivots=np.zeros(0, np.uint32))[0].size == 0
 
 
-@pytest.mark.parametrize("env", [None, "HGA_CN_FORCE_GLOBAL", "HGA_CN_TWO_STAGE"])
+@pytest.mark.parametrize("env", [None, "HGA_CN_FORCE_BLOCK", "HGA_CN_FORCE_GLOBAL", "HGA_CN_TWO_STAGE", "HGA_CN_RCAP"])
 def test_connections_random_first_id(gpu_ctx, hga_mod, monkeypatch, env):
     if env:
         monkeypatch.setenv(env, "1")
@@ -106,3 +106,23 @@ def test_connections_no_hits(gpu_ctx):
     bases = b"ACGTACGTAC"
     lookup(gpu_ctx, bases, np.array([0, 10], np.uint64), 4, np.zeros(0, np.uint64))
     assert gpu_ctx.connections()[0].size == 0
+
+
+def test_connections_long_kmer_lists(gpu_ctx):
+    """KmerIDs shared by ~1000 reads: a pivot's pairs span several owner-map windows (segments
+    straddling window starts) while its distinct candidates still fit the LDS table."""
+    rng = np.random.default_rng(17)
+    rnd = lambda n: bytes(rng.choice(list(b"ACGT"), n).tolist())
+    k1, k2, k3 = rnd(17), rnd(17), rnd(17)
+    reads = []
+    for i in range(1100):
+        r = rnd(20) + k1 + rnd(9) + k2 + rnd(9) + k3
+        if i % 7 == 0:
+            r += rnd(5) + k1          # multiplicity 2
+        reads.append(r)
+    bases = b"".join(reads)
+    offsets = np.cumsum([0] + [len(x) for x in reads]).astype(np.uint64)
+    sdk = np.unique(np.concatenate([oracle.kmer_windows(k, 17)[0] for k in (k1, k2, k3)]))
+    idx = lookup(gpu_ctx, bases, offsets, 17, sdk)
+    for ms in (1, 4):
+        same(gpu_ctx.connections(min_score=ms), oracle.connections(idx, min_score=ms))

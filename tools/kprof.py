@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--lookup", action="store_true")
+    ap.add_argument("--connections", action="store_true", help="also get_all_connections (implies --lookup)")
+    ap.add_argument("--hll", action="store_true", help="also hll_registers k=19 (implies --lookup)")
     a = ap.parse_args()
     ga, gb, ra, rb = bench.make_c2(0)
     ctx = hga.Ctx(0)
@@ -29,7 +31,7 @@ def main():
         bench.count_step(ctx)
     st = ctx.count_stats()
     print(f"instances={st.instances} rows={st.distinct_rows} buckets={st.buckets} max_split={st.max_split}")
-    if a.lookup:
+    if a.lookup or a.connections or a.hll:
         bases, offsets = bench.make_c3(ga, gb, 0)
         sdk, _, _ = ctx.select(bench.LOWER, bench.UPPER)
         ctx2 = hga.Ctx(0)
@@ -38,6 +40,10 @@ def main():
         for _ in range(a.reps):
             ctx2.lookup_run()
         print(f"hits={ctx2.lookup_sizes().hits}")
+        for _ in range(a.reps if a.connections else 0):
+            ctx2.connections_run(min_score=1)
+        for _ in range(a.reps if a.hll else 0):
+            ctx2.hll_registers(19)
         ctx2.close()
     ctx.close()
 

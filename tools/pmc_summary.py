@@ -16,7 +16,7 @@ import sys
 
 
 def kname(full):
-    m = re.search(r"\b((?:kc|lk|rs|sc)_[A-Za-z0-9_]+|pack_kernel)(<[^>]*>)?", full)
+    m = re.search(r"\b((?:kc|lk|rs|sc|cn|hll)_[A-Za-z0-9_]+|pack_kernel)(<[^>]*>)?", full)
     return (m.group(1) + (m.group(2) or "")) if m else full.split("(")[0][:40]
 
 
