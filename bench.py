@@ -276,6 +276,38 @@ def hll_leg(ctx2, D, n_bases, bases, offsets, args):
     return out
 
 
+def ingest_leg(ga, gb, threads):
+    """Host ingest of the CLIs: the C2 pair written as ART-like FASTQ, then
+    jf_stream (jf_occurrences' per-file read) and load_records (categorization / auto-k) with the
+    multi-threaded readers, the sequential restatement timed beside them."""
+    import shutil
+    import tempfile
+    d = tempfile.mkdtemp(prefix="hga_ingest_")
+    try:
+        paths = [os.path.join(d, "mg1655.fq"), os.path.join(d, "uti89.fq")]
+        for g, pth, seed, name in ((ga, paths[0], 1000, "A"), (gb, paths[1], 1001, "B")):
+            hga.write_art_fastq(g, name, COVERAGE * len(g) // READ_LEN, READ_LEN, seed, pth)
+        size = sum(os.path.getsize(p) for p in paths)
+        out = {"files": "C2 pair as ART-like FASTQ", "bytes": size}
+        for label, t in (("parallel", threads), ("sequential", 1)):
+            hga.set_host_threads(t)
+            for _ in range(2 if t > 1 else 1):   # warm page cache / first run
+                t0 = time.perf_counter()
+                n = sum(len(hga.jf_stream(p)) for p in paths)
+                dt_jf = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            rec = hga.load_records(paths, True)
+            dt_lr = time.perf_counter() - t0
+            out[label] = {"threads": t, "jf_stream_s": round(dt_jf, 3), "jf_stream_GBps": round(size / dt_jf / 1e9, 3),
+                          "load_records_s": round(dt_lr, 3), "load_records_GBps": round(size / dt_lr / 1e9, 3),
+                          "bases": int(n), "records": int(len(rec["offsets"]) - 1)}
+        hga.set_host_threads(0)
+        out["note"] = "wall time through the ctypes mirror (includes the copy into Python bytes)"
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -283,6 +315,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lookup", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the host FASTQ ingest leg")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("HGA_CPU_THREADS", "16")))
     args = ap.parse_args()
     D = Dist(args.gpus)
@@ -418,6 +451,8 @@ def main():
 
     if not args.no_cpu and D.rank == 0:
         result["cpu_baseline"] = cpu_baseline(ra, rb, args.cpu_threads)
+    if not args.no_ingest and D.rank == 0 and D.world == 1:
+        result["ingest"] = ingest_leg(ga, gb, args.cpu_threads)
     ctx.close()
     D.close()
     if D.rank == 0:

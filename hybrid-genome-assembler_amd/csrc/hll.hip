@@ -16,7 +16,7 @@
 //               LDS (a window only touches LDS when it raises its register, which after the
 //               first few thousand windows almost never happens); every workgroup loops over
 //               tiles and writes its registers once.
-//   hll_reduce  max over the workgroups' register rows.
+//   hll_reduce  max over the workgroups' register rows (row groups in parallel + atomicMax).
 // Algorithmic bytes: 0.375 B per base (packed codes + valid bits) + 0.125 B (read-start bits).
 #include <algorithm>
 
@@ -89,12 +89,19 @@ __global__ void __launch_bounds__(HL_T) hll_scan(const uint32_t* __restrict__ pk
     for (uint32_t i = threadIdx.x; i < m; i += HL_T) part[(uint64_t)blockIdx.x * m + i] = (uint8_t)reg[i];
 }
 
-__global__ void hll_reduce(const uint8_t* __restrict__ part, uint32_t nblk, uint32_t m, uint8_t* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// Max over the workgroups' register rows: block (x, y) takes 256 registers of rows
+// [y * HL_RG, (y + 1) * HL_RG) (independent loads, unrolled), then one atomicMax per register
+// and block (HL_RG = 64: 32 atomics per register at 2048 rows).
+constexpr uint32_t HL_RG = 64;
+__global__ void __launch_bounds__(256) hll_reduce(const uint8_t* __restrict__ part, uint32_t nblk, uint32_t m,
+                                                  uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
+    const uint32_t r0 = blockIdx.y * HL_RG, r1 = min(nblk, r0 + HL_RG);
     uint32_t v = 0;
-    for (uint32_t w = 0; w < nblk; ++w) v = max(v, (uint32_t)part[(uint64_t)w * m + i]);
-    out[i] = (uint8_t)v;
+#pragma unroll 8
+    for (uint32_t w = r0; w < r1; ++w) v = max(v, (uint32_t)part[(uint64_t)w * m + i]);
+    if (v) atomicMax(&out[i], v);
 }
 
 }  // namespace
@@ -114,19 +121,23 @@ void hll_registers(hga_ctx* c, int k, int b, uint8_t* regs) {
     }
     const uint64_t want = (n_threads + HL_T - 1) / HL_T;
     const uint32_t nblk = (uint32_t)std::min<uint64_t>(want, (uint64_t)c->num_cu * 8);
-    uint8_t* part = static_cast<uint8_t*>(L.hll_part.ensure((uint64_t)nblk * m + m));
-    uint8_t* dout = part + (uint64_t)nblk * m;
+    uint8_t* part = static_cast<uint8_t*>(L.hll_part.ensure((uint64_t)nblk * m + 4ull * m));
+    uint32_t* dout = reinterpret_cast<uint32_t*>(part + (uint64_t)nblk * m);
+    HGA_HIP(hipMemsetAsync(dout, 0, 4ull * m, c->stream));
     c->launch("hll_scan", [&] {
         hipLaunchKernelGGL(hll_scan, dim3(nblk), dim3(HL_T), m * 4, c->stream, L.packed.as<uint32_t>(),
                            L.valid.as<uint16_t>(), L.starts.as<unsigned int>(), nb, k, b, n_threads, part);
     });
     c->check_launch("hll_scan");
     c->launch("hll_reduce", [&] {
-        hipLaunchKernelGGL(hll_reduce, dim3((m + 255) / 256), dim3(256), 0, c->stream, part, nblk, m, dout);
+        hipLaunchKernelGGL(hll_reduce, dim3((m + 255) / 256, (nblk + HL_RG - 1) / HL_RG), dim3(256), 0, c->stream,
+                           part, nblk, m, dout);
     });
     c->check_launch("hll_reduce");
-    HGA_HIP(hipMemcpyAsync(regs, dout, m, hipMemcpyDeviceToHost, c->stream));
+    std::vector<uint32_t> r32(m);
+    HGA_HIP(hipMemcpyAsync(r32.data(), dout, 4ull * m, hipMemcpyDeviceToHost, c->stream));
     c->sync();
+    for (uint32_t i = 0; i < m; ++i) regs[i] = (uint8_t)r32[i];
 }
 
 }  // namespace hga

@@ -109,6 +109,7 @@ HOST_SYMBOLS = {
     "hgh_jf_stream": (C.c_int, [C.c_char_p, C.POINTER(_vp), _u64p, _u64p]),
     "hgh_fmt_double": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
     "hgh_hll_estimate": (C.c_double, [_u8p, C.c_int]),
+    "hgh_set_threads": (None, [C.c_int]),
 }
 
 
@@ -450,6 +451,11 @@ def write_art_fastq(genome: bytes, name: str, n_reads: int, read_len: int, seed:
 
 def write_nanosim_fasta(genome: bytes, name: str, n_reads: int, seed: int, path: str):
     _hck(host().hgh_write_nanosim_fasta(genome, len(genome), name.encode(), n_reads, seed, path.encode()))
+
+
+def set_host_threads(n: int):
+    """Reader threads of load_records / jf_stream (1 = the sequential readers, 0 = default)."""
+    host().hgh_set_threads(n)
 
 
 def load_records(paths, annotate: bool):

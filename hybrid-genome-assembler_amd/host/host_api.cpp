@@ -140,7 +140,7 @@ int hgh_load_records(const char** paths, int n_paths, int annotate, char** bases
 
 int hgh_jf_stream(const char* path, char** out, uint64_t* len, uint64_t* n_records) {
     return guard([&] {
-        std::string s = hgah::jf_stream(path, n_records);
+        const hgah::Bytes s = hgah::jf_stream(path, n_records);
         *out = dup(s.data(), s.size());
         *len = s.size();
     });
@@ -152,6 +152,9 @@ int hgh_fmt_double(double v, char* buf, int cap) {
     std::memcpy(buf, s.c_str(), s.size() + 1);
     return (int)s.size();
 }
+
+// Reader threads of load_records / jf_stream (1 = the sequential readers).
+void hgh_set_threads(int n) { hgah::set_host_threads(n); }
 
 // hll::HyperLogLog::estimate of 2^b registers (kmer_analysis.h).
 double hgh_hll_estimate(const uint8_t* regs, int b) { return hgah::hll_estimate(regs, b); }

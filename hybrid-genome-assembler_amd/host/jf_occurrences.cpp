@@ -127,7 +127,7 @@ int main(int argc, char* argv[]) {
             check(hga_count_add_rows(ctx, f, dk.data(), dc.data(), dk.size()), "hga_count_add_rows");
             continue;
         }
-        const std::string s = hgah::jf_stream(read_paths[f]);
+        const hgah::Bytes s = hgah::jf_stream(read_paths[f]);
         check(hga_count_add(ctx, f, s.data(), s.size()), "hga_count_add");
         counted.push_back(f);
     }

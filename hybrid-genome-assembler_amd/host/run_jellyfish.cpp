@@ -25,7 +25,7 @@ int main(int argc, char* argv[]) {
     };
     check(hga_ctx_create(&ctx, dev_env ? std::atoi(dev_env) : 0), "hga_ctx_create");
     check(hga_count_begin(ctx, k, 1), "hga_count_begin");
-    const std::string s = hgah::jf_stream(reads);
+    const hgah::Bytes s = hgah::jf_stream(reads);
     check(hga_count_add(ctx, 0, s.data(), s.size()), "hga_count_add");
     check(hga_count_run(ctx, 2), "hga_count_run");
     uint64_t *keys = nullptr, n = 0;

@@ -1,5 +1,6 @@
 // seqio.cpp — see seqio.h.  Reference semantics are cited per function.
 #include "seqio.h"
+#include "seqio_internal.h"
 
 #include <charconv>
 #include <cstdio>
@@ -24,38 +25,6 @@ std::string FileMeta::repr() const {
 namespace {
 
 enum class Rec { FASTQ, FASTA };
-enum class Hdr { UNKNOWN, SIMLORD, NANOSIM, PASS };
-
-struct HeaderParsers {
-    // SequenceRecordIterator.h:98-105
-    std::regex simlord{";length=([0-9]+)bp;startpos=([0-9]+);"};
-    std::regex nanosim{"_([0-9]+)_[^_]+_[^_]+_[^_]+_[^_]+_([0-9]+)_"};
-    std::regex pass{"([0-9]+)_([0-9]+)\\|([0-9]+)\\|"};
-
-    // (start, length) as in parse_*_header (SequenceRecordIterator.cpp:179-205)
-    std::pair<uint32_t, uint32_t> parse(Hdr h, const std::string& s) const {
-        std::smatch m;
-        switch (h) {
-            case Hdr::SIMLORD:
-                if (std::regex_search(s, m, simlord))
-                    return {(uint32_t)std::stoul(m[2].str()), (uint32_t)std::stoul(m[1].str())};
-                break;
-            case Hdr::NANOSIM:
-                if (std::regex_search(s, m, nanosim))
-                    return {(uint32_t)std::stoul(m[1].str()), (uint32_t)std::stoul(m[2].str())};
-                break;
-            case Hdr::PASS:
-                if (std::regex_search(s, m, pass)) {
-                    const uint32_t len = (uint32_t)(std::stoul(m[2].str()) - std::stoul(m[1].str()));
-                    return {(uint32_t)std::stoul(m[3].str()), len};
-                }
-                break;
-            default: break;
-        }
-        return {0, 0};
-    }
-};
-
 struct EndOfInput {};
 
 // The reader's line stream: getline over the files in order, switching file on EOF.
@@ -120,15 +89,21 @@ class LineStream {
     int type_ = 1;
 };
 
+
+}  // namespace
+
 std::string basename_of(const std::string& p) {
     const size_t i = p.find_last_of("/\\");
     return i == std::string::npos ? p : p.substr(i + 1);
 }
 
-}  // namespace
+const HeaderParsers& header_parsers() {
+    static const HeaderParsers hp;
+    return hp;
+}
 
-RecordSet load_records(const std::vector<std::string>& paths, bool annotate, bool keep_text) {
-    HeaderParsers hp;
+RecordSet load_records_seq(const std::vector<std::string>& paths, bool annotate, bool keep_text) {
+    const HeaderParsers& hp = header_parsers();
     LineStream ls(paths, hp);
     RecordSet rs;
     rs.file_meta.resize(paths.size());
@@ -155,7 +130,7 @@ RecordSet load_records(const std::vector<std::string>& paths, bool annotate, boo
         const int fidx = ls.file_index();
         const std::string hdr = header.empty() ? std::string() : header.substr(1);
         const auto se = hp.parse(ls.hdr(), hdr);
-        rs.bases.insert(rs.bases.end(), seq.begin(), seq.end());
+        rs.bases.append(seq.data(), seq.size());
         rs.offsets.push_back(rs.bases.size());
         rs.category.push_back(annotate ? fidx : 0);
         rs.start.push_back(se.first != 0 ? se.first : 0);
@@ -193,7 +168,7 @@ RecordSet load_records(const std::vector<std::string>& paths, bool annotate, boo
     return rs;
 }
 
-std::string jf_stream(const std::string& path, uint64_t* n_records) {
+Bytes jf_stream_seq(const std::string& path, uint64_t* n_records) {
     std::FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) throw std::invalid_argument("File with path \"" + path + "\" does not exist");
     std::string data;
@@ -206,8 +181,7 @@ std::string jf_stream(const std::string& path, uint64_t* n_records) {
         throw std::runtime_error("short read on " + path);
     }
     std::fclose(f);
-    std::string out;
-    out.reserve(data.size());
+    Bytes out;
     uint64_t recs = 0;
     size_t i = 0;
     const size_t n = data.size();
@@ -230,13 +204,13 @@ std::string jf_stream(const std::string& path, uint64_t* n_records) {
             if (recs) out.push_back('\n');
             ++recs;
             while ((have = next_line(b, e)) && !(e > b && data[b] == '>'))
-                out.append(data, b, e - b);
+                out.append(data.data() + b, e - b);
         } else if (h == '@') {
             if (recs) out.push_back('\n');
             ++recs;
             size_t seqlen = 0;
             while ((have = next_line(b, e)) && !(e > b && data[b] == '+')) {
-                out.append(data, b, e - b);
+                out.append(data.data() + b, e - b);
                 seqlen += e - b;
             }
             size_t qlen = 0;

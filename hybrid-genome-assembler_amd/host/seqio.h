@@ -17,6 +17,36 @@
 
 namespace hgah {
 
+// Growable byte buffer on anonymous memory (transparent huge pages where the kernel allows),
+// never zero-filled: resize() leaves new bytes unspecified.  Holds the readers' large outputs
+// (hundreds of MB), where value-initialising a std::string / std::vector costs as much as the
+// parse itself.
+class Bytes {
+   public:
+    Bytes() = default;
+    ~Bytes();
+    Bytes(Bytes&& o) noexcept : p_(o.p_), n_(o.n_), cap_(o.cap_) { o.p_ = nullptr; o.n_ = o.cap_ = 0; }
+    Bytes& operator=(Bytes&& o) noexcept;
+    Bytes(const Bytes&) = delete;
+    Bytes& operator=(const Bytes&) = delete;
+    char* data() { return p_; }
+    const char* data() const { return p_; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    char& operator[](size_t i) { return p_[i]; }
+    char operator[](size_t i) const { return p_[i]; }
+    void resize(size_t n);
+    void clear() { n_ = 0; }
+    void append(const char* s, size_t n);
+    void push_back(char c) { append(&c, 1); }
+    std::string str() const { return std::string(p_ ? p_ : "", n_); }
+
+   private:
+    void reserve(size_t n);
+    char* p_ = nullptr;
+    size_t n_ = 0, cap_ = 0;
+};
+
 struct FileMeta {               // MetaData / ReadFileMetaData, SequenceRecordIterator.h:52-68
     std::string filename;
     uint64_t records = 0;
@@ -30,7 +60,7 @@ struct FileMeta {               // MetaData / ReadFileMetaData, SequenceRecordIt
 
 struct RecordSet {
     // CSR of sequences in reader order; read i has ReadID i + 1.
-    std::vector<char> bases;
+    Bytes bases;
     std::vector<uint64_t> offsets{0};
     std::vector<int32_t> category;      // GenomeReadData::category_id
     std::vector<uint32_t> start, end;   // simulator-header coordinates (0 when unknown)
@@ -44,10 +74,20 @@ struct RecordSet {
 
 // Throws std::invalid_argument / std::logic_error with the reference's messages.
 // keep_text=false skips headers/qualities (the lookup needs sequences only).
+// load_records / jf_stream run multi-threaded (fastio.cpp) with host_threads() threads and
+// fall back to the sequential *_seq definitions for layouts that are not line-local; the
+// results are identical.
 RecordSet load_records(const std::vector<std::string>& paths, bool annotate, bool keep_text = true);
+RecordSet load_records_seq(const std::vector<std::string>& paths, bool annotate, bool keep_text = true);
 
 // Whole-file read of the sequences jellyfish would count, '\n'-separated.
-std::string jf_stream(const std::string& path, uint64_t* n_records = nullptr);
+Bytes jf_stream(const std::string& path, uint64_t* n_records = nullptr);
+Bytes jf_stream_seq(const std::string& path, uint64_t* n_records = nullptr);
+
+// Reader threads: set_host_threads(n > 0) overrides HGA_HOST_THREADS (default min(16, cores));
+// 1 = the sequential readers.
+int host_threads();
+void set_host_threads(int n);
 
 // fmt "{}" formatting of a double (shortest round trip, fmt's fixed/exponent switch).
 std::string fmt_double(double v);
