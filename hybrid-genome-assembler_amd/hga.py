@@ -502,3 +502,119 @@ def fmt_double(v: float) -> str:
     buf = C.create_string_buffer(64)
     n = host().hgh_fmt_double(v, buf, 64)
     return buf.value.decode() if n >= 0 else ""
+
+
+# ---------------------------------------------------------------------------- clustering stages
+# lib/libhga_cluster.so: ReadClusteringEngine after construct_indices (host/clustering.cpp).
+class ClusterConfig(C.Structure):
+    """ReadClusteringConfig (src/clustering/ReadClusteringEngine.h:138-148)."""
+    _fields_ = [("sc_min_size", C.c_int), ("sc_max_size", C.c_int), ("sc_fraction", C.c_double),
+                ("sc_score", C.c_uint64), ("core_enrichment", C.c_uint64), ("tail_amplification", C.c_uint64),
+                ("threads", C.c_int), ("spectral_dims", C.c_int), ("force_spectral", C.c_int)]
+
+
+def cluster_config(sc_min=30, sc_max=-1, sc_fraction=0.15, sc_score=0, enrich=20, tail=40, threads=1, dims=16,
+                   force_spectral=False) -> ClusterConfig:
+    return ClusterConfig(sc_min, sc_max, sc_fraction, sc_score, enrich, tail, threads, dims, 1 if force_spectral else 0)
+
+
+CLUSTER_SYMBOLS = {
+    "hgc_last_error": (C.c_char_p, []),
+    "hgc_free": (None, [_vp]),
+    "hgc_cluster": (C.c_int, [C.c_char_p, _u64p, _i32p, C.c_uint64, C.c_uint64, C.c_uint32, _u64p, _u32p, _u64p,
+                              _u32p, _u32p, _u64p, _u32p, C.c_uint32, C.POINTER(ClusterConfig), C.c_int,
+                              C.POINTER(_u32p), _u64p, C.POINTER(_u32p), C.POINTER(_vp)]),
+    "hgc_union_find": (C.c_int, [_u32p, _u32p, _u64p, C.c_uint64, _u32p, C.c_uint64, C.c_int, C.c_int,
+                                 C.POINTER(_u64p), C.POINTER(_u32p), _u64p, C.POINTER(_u64p), C.POINTER(_u32p)]),
+    "hgc_spectral": (C.c_int, [_u32p, _u32p, _u64p, C.c_uint64, C.c_int, C.POINTER(_u64p), C.POINTER(_u32p), _u64p]),
+    "hgc_sym_eigen": (C.c_int, [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+}
+_cl = None
+
+
+def cluster_lib():
+    global _cl
+    if _cl is None:
+        path = os.path.join(LIB_DIR, "libhga_cluster.so")
+        if not os.path.exists(path):
+            raise HgaError(f"{path} missing: build it with `make -C hybrid-genome-assembler_amd`")
+        _cl = C.CDLL(path)
+        _bind(_cl, CLUSTER_SYMBOLS)
+    return _cl
+
+
+def _cck(status):
+    if status != 0:
+        raise HgaError(f"clustering: {cluster_lib().hgc_last_error().decode()}")
+
+
+def _conn_arrays(conns):
+    x = np.ascontiguousarray([c[0] for c in conns], np.uint32)
+    y = np.ascontiguousarray([c[1] for c in conns], np.uint32)
+    s = np.ascontiguousarray([c[2] for c in conns], np.uint64)
+    return x, y, s
+
+
+def _components(ptr, ids, n):
+    L = cluster_lib()
+    p = _take(ptr, n.value + 1, np.uint64, L.hgc_free)
+    v = _take(ids, int(p[-1]), np.uint32, L.hgc_free)
+    return [v[p[i]:p[i + 1]].tolist() for i in range(n.value)]
+
+
+def union_find(conns, restricted=(), min_size=1, max_size=-1):
+    """union_find (ReadClusteringEngine.cpp:424-489): [(component ids, spanning-tree edges)]."""
+    x, y, s = _conn_arrays(conns)
+    r = np.ascontiguousarray(sorted(restricted), np.uint32)
+    cp, ci, tp, txy = _u64p(), _u32p(), _u64p(), _u32p()
+    n = C.c_uint64()
+    _cck(cluster_lib().hgc_union_find(_p(x, C.c_uint32), _p(y, C.c_uint32), _p(s, C.c_uint64), len(x),
+                                      _p(r, C.c_uint32), len(r), min_size, max_size, C.byref(cp), C.byref(ci),
+                                      C.byref(n), C.byref(tp), C.byref(txy)))
+    comps = _components(cp, ci, n)
+    tptr = _take(tp, n.value + 1, np.uint64, cluster_lib().hgc_free)
+    t = _take(txy, 2 * int(tptr[-1]), np.uint32, cluster_lib().hgc_free).reshape(-1, 2)
+    return [(comps[i], [tuple(e) for e in t[tptr[i]:tptr[i + 1]].tolist()]) for i in range(n.value)]
+
+
+def spectral_clustering(conns, dims=16):
+    """spectral_clustering (ReadClusteringEngine.cpp:653-697)."""
+    x, y, s = _conn_arrays(conns)
+    cp, ci = _u64p(), _u32p()
+    n = C.c_uint64()
+    _cck(cluster_lib().hgc_spectral(_p(x, C.c_uint32), _p(y, C.c_uint32), _p(s, C.c_uint64), len(x), dims,
+                                    C.byref(cp), C.byref(ci), C.byref(n)))
+    return _components(cp, ci, n)
+
+
+def sym_eigen(a):
+    a = np.ascontiguousarray(a, np.float64)
+    n = a.shape[0]
+    val, vec = np.zeros(n), np.zeros((n, n))
+    _cck(cluster_lib().hgc_sym_eigen(_p(a, C.c_double), n, _p(val, C.c_double), _p(vec, C.c_double)))
+    return val, vec
+
+
+def cluster_host(bases: bytes, offsets, category, idx, avg_read_length, cfg=None, debug=False, first_read_id=1):
+    """run_clustering after construct_indices on the host (no device state): (component ids,
+    per-read component id (0 = none), log text)."""
+    L = cluster_lib()
+    cfg = cfg or cluster_config()
+    off = np.ascontiguousarray(offsets, np.uint64)
+    cat = np.ascontiguousarray(category, np.int32)
+    a = {k: np.ascontiguousarray(idx[k], np.uint64 if k.endswith("ptr") else np.uint32)
+         for k in ("hit_ptr", "sorted_kid", "first_ptr", "first_kid", "first_pos", "kci_ptr", "kci_read")}
+    n = len(off) - 1
+    ip, op = _u32p(), _u32p()
+    lp = C.c_void_p()
+    ni = C.c_uint64()
+    _cck(L.hgc_cluster(bases, _p(off, C.c_uint64), _p(cat, C.c_int32), n, avg_read_length, first_read_id,
+                       _p(a["hit_ptr"], C.c_uint64), _p(a["sorted_kid"], C.c_uint32), _p(a["first_ptr"], C.c_uint64),
+                       _p(a["first_kid"], C.c_uint32), _p(a["first_pos"], C.c_uint32), _p(a["kci_ptr"], C.c_uint64),
+                       _p(a["kci_read"], C.c_uint32), len(a["kci_ptr"]) - 1, C.byref(cfg), 1 if debug else 0,
+                       C.byref(ip), C.byref(ni), C.byref(op), C.byref(lp)))
+    ids = _take(ip, ni.value, np.uint32, L.hgc_free)
+    owner = _take(op, n, np.uint32, L.hgc_free)
+    log = C.string_at(lp.value).decode()
+    L.hgc_free(lp.value)
+    return ids, owner, log

@@ -11,10 +11,11 @@
 // "Index construction took <ms>ms" timing line and, when every file is a category
 // (ReadClusteringEngine.cpp:229), "X out of Y kmers are discriminative" (:285-297).
 //
-// The stages after index construction (connections, union-find, tails, spectral
-// clustering, export; ReadClusteringEngine.cpp:301-826) are out of this build's
-// scope; with --index-out <path> the constructed index is written
-// as a binary file for a downstream consumer.
+// The stages after index construction (ReadClusteringEngine.cpp:301-826) run in
+// host/clustering.cpp: the first connection pass on the GPU (hga_connections_run on the
+// lookup's device-resident indices), union-find, merging, spanning-tree tails, spectral
+// clustering and the per-component FASTA/FASTQ export with the reference's timing lines.
+// With --index-out <path> the constructed index is also written as a binary file.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -27,6 +28,7 @@
 #include <vector>
 
 #include "args.h"
+#include "clustering.h"
 #include "hga.h"
 #include "seqio.h"
 
@@ -84,8 +86,6 @@ int main(int argc, char* argv[]) {
            [&](const std::string& v) { index_out = v; });
     ap.parse(argc, argv);
     for (auto& p : ap.positional) read_paths.push_back(p);
-    (void)threads; (void)sc_min; (void)sc_max; (void)dims; (void)sc_fraction; (void)sc_score; (void)tail;
-    (void)enrich; (void)force_spectral;
     if (ap.has("help")) {
         std::cout << ap.describe();
         return 0;
@@ -96,7 +96,7 @@ int main(int argc, char* argv[]) {
     const int k = kk.second;
     if (k < 1 || k > 32) throw std::invalid_argument("Kmer size must be in [1, 32]");
 
-    hgah::RecordSet rs = hgah::load_records(read_paths, debug, !index_out.empty());
+    hgah::RecordSet rs = hgah::load_records(read_paths, debug, true);   // headers/qualities for the export
     for (auto& m : rs.file_meta) std::cout << m.repr();
     if (output_folder_path.empty()) output_folder_path = "./" + rs.meta.filename + "_clusters/";
     const bool engine_debug = rs.file_meta.size() == rs.categories;   // ReadClusteringEngine.cpp:229
@@ -149,9 +149,21 @@ int main(int argc, char* argv[]) {
         std::fwrite(kci_read.data(), 4, kci_read.size(), f);
         std::fclose(f);
     }
-    std::cerr << "categorization: " << sz.reads_hit << " of " << sz.n_reads << " reads carry SDKs (" << sz.hits
-              << " hits); the clustering stages after index construction are not part of this build "
-                 "(output folder " << output_folder_path << " not written)\n";
+    hgah::ClusteringConfig cfg;   // ReadClusteringConfig (ReadClusteringEngine.h:138-148)
+    cfg.scaffold_component_min_size = sc_min;
+    cfg.scaffold_component_max_size = sc_max;
+    cfg.scaffold_forming_fraction = sc_fraction;
+    cfg.scaffold_forming_score = sc_score;
+    cfg.enrichment_connections_min_score = enrich;
+    cfg.tail_amplification_min_score = tail;
+    cfg.threads = threads;
+    cfg.spectral_dims = dims;
+    cfg.force_spectral = force_spectral;
+    hgah::ClusteringEngine engine(cfg, engine_debug, rs, 1, std::move(hit_ptr), std::move(sorted_kid),
+                                  std::move(first_ptr), std::move(first_kid), std::move(first_pos), kci_ptr, kci_read,
+                                  ctx);
+    const std::vector<hgah::ComponentID> cluster_ids = engine.run(std::cout);   // run_clustering (:699-802)
+    engine.export_components(cluster_ids, output_folder_path, std::cout);       // read_clustering.cpp:82
     hga_ctx_destroy(ctx);
     return 0;
 }

@@ -155,3 +155,47 @@ def test_categorization_end_to_end(tmp_path):
         arr = np.frombuffer(raw[off:off + int(cnt) * np.dtype(dt).itemsize], dt)
         off += int(cnt) * np.dtype(dt).itemsize
         assert np.array_equal(arr, g[name]), name
+
+
+@pytest.mark.parametrize("args,cfg", [
+    (["--sc_min_size", "5", "--core_enrichment", "8", "--tail_amplification", "10"],
+     dict(sc_min=5, sc_max=-1, sc_fraction=0.15, sc_score=0, enrich=8, tail=10, dims=16)),
+    (["--sc_min_size", "3", "--sc_max_size", "40", "--sc_fraction", "0.3", "--core_enrichment", "4",
+      "--tail_amplification", "6", "--spectral_dims", "4"],
+     dict(sc_min=3, sc_max=40, sc_fraction=0.3, sc_score=0, enrich=4, tail=6, dims=4))])
+def test_categorization_clusters_and_export(tmp_path, hga_mod, args, cfg):
+    """The whole categorization run (first connection pass on the GPU, the rest on the host) against
+    the Python restatement of run_clustering + export_components (ReadClusteringEngine.cpp:699-826)."""
+    import pyref_cluster as pc
+    k = 15
+    ga = hga_mod.gen_genome(40_000, 5)
+    gb = hga_mod.gen_haplotype(ga, 0.02, 0, 6)
+    paths = [str(tmp_path / "hapA.fa"), str(tmp_path / "hapB.fa")]
+    hga_mod.write_nanosim_fasta(ga, "hapA", 180, 7, paths[0])
+    hga_mod.write_nanosim_fasta(gb, "hapB", 180, 8, paths[1])
+    ka, _ = oracle.kmer_windows(ga, k)
+    kb, _ = oracle.kmer_windows(gb, k)
+    sdk = np.setxor1d(np.unique(ka), np.unique(kb))
+    (tmp_path / "sdk.txt").write_text("".join(kmer_str(c, k) + "\n" for c in sdk))
+    out = subprocess.run([os.path.join(BIN, "categorization"), *paths, "-k", str(tmp_path / "sdk.txt"), "-d",
+                          "-o", str(tmp_path / "clusters"), *args], capture_output=True, text=True, cwd=tmp_path,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    for line in ("Index construction took", "Calculation of connections between reads took", "Union-find took",
+                 "Merging into core components took"):
+        assert line in out.stdout
+    rec = hga_mod.load_records(paths, True)
+    idx = oracle.construct_indices(rec["bases"], rec["offsets"], k, sdk)
+    lengths = np.diff(rec["offsets"])
+    eng = pc.Engine(idx, lengths, rec["category"], int(rec["meta"][-1][4]), True, cfg)
+    want = eng.run()
+    assert f"Exported {len(want)} components\n" in out.stdout
+    files = sorted(os.listdir(tmp_path / "clusters"))
+    assert files == sorted(f"#{c}.fa" for c in want)
+    headers = [l[1:].split("\n")[0] for p in paths for l in open(p).read().split(">")[1:]]
+    for c in want:
+        text = open(tmp_path / "clusters" / f"#{c}.fa").read()
+        members = sorted(eng.comps[c]["reads"])
+        exp = "".join(f">{headers[r - 1]}\n{rec['bases'][rec['offsets'][r - 1]:rec['offsets'][r]].decode()}\n"
+                      for r in members)
+        assert text == exp
