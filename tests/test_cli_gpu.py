@@ -192,7 +192,7 @@ def test_categorization_clusters_and_export(tmp_path, hga_mod, args, cfg):
     assert f"Exported {len(want)} components\n" in out.stdout
     files = sorted(os.listdir(tmp_path / "clusters"))
     assert files == sorted(f"#{c}.fa" for c in want)
-    headers = [l[1:].split("\n")[0] for p in paths for l in open(p).read().split(">")[1:]]
+    headers = [l.split("\n")[0] for p in paths for l in open(p).read().split(">")[1:]]
     for c in want:
         text = open(tmp_path / "clusters" / f"#{c}.fa").read()
         members = sorted(eng.comps[c]["reads"])
