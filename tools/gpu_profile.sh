@@ -13,7 +13,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
     || { echo "stats run failed"; tail -5 $R/gpurun_out/stats_$TAG.err; exit 1; }
 for p in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $p --output-format csv -d $R/gpurun_out/hbm_${TAG}_$p -o run -- \
-      python3 $R/tools/kprof.py --reps 2 --lookup > $R/gpurun_out/hbm_${TAG}_$p.log 2>&1 \
+      python3 $R/tools/kprof.py --reps 2 --lookup --connections --hll > $R/gpurun_out/hbm_${TAG}_$p.log 2>&1 \
       || { echo "pmc $p failed"; tail -3 $R/gpurun_out/hbm_${TAG}_$p.log; exit 1; }
 done
 cd $R && python3 tools/pmc_summary.py gpurun_out/hbm_${TAG}_* --json gpurun_out/hbm_$TAG.json > gpurun_out/hbm_$TAG.txt \
