@@ -460,6 +460,9 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 constexpr uint32_t QN_C = 128;   // miss-queue entries per wave
+#ifndef HGA_CNT_BRANCHLESS
+#define HGA_CNT_BRANCHLESS 0
+#endif
 #ifndef HGA_EMIT_STAGE
 #define HGA_EMIT_STAGE 1
 #endif
@@ -566,8 +569,16 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 #pragma unroll
                     for (int t = GRP - 1; t >= 0; --t) w = kg[q][t] == rv[q] ? t : w;
                     const bool live = rv[q] != EMPTY;   // EMPTY would match an empty slot
+#if HGA_CNT_BRANCHLESS
+                    // every lane issues the add (+0 into its home group's first slot when it
+                    // misses): no per-element exec-mask branch around the LDS atomic
+                    const bool hit = live && w >= 0;
+                    atomicAdd(&cf[GRP * g + (hit ? (uint32_t)w : 0u)], hit ? 1u : 0u);
+                    miss |= (live && !hit ? 1u : 0u) << q;
+#else
                     if (live && w >= 0) atomicAdd(&cf[GRP * g + w], 1u);
                     else if (live) miss |= 1u << q;
+#endif
                 }
                 // the misses (new keys, keys displaced from home) are compacted into this
                 // wave's queue once per batch
@@ -736,7 +747,7 @@ __global__ void __launch_bounds__(NT_H) kc_spec_hist(const uint32_t* __restrict_
                                                      unsigned long long* __restrict__ over_cur,
                                                      uint64_t over_cap,
                                                      unsigned long long* __restrict__ err) {
-    __shared__ uint32_t lh[MAX_THR * TL];
+    extern __shared__ uint32_t lh[];   // n_thr * TL counters (sized at launch: occupancy)
     __shared__ double sthr[MAX_THR];
     for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_H) lh[i] = 0;
     if (threadIdx.x < n_thr) sthr[threadIdx.x] = thr[threadIdx.x];
@@ -785,7 +796,7 @@ __global__ void kc_hist_compact(const unsigned long long* __restrict__ hist, uin
     }
 }
 
-constexpr int SEL_R = 16;   // rows per thread: one cursor atomic per 4096 rows
+constexpr int SEL_R = 32;   // rows per thread: one cursor atomic (and one count atomic) per 8192 rows
 __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ keys,
                                                   const uint32_t* __restrict__ cnt, uint64_t rows,
                                                   uint64_t cap, uint32_t F, int64_t lower,
@@ -814,11 +825,13 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
     }
     uint32_t tot;
     const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popc(take), ws, &tot);
-    uint32_t dsum = (uint32_t)__popc(disc);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
-    if ((threadIdx.x & 63) == 0 && dsum) atomicAdd(&stat[1], (unsigned long long)dsum);
-    if (threadIdx.x == 0) s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
+    // same-address device atomics serialise (≈88/µs chip-wide): one pair per workgroup
+    uint32_t dtot;
+    (void)block_excl_scan<NT_H>((uint32_t)__popc(disc), ws, &dtot);
+    if (threadIdx.x == 0) {
+        s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
+        if (dtot) atomicAdd(&stat[1], (unsigned long long)dtot);
+    }
     __syncthreads();
     uint64_t o = s_base + ex;
 #pragma unroll
@@ -1143,9 +1156,9 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     HGA_HIP(hipMemsetAsync(ctrl, 0, 32, c->stream));
     HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_for(std::max<uint64_t>(s.rows, 1), NT_H),
-                                                       (uint64_t)c->num_cu * 2);
+                                                       (uint64_t)c->num_cu * 4);
     c->launch("kc_spec_hist", [&] {
-        hipLaunchKernelGGL(kc_spec_hist, dim3(grid), dim3(NT_H), 0, c->stream,
+        hipLaunchKernelGGL(kc_spec_hist, dim3(grid), dim3(NT_H), (size_t)n_thr * TL * 4, c->stream,
                            s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, dthr, n_thr,
                            hist, over, ctrl, over_cap, ctrl + 1);
     });

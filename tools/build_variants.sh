@@ -7,7 +7,7 @@ mkdir -p $R/build_var
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   d=$R/build_var/obj_$name; mkdir -p $d
-  for f in sort count exchange lookup api; do
+  for f in sort count exchange lookup connect hll api; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$R/include -I$P/host $flags -c $P/csrc/$f.hip -o $d/$f.o &
   done
   wait || exit 1
