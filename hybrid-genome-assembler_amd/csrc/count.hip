@@ -252,20 +252,36 @@ struct PackFile {
     const uint8_t* seq;
     uint64_t n, woff, nw;
 };
+constexpr int PK_W = 4;   // words per thread (grid-strided: every load instruction coalesced)
 __global__ void kc_pack_files(const PackFile* __restrict__ files, uint32_t F, uint64_t total_words,
                               uint32_t* __restrict__ pk, uint16_t* __restrict__ vd,
                               unsigned long long* __restrict__ gstat, uint64_t n_first) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < 8) gstat[g] = g == 3 ? (unsigned long long)n_first : 0ull;
-    if (g >= total_words) return;
-    uint32_t f = 0;
-    while (f + 1 < F && files[f + 1].woff <= g) ++f;
-    const PackFile pf = files[f];
-    const uint64_t wl = g - pf.woff;
-    uint32_t code = 0, valid = 0;
-    if (wl >= (uint64_t)PAD_WORDS && wl - PAD_WORDS < pf.nw) pack_word<false>(pf.seq, pf.n, wl - PAD_WORDS, code, valid);
-    pk[g] = code;
-    vd[g] = (uint16_t)valid;
+    const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    if (g0 < 8) gstat[g0] = g0 == 3 ? (unsigned long long)n_first : 0ull;
+    uint4 raw[PK_W];
+    PackFile pf[PK_W];
+    uint64_t wl[PK_W];
+    bool in[PK_W];
+#pragma unroll
+    for (int u = 0; u < PK_W; ++u) {   // all loads first
+        const uint64_t g = g0 + (uint64_t)u * stride;
+        uint32_t f = 0;
+        while (f + 1 < F && files[f + 1].woff <= g) ++f;
+        pf[u] = files[f];
+        wl[u] = g - pf[u].woff;
+        in[u] = g < total_words && wl[u] >= (uint64_t)PAD_WORDS && wl[u] - PAD_WORDS < pf[u].nw;
+        raw[u] = in[u] ? load16(pf[u].seq, (int64_t)((wl[u] - PAD_WORDS) * 16), pf[u].n) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < PK_W; ++u) {
+        const uint64_t g = g0 + (uint64_t)u * stride;
+        if (g >= total_words) continue;
+        uint32_t code = 0, valid = 0;
+        if (in[u]) pack_bytes<false>(raw[u], code, valid);
+        pk[g] = code;
+        vd[g] = (uint16_t)valid;
+    }
 }
 
 // ---------------------------------------------------------------- layout
@@ -806,7 +822,7 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
     __shared__ uint32_t ws[NT_H / 64 + 1];
     __shared__ unsigned long long s_base;
     const uint64_t base = (uint64_t)blockIdx.x * NT_H * SEL_R;
-    uint32_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
+    uint64_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
 #pragma unroll
     for (int q = 0; q < SEL_R; ++q) {
         const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
@@ -819,15 +835,15 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
             nz += c > 0;
         }
         if (lower <= total && total <= upper) {
-            take |= 1u << q;
-            if (nz == 1) disc |= 1u << q;
+            take |= 1ull << q;
+            if (nz == 1) disc |= 1ull << q;
         }
     }
     uint32_t tot;
-    const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popc(take), ws, &tot);
+    const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popcll(take), ws, &tot);
     // same-address device atomics serialise (≈88/µs chip-wide): one pair per workgroup
     uint32_t dtot;
-    (void)block_excl_scan<NT_H>((uint32_t)__popc(disc), ws, &dtot);
+    (void)block_excl_scan<NT_H>((uint32_t)__popcll(disc), ws, &dtot);
     if (threadIdx.x == 0) {
         s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
         if (dtot) atomicAdd(&stat[1], (unsigned long long)dtot);
@@ -836,10 +852,10 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
     uint64_t o = s_base + ex;
 #pragma unroll
     for (int q = 0; q < SEL_R; ++q)
-        if ((take >> q) & 1u) {
+        if ((take >> q) & 1ull) {
             const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
             out[o] = keys[r];
-            out_flag[o] = (disc >> q) & 1u;
+            out_flag[o] = (uint32_t)((disc >> q) & 1ull);
             ++o;
         }
 }
@@ -1005,7 +1021,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     Blk* table = static_cast<Blk*>(s.regions.ensure(table_cap * sizeof(Blk)));
     // P: pack all files + counter init, one launch
     c->launch("kc_pack", [&] {
-        hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256)), dim3(256), 0,
+        hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256 * PK_W)), dim3(256), 0,
                            c->stream, d_pf, F, woff[F], pk_all, vd_all, gstat, n_first);
     });
     c->check_launch("kc_pack");

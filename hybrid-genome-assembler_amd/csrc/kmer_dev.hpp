@@ -187,9 +187,7 @@ __device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
 // One thread per 16 bases: packed codes (first base in bits 31:30) and valid bits.
 // 16 bases starting at 16w -> 2-bit codes (MSB-first) + valid bits.
 template <bool REF>
-__device__ __forceinline__ void pack_word(const uint8_t* __restrict__ s, uint64_t n, uint64_t w, uint32_t& code,
-                                          uint32_t& valid) {
-    const uint4 v = load16(s, (int64_t)(w * 16), n);
+__device__ __forceinline__ void pack_bytes(const uint4 v, uint32_t& code, uint32_t& valid) {
     const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
     code = 0;
     valid = 0;
@@ -203,6 +201,12 @@ __device__ __forceinline__ void pack_word(const uint8_t* __restrict__ s, uint64_
         code |= c << (30 - 2 * j);
         valid |= (ok ? 1u : 0u) << j;
     }
+}
+
+template <bool REF>
+__device__ __forceinline__ void pack_word(const uint8_t* __restrict__ s, uint64_t n, uint64_t w, uint32_t& code,
+                                          uint32_t& valid) {
+    pack_bytes<REF>(load16(s, (int64_t)(w * 16), n), code, valid);
 }
 
 template <bool REF>
