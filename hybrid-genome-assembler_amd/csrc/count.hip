@@ -36,7 +36,7 @@ constexpr int P_B = 16;       // window ends per thread
 constexpr int TP_B = NT_B * P_B;       // 8192 window ends per tile
 constexpr uint64_t ST_ALIGN = TP_B;    // super-tiles are whole tiles
 #ifndef HGA_MAX_FB
-#define HGA_MAX_FB 12
+#define HGA_MAX_FB 13
 #endif
 #ifndef HGA_NT_C
 #define HGA_NT_C 1024
@@ -479,6 +479,21 @@ constexpr uint32_t QN_C = 128;   // miss-queue entries per wave
 #ifndef HGA_CNT_BRANCHLESS
 #define HGA_CNT_BRANCHLESS 0
 #endif
+#ifndef HGA_EXP_LOADONLY
+#define HGA_EXP_LOADONLY 0
+#endif
+#ifndef HGA_EXP_NOADD
+#define HGA_EXP_NOADD 0
+#endif
+#ifndef HGA_EXP_NOMISS
+#define HGA_EXP_NOMISS 0
+#endif
+#ifndef HGA_EXP_NOCLAIM
+#define HGA_EXP_NOCLAIM 0
+#endif
+#ifndef HGA_EXP_NOEMIT
+#define HGA_EXP_NOEMIT 0
+#endif
 #ifndef HGA_EMIT_STAGE
 #define HGA_EMIT_STAGE 1
 #endif
@@ -493,7 +508,8 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                                                  uint32_t T, uint32_t maxload, uint32_t min_count,
                                                  KP kp, uint64_t* __restrict__ out_key,
                                                  uint32_t* __restrict__ out_cnt, uint64_t cap,
-                                                 unsigned long long* __restrict__ gstat) {
+                                                 unsigned long long* __restrict__ gstat,
+                                                 const uint32_t* __restrict__ blist) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_TAB];
     __shared__ uint32_t s_occ, s_ovf, s_sp, s_ranges;
     __shared__ uint32_t stk_lo[40], stk_hi[40];
@@ -505,14 +521,18 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
     E* myq = qbuf[threadIdx.x >> 6];
     uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + (size_t)T * sizeof(E));
     const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;
-    const uint64_t* f = fs + (uint64_t)b * (F + 1);
     const E EMPTY = ~E(0);
     const uint32_t rbits = kp.rbits;
     const uint32_t SUBB = rbits < 16 ? rbits : 16;
     const uint32_t full_hi = 1u << SUBB;
     const uint32_t mc = min_count ? min_count : 1u;
     const uint32_t G = T / GRP;
+    // every bucket (blist null), or the buckets listed by kc_count_p (count in gstat[5])
+    const uint32_t n_b = blist ? (uint32_t)gstat[5] : gridDim.x;
+    for (uint32_t it = blockIdx.x; it < n_b; it += gridDim.x) {
+    const uint32_t b = blist ? blist[it] : it;
+    const uint64_t* f = fs + (uint64_t)b * (F + 1);
+    __syncthreads();
     if (tid == 0) {
         stk_lo[0] = 0;
         stk_hi[0] = full_hi;
@@ -574,6 +594,15 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                 // 1) every home group read before any counter is touched (the counters share
                 //    the LDS array, so an atomic in between would serialise the reads): one LDS
                 //    round trip settles every element whose key already sits in its home group
+#if HGA_EXP_LOADONLY
+                {
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int q = 0; q < PF_C; ++q) acc += (uint32_t)rv[q];
+                    if (acc == 0x12345678u) atomicAdd(&cf[0], 1u);
+                    continue;
+                }
+#endif
                 E kg[PF_C][GRP];
 #pragma unroll
                 for (int q = 0; q < PF_C; ++q) read_group(keys, (uint32_t)rv[q] & (G - 1), kg[q]);
@@ -592,10 +621,17 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                     atomicAdd(&cf[GRP * g + (hit ? (uint32_t)w : 0u)], hit ? 1u : 0u);
                     miss |= (live && !hit ? 1u : 0u) << q;
 #else
+#if HGA_EXP_NOADD
+                    if (live && w < 0) miss |= 1u << q;
+#else
                     if (live && w >= 0) atomicAdd(&cf[GRP * g + w], 1u);
                     else if (live) miss |= 1u << q;
 #endif
+#endif
                 }
+#if HGA_EXP_NOMISS
+                miss = 0;
+#endif
                 // the misses (new keys, keys displaced from home) are compacted into this
                 // wave's queue once per batch
                 const uint32_t nm = (uint32_t)__popc(miss);
@@ -742,6 +778,330 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                     out_cnt[(size_t)ff * cap + o] = c >= mc ? c : 0u;
                 }
                 ++o;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) atomicMax(&gstat[1], (unsigned long long)s_ranges);
+    }
+}
+
+// ---------------------------------------------------------------- pass C (packed entries)
+// F <= 2 files, u32 remainders, every per-file run of the bucket < 65536 instances (so no
+// count can pass 16 bits): one u64 LDS entry per slot, key in the low 32 bits, the counts in
+// the high 32 (F = 1: one 32-bit count; F = 2: file 0 in bits 32-47, file 1 in bits 48-63).
+// A hit is one ds_add_u64 into the entry it matched; a new key claims the first empty slot of
+// its home group with one ds_cmpst_b64 that also sets its count — inline, no loop — so only
+// keys whose home group is full (or that lost a claim race) go through the per-wave queue.
+// 64 KB per workgroup: two workgroups per CU, one's prologue / emit overlaps the other's stream.
+// Buckets this kernel cannot take (a per-file run >= 65536) are listed for kc_count.
+#ifndef HGA_NT_P
+#define HGA_NT_P 512
+#endif
+#ifndef HGA_PF_P
+#define HGA_PF_P 8
+#endif
+#ifndef HGA_GP_P
+#define HGA_GP_P 2
+#endif
+constexpr int NT_P = HGA_NT_P;
+constexpr int PF_P = HGA_PF_P;          // binned elements per thread per batch
+constexpr int GP_P = HGA_GP_P;          // entries per probe group (2: one ds_read_b128)
+constexpr uint32_t T_P = 8192;          // entries (64 KB)
+constexpr uint32_t G_P = T_P / GP_P;
+constexpr uint32_t QN_P = 128;          // per-wave queue of unsettled keys
+constexpr uint32_t MAXPROBE_P = 64;     // groups probed before the table counts as over-full
+constexpr uint64_t EMPTY_P = 0xFFFFFFFFull;
+static_assert(T_P % NT_P == 0, "emit: whole slots per thread");
+
+__device__ __forceinline__ void read_group_p(const uint64_t* tab, uint32_t g, uint64_t (&e)[GP_P]) {
+#pragma unroll
+    for (int t = 0; t < GP_P / 2; ++t) {
+        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(tab)[g * (GP_P / 2) + t];
+        e[2 * t] = v.x;
+        e[2 * t + 1] = v.y;
+    }
+}
+
+// Settle key r (count +inc) by probing from its home group; false if MAXPROBE_P groups were full.
+__device__ __forceinline__ bool probe_p(uint64_t* tab, uint32_t r, uint64_t inc) {
+    uint32_t g = r & (G_P - 1);
+    for (uint32_t steps = 0; steps < MAXPROBE_P;) {
+        uint64_t e[GP_P];
+        read_group_p(tab, g, e);
+        int w = -1, e0 = -1;
+#pragma unroll
+        for (int t = GP_P - 1; t >= 0; --t) {
+            w = (uint32_t)e[t] == r ? t : w;
+            e0 = e[t] == EMPTY_P ? t : e0;
+        }
+        if (w >= 0) {
+            atomicAdd((unsigned long long*)&tab[g * GP_P + w], (unsigned long long)inc);
+            return true;
+        }
+        if (e0 >= 0) {
+            const uint32_t sl = g * GP_P + (uint32_t)e0;
+            const uint64_t old = atomicCAS((unsigned long long*)&tab[sl], (unsigned long long)EMPTY_P,
+                                           (unsigned long long)(inc | r));
+            if (old == EMPTY_P) return true;
+            if ((uint32_t)old == r) {
+                atomicAdd((unsigned long long*)&tab[sl], (unsigned long long)inc);
+                return true;
+            }
+            continue;   // lost the slot to another key: re-read the same group
+        }
+        g = (g + 1) & (G_P - 1);
+        ++steps;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(NT_P, 4) kc_count_p(const uint32_t* __restrict__ binned,
+                                                   const uint64_t* __restrict__ fs, uint32_t F,
+                                                   uint32_t min_count, KP kp, uint64_t* __restrict__ out_key,
+                                                   uint32_t* __restrict__ out_cnt, uint64_t cap,
+                                                   unsigned long long* __restrict__ gstat,
+                                                   uint32_t* __restrict__ blist) {
+    __shared__ __attribute__((aligned(16))) uint64_t tab[T_P];
+    __shared__ uint32_t qbuf[NT_P / 64][QN_P];
+    __shared__ uint32_t s_ovf, s_sp, s_ranges;
+    __shared__ uint32_t stk_lo[40], stk_hi[40];
+    __shared__ uint32_t ws[NT_P / 64 + 1];
+    __shared__ unsigned long long s_base;
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    uint32_t* myq = qbuf[tid >> 6];
+    const uint32_t b = blockIdx.x;
+    const uint64_t* f = fs + (uint64_t)b * (F + 1);
+    for (uint32_t ff = 0; ff < F; ++ff)
+        if (f[ff + 1] - f[ff] >= 65536u && F > 1) {   // a count could pass 16 bits: kc_count takes it
+            if (tid == 0) blist[atomicAdd(&gstat[5], 1ull)] = b;
+            return;
+        }
+    const uint32_t rbits = kp.rbits;
+    const uint32_t SUBB = rbits < 16 ? rbits : 16;
+    const uint32_t full_hi = 1u << SUBB;
+    const uint32_t mc = min_count ? min_count : 1u;
+    if (tid == 0) {
+        stk_lo[0] = 0;
+        stk_hi[0] = full_hi;
+        s_sp = 1;
+        s_ranges = 0;
+    }
+    __syncthreads();
+    while (true) {
+        const uint32_t sp = s_sp;
+        if (sp == 0) break;
+        const uint32_t lo = stk_lo[sp - 1], hi = stk_hi[sp - 1];
+        __syncthreads();
+        if (tid == 0) {
+            s_sp = sp - 1;
+            s_ovf = 0;
+        }
+        for (uint32_t i = tid; i < T_P; i += NT_P) tab[i] = EMPTY_P;
+        __syncthreads();
+        const bool filt = !(lo == 0 && hi == full_hi);
+        uint32_t qn = 0;   // this wave's queued keys (uniform)
+        for (uint32_t ff = 0; ff < F; ++ff) {
+            const uint64_t a = f[ff], e = f[ff + 1];
+            const uint64_t inc = F == 1 ? (1ull << 32) : (1ull << (32 + 16 * ff));
+            constexpr uint64_t STEP = (uint64_t)NT_P * PF_P;
+            if (a == e) continue;
+            const uint64_t nfull = (e - a) / STEP;
+            uint32_t nx[PF_P];
+            auto load = [&](uint64_t i0, uint64_t bi) {
+                if (bi < nfull) {
+                    const uint32_t* __restrict__ bp = binned + i0;
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) nx[q] = bp[q * NT_P + tid];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) {
+                        const uint64_t i = i0 + (uint64_t)q * NT_P + tid;
+                        nx[q] = i < e ? binned[i] : 0xFFFFFFFFu;
+                    }
+                }
+            };
+            // settle the queue 64 keys at a time (all lanes busy); leftovers stay queued
+            auto drain = [&](uint32_t min_take) {   // while at least min_take (>= 1) are queued
+                while (qn >= min_take && qn > 0) {
+                    const uint32_t take = qn < 64 ? qn : 64;
+                    const uint32_t q0 = qn - take;
+                    bool ok = true;
+                    if (lane < take) ok = probe_p(tab, myq[q0 + lane], inc);
+                    if (!ok) s_ovf = 1u;
+                    qn = q0;
+                    wave_lds_sync();
+                }
+            };
+            load(a, 0);
+            uint64_t bi = 0;
+            for (uint64_t i0 = a; i0 < e; i0 += STEP, ++bi) {
+                uint32_t rv[PF_P];
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q) rv[q] = nx[q];
+                if (i0 + STEP < e) load(i0 + STEP, bi + 1);
+                if (filt) {
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) {
+                        const uint32_t sk = SUBB ? rv[q] >> (rbits - SUBB) : 0u;
+                        rv[q] = (sk >= lo && sk < hi) ? rv[q] : 0xFFFFFFFFu;
+                    }
+                }
+#if HGA_EXP_LOADONLY
+                {
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) acc += rv[q];
+                    if (acc == 0x12345678u) s_ovf = 2u;
+                    continue;
+                }
+#endif
+                // 1) home groups of the whole batch read before any entry is touched
+                uint64_t eg[PF_P][GP_P];
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q) read_group_p(tab, rv[q] & (G_P - 1), eg[q]);
+                uint32_t claim = 0, slot[PF_P];
+                uint32_t miss = 0;
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q) {
+                    const uint32_t g = rv[q] & (G_P - 1);
+                    int w = -1, e0 = -1;
+#pragma unroll
+                    for (int t = GP_P - 1; t >= 0; --t) {
+                        w = (uint32_t)eg[q][t] == rv[q] ? t : w;
+                        e0 = eg[q][t] == EMPTY_P ? t : e0;
+                    }
+                    const bool live = rv[q] != 0xFFFFFFFFu;
+                    slot[q] = g * GP_P + (uint32_t)(w >= 0 ? w : e0);
+                    if (live && w >= 0) atomicAdd((unsigned long long*)&tab[slot[q]], (unsigned long long)inc);
+                    else if (live && e0 >= 0) claim |= 1u << q;
+                    else if (live) miss |= 1u << q;
+                }
+#if HGA_EXP_NOCLAIM
+                claim = 0; miss = 0;
+#endif
+                // 2) new keys: claim the first empty slot of the home group (count included)
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q)
+                    if ((claim >> q) & 1u) {
+                        const uint64_t old = atomicCAS((unsigned long long*)&tab[slot[q]],
+                                                       (unsigned long long)EMPTY_P,
+                                                       (unsigned long long)(inc | rv[q]));
+                        if (old != EMPTY_P) {
+                            if ((uint32_t)old == rv[q]) atomicAdd((unsigned long long*)&tab[slot[q]], (unsigned long long)inc);
+                            else miss |= 1u << q;
+                        }
+                    }
+                // 3) the rest (home group full, or a lost claim) into this wave's queue
+                const uint32_t nm = (uint32_t)__popc(miss);
+                const uint64_t any = __ballot(nm != 0u);
+                if (any) {
+                    const uint32_t incl = wave_incl_scan(nm, (int)lane);
+                    const uint32_t tot = __shfl(incl, 63);
+                    if (qn + tot > QN_P) {   // no room: settle the queue first, then these in place
+                        drain(1);
+                        bool ok = true;
+                        while (__any(miss != 0u)) {
+                            if (miss) {
+                                const int q = __builtin_ctz(miss);
+                                miss &= miss - 1u;
+                                uint32_t pick = rv[0];
+#pragma unroll
+                                for (int t = 1; t < PF_P; ++t) pick = q == t ? rv[t] : pick;
+                                ok = probe_p(tab, pick, inc) && ok;
+                            }
+                        }
+                        if (!ok) s_ovf = 1u;
+                    } else {
+                        uint32_t pos = qn + incl - nm;
+                        while (miss) {
+                            const int q = __builtin_ctz(miss);
+                            miss &= miss - 1u;
+                            uint32_t pick = rv[0];
+#pragma unroll
+                            for (int t = 1; t < PF_P; ++t) pick = q == t ? rv[t] : pick;
+                            myq[pos++] = pick;
+                        }
+                        qn += tot;
+                        wave_lds_sync();
+                        drain(64);
+                    }
+                }
+                if ((i0 - a) % (4 * STEP) == 0 && __atomic_load_n(&s_ovf, __ATOMIC_RELAXED)) break;
+            }
+            drain(1);
+        }
+        __syncthreads();
+        if (s_ovf) {
+            __syncthreads();
+            if (tid == 0) {
+                if (hi - lo <= 1 || s_sp + 2 > 40) {
+                    atomicOr(&gstat[2], 1ull);
+                    s_sp = 0;
+                } else {
+                    const uint32_t mid = lo + (hi - lo) / 2;
+                    stk_lo[s_sp] = mid; stk_hi[s_sp] = hi;
+                    stk_lo[s_sp + 1] = lo; stk_hi[s_sp + 1] = mid;
+                    s_sp += 2;
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+#if HGA_EXP_NOEMIT
+        if (tab[tid] == 0x1234567ull) s_ranges = 9;
+        __syncthreads();
+        continue;
+#endif
+        // emit: each thread owns ES consecutive entries; kept rows are compacted in place
+        constexpr int ES = T_P / NT_P;
+        uint64_t ent[ES];
+#pragma unroll
+        for (int j = 0; j < ES; j += 2) {
+            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(tab)[(tid * ES + j) / 2];
+            ent[j] = v.x;
+            ent[j + 1] = v.y;
+        }
+        uint32_t keep = 0;
+#pragma unroll
+        for (int j = 0; j < ES; ++j) {
+            uint64_t c = ent[j] >> 32;
+            if (F == 1) {
+                c = c >= mc ? c : 0u;
+            } else {
+                const uint32_t c0 = (uint32_t)c & 0xFFFFu, c1 = (uint32_t)(c >> 16);
+                c = (uint64_t)(c0 >= mc ? c0 : 0u) | ((uint64_t)(c1 >= mc ? c1 : 0u) << 16);
+            }
+            ent[j] = (c << 32) | (ent[j] & 0xFFFFFFFFull);
+            if (ent[j] != EMPTY_P && c) keep |= 1u << j;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<NT_P>((uint32_t)__popc(keep), ws, &tot);
+        if (tid == 0) {
+            s_base = tot ? atomicAdd(&gstat[0], (unsigned long long)tot) : 0ull;
+            ++s_ranges;
+        }
+        __syncthreads();   // every entry read: the table becomes the staging area
+        uint32_t o = ex;
+#pragma unroll
+        for (int j = 0; j < ES; ++j)
+            if ((keep >> j) & 1u) tab[o++] = ent[j];
+        __syncthreads();
+        const uint64_t base = s_base;
+        if (base + tot > cap) {
+            if (tid == 0 && tot) atomicOr(&gstat[2], 2ull);
+        } else {
+            const uint64_t hb = kp.fb ? ((uint64_t)b << rbits) : 0ull;
+            for (uint32_t j = tid; j < tot; j += NT_P) {
+                const uint64_t v = tab[j];
+                out_key[base + j] = mix_inv(hb | (v & 0xFFFFFFFFull), kp.mix);
+                if (F == 1) {
+                    out_cnt[base + j] = (uint32_t)(v >> 32);
+                } else {
+                    out_cnt[base + j] = (uint32_t)(v >> 32) & 0xFFFFu;
+                    out_cnt[cap + base + j] = (uint32_t)(v >> 48);
+                }
             }
         }
         __syncthreads();
@@ -939,9 +1299,13 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     kp.mix = make_mix(s.k);
     const uint32_t nbits = 2u * (uint32_t)s.k;
     // fan-out: ~16K windows per fine bucket, at most 8192 buckets, never more bits than the key
+    // packed-entry counting (kc_count_p): F <= 2 and u32 remainders; ~32K windows per bucket
+    static const bool legacy = std::getenv("HGA_COUNT_LEGACY") != nullptr;
+    const bool packed = F <= 2 && nbits - std::min<uint32_t>(MAX_FB, nbits) <= 31 && !legacy;
+    const uint64_t per_bucket = packed ? 65536 : 16384;
     uint32_t fb = 0, fb_max = MAX_FB;
     if (const char* e = std::getenv("HGA_FB_MAX")) fb_max = std::min<uint32_t>(MAX_FB, (uint32_t)std::atoi(e));
-    while (fb < fb_max && fb < nbits && (total_bytes >> fb) > 16384) ++fb;
+    while (fb < fb_max && fb < nbits && (total_bytes >> fb) > per_bucket) ++fb;
     kp.fb = fb;
     kp.nb = 1u << fb;
     kp.rbits = nbits - fb;
@@ -1064,15 +1428,28 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     });
     c->check_launch("kc_rebin");
     // C: per-bucket count
+    if (packed && e32) {
+        uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nb * 4));
+        c->launch("kc_count", [&] {
+            hipLaunchKernelGGL(kc_count_p, dim3(nb), dim3(NT_P), 0, c->stream, static_cast<const uint32_t*>(binned), fs, F,
+                               min_per_file, kp, s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, blist);
+            // buckets with a per-file run >= 65536 (listed in blist, count in gstat[5])
+            hipLaunchKernelGGL(kc_count<uint32_t>, dim3(std::min<uint32_t>(nb, (uint32_t)c->num_cu)), dim3(NT_C), 0,
+                               c->stream, static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
+                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat,
+                               (const uint32_t*)blist);
+        });
+        c->check_launch("kc_count");
+    } else
     c->launch("kc_count", [&] {
         if (e32)
             hipLaunchKernelGGL(kc_count<uint32_t>, dim3(nb), dim3(NT_C), 0, c->stream,
                                static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
-                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, (const uint32_t*)nullptr);
         else
             hipLaunchKernelGGL(kc_count<uint64_t>, dim3(nb), dim3(NT_C), 0, c->stream,
                                static_cast<const uint64_t*>(binned), fs, F, T, maxload, min_per_file, kp,
-                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat);
+                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, (const uint32_t*)nullptr);
     });
     c->check_launch("kc_count");
     unsigned long long h_stat[8];
