@@ -12,5 +12,5 @@ for spec in "$@"; do
   done
   wait || exit 1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $d/*.o -o $R/build_var/$name.so
-  echo "built $name ($flags)"
+  rm -rf $d; echo "built $name ($flags)"
 done
