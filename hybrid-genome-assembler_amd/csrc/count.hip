@@ -491,6 +491,21 @@ constexpr uint32_t QN_C = 128;   // miss-queue entries per wave
 #ifndef HGA_EXP_NOCLAIM
 #define HGA_EXP_NOCLAIM 0
 #endif
+#ifndef HGA_EXP_SH_LOADONLY
+#define HGA_EXP_SH_LOADONLY 0
+#endif
+#ifndef HGA_EXP_SH_NOROWS
+#define HGA_EXP_SH_NOROWS 0
+#endif
+#ifndef HGA_EXP_SH_NODIV
+#define HGA_EXP_SH_NODIV 0
+#endif
+#ifndef HGA_EXP_SH_NOLDS
+#define HGA_EXP_SH_NOLDS 0
+#endif
+#ifndef HGA_EXP_SH_NOFLUSH
+#define HGA_EXP_SH_NOFLUSH 0
+#endif
 #ifndef HGA_EXP_NOEMIT
 #define HGA_EXP_NOEMIT 0
 #endif
@@ -1111,76 +1126,141 @@ __global__ void __launch_bounds__(NT_P, 4) kc_count_p(const uint32_t* __restrict
 
 // ---------------------------------------------------------------- histogram / select
 constexpr int NT_H = 256;
+constexpr int NT_S = 1024;            // spec_hist workgroup
+constexpr int SG_S = 4;               // 4-row groups per thread per step (16-B loads, all issued together)
 constexpr uint32_t TL = 1024;         // LDS-privatised totals
 constexpr uint32_t TD = 1u << 16;     // dense global totals; beyond -> overflow list
 constexpr uint32_t MAX_THR = 16;
 
-__global__ void __launch_bounds__(NT_H) kc_spec_hist(const uint32_t* __restrict__ cnt, uint64_t rows,
+// Threshold index of a row: std::set<double>::upper_bound of ((double)prev / total) * 100
+// (JellyfishOccurrenceReader.cpp:103), IEEE round-to-nearest, no FMA; thresholds ascending
+// and unique (a std::set), so upper_bound = the number of thresholds <= x.  Branch-free over
+// the uniform threshold array (scalar loads).
+__device__ __forceinline__ uint32_t spec_index(uint32_t prev, uint32_t total, const double* __restrict__ thr,
+                                               uint32_t n_thr) {
+    const double x = __dmul_rn(__ddiv_rn((double)prev, (double)total), 100.0);
+    uint32_t ti = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < MAX_THR; ++t)
+        if (t < n_thr) ti += thr[t] <= x ? 1u : 0u;
+    return ti;
+}
+
+// Per row: total and prevalent count -> threshold index -> one LDS increment (total < TL).
+// Rows are taken four at a time with 16-B loads per file (rows_cap is a multiple of 4) and
+// SG_S groups in flight per thread; one workgroup per CU, whose LDS histogram is flushed with
+// one global atomic per nonzero bin.  Totals in [TL, TD) (rare) go to the dense global
+// histogram directly (ctrl[3] counts them), >= TD to an overflow list.
+__global__ void __launch_bounds__(NT_S) kc_spec_hist(const uint32_t* __restrict__ cnt, uint64_t rows,
                                                      uint64_t cap, uint32_t F,
                                                      const double* __restrict__ thr, uint32_t n_thr,
                                                      unsigned long long* __restrict__ hist,
                                                      unsigned long long* __restrict__ over,
-                                                     unsigned long long* __restrict__ over_cur,
-                                                     uint64_t over_cap,
-                                                     unsigned long long* __restrict__ err) {
-    extern __shared__ uint32_t lh[];   // n_thr * TL counters (sized at launch: occupancy)
-    __shared__ double sthr[MAX_THR];
-    for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_H) lh[i] = 0;
-    if (threadIdx.x < n_thr) sthr[threadIdx.x] = thr[threadIdx.x];
+                                                     unsigned long long* __restrict__ ctrl,
+                                                     uint64_t over_cap) {
+    extern __shared__ uint32_t lh[];   // n_thr * TL counters (sized at launch)
+    for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_S) lh[i] = 0;
     __syncthreads();
-    for (uint64_t r = (uint64_t)blockIdx.x * NT_H + threadIdx.x; r < rows;
-         r += (uint64_t)gridDim.x * NT_H) {
-        uint64_t total = 0;
-        uint32_t prev = 0;
-        for (uint32_t f = 0; f < F; ++f) {
-            const uint32_t c = cnt[(size_t)f * cap + r];
-            total += c;
-            prev = c > prev ? c : prev;
+    const uint64_t groups = (rows + 3) / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * NT_S;
+    const uint4* __restrict__ c4 = reinterpret_cast<const uint4*>(cnt);
+    for (uint64_t g0 = (uint64_t)blockIdx.x * NT_S + threadIdx.x; g0 < groups; g0 += stride * SG_S) {
+        uint32_t tot[SG_S][4], prv[SG_S][4];
+#pragma unroll
+        for (int u = 0; u < SG_S; ++u) {
+            const uint64_t g = g0 + (uint64_t)u * stride;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tot[u][j] = prv[u][j] = 0;
+#pragma unroll
+            for (uint32_t f = 0; f < 4; ++f)
+                if (f < F && g < groups) {
+                    const uint4 v = c4[(f * cap) / 4 + g];
+                    const uint32_t c[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        tot[u][j] += c[j];
+                        prv[u][j] = c[j] > prv[u][j] ? c[j] : prv[u][j];
+                    }
+                }
+            for (uint32_t f = 4; f < F && g < groups; ++f) {
+                const uint4 v = c4[(f * cap) / 4 + g];
+                const uint32_t c[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    tot[u][j] += c[j];
+                    prv[u][j] = c[j] > prv[u][j] ? c[j] : prv[u][j];
+                }
+            }
         }
-        // ((double)prevalent / (double)total) * 100, IEEE round-to-nearest, no FMA
-        const double x = __dmul_rn(__ddiv_rn((double)prev, (double)total), 100.0);
-        uint32_t ti = 0;
-        while (ti < n_thr && !(sthr[ti] > x)) ++ti;   // std::set::upper_bound
-        if (ti >= n_thr) { atomicOr(err, 1ull); continue; }
-        if (total < TL) atomicAdd(&lh[ti * TL + (uint32_t)total], 1u);
-        else if (total < TD) atomicAdd(&hist[(uint64_t)ti * TD + total], 1ull);
-        else {
-            const unsigned long long o = atomicAdd(over_cur, 1ull);
-            if (o < over_cap) over[o] = ((unsigned long long)ti << 56) | total;
-            else atomicOr(err, 2ull);
+#pragma unroll
+        for (int u = 0; u < SG_S; ++u) {
+            const uint64_t g = g0 + (uint64_t)u * stride;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (g * 4 + j >= rows) continue;
+                const uint32_t total = tot[u][j];
+                const uint32_t ti = spec_index(prv[u][j], total, thr, n_thr);
+                if (ti >= n_thr) { atomicOr(&ctrl[1], 1ull); continue; }
+                if (total < TL) {
+                    atomicAdd(&lh[ti * TL + total], 1u);
+                } else if (total < TD) {
+                    atomicAdd(&hist[(uint64_t)ti * TD + total], 1ull);
+                    atomicAdd(&ctrl[3], 1ull);
+                } else {
+                    const unsigned long long o = atomicAdd(&ctrl[0], 1ull);
+                    if (o < over_cap) over[o] = ((unsigned long long)ti << 56) | total;
+                    else atomicOr(&ctrl[1], 2ull);
+                }
+            }
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_H) {
+    for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_S) {
         const uint32_t v = lh[i];
         if (v) atomicAdd(&hist[(uint64_t)(i / TL) * TD + (i % TL)], (unsigned long long)v);
     }
 }
 
-// Nonzero dense bins -> (threshold index << 56 | total, count) pairs.
-__global__ void kc_hist_compact(const unsigned long long* __restrict__ hist, uint64_t n,
-                                unsigned long long* __restrict__ out, unsigned long long* __restrict__ cur,
-                                uint64_t cap) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const unsigned long long v = hist[i];
-    if (!v) return;
-    const unsigned long long o = atomicAdd(cur, 1ull);
-    if (o < cap) {
-        out[2 * o] = ((unsigned long long)(i / TD) << 56) | (i % TD);
+// Nonzero dense bins -> (threshold index << 56 | total, count) pairs, one cursor atomic per
+// workgroup; bins are zeroed as they are read (the histogram is cleared once, at allocation).
+// Totals >= TL are scanned only when kc_spec_hist put rows there (ctrl[3]).
+constexpr int NT_HC = 256;
+__global__ void __launch_bounds__(NT_HC) kc_hist_compact(unsigned long long* __restrict__ hist, uint32_t n_thr,
+                                                         unsigned long long* __restrict__ out,
+                                                         unsigned long long* __restrict__ ctrl, uint64_t cap) {
+    __shared__ uint32_t ws[NT_HC / 64 + 1];
+    __shared__ unsigned long long s_base;
+    const uint64_t i = (uint64_t)blockIdx.x * NT_HC + threadIdx.x;
+    const uint32_t ti = (uint32_t)(i / TD), tot = (uint32_t)(i % TD);
+    const uint32_t bt = (uint32_t)(((uint64_t)blockIdx.x * NT_HC) % TD);
+    if (bt >= TL && ctrl[3] == 0) return;   // uniform per workgroup (TL is a multiple of NT_HC)
+    unsigned long long v = 0;
+    if (ti < n_thr) {
+        v = hist[i];
+        if (v) hist[i] = 0;
+    }
+    uint32_t n;
+    const uint32_t ex = block_excl_scan<NT_HC>(v ? 1u : 0u, ws, &n);
+    if (threadIdx.x == 0) s_base = n ? atomicAdd(&ctrl[2], (unsigned long long)n) : 0ull;
+    __syncthreads();
+    const uint64_t o = s_base + ex;
+    if (v && o < cap) {
+        out[2 * o] = ((unsigned long long)ti << 56) | tot;
         out[2 * o + 1] = v;
     }
 }
 
-constexpr int SEL_R = 32;   // rows per thread: one cursor atomic (and one count atomic) per 8192 rows
+constexpr int SEL_R = 16;   // rows per thread: one cursor atomic (and one count atomic) per 4096 rows
 __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ keys,
                                                   const uint32_t* __restrict__ cnt, uint64_t rows,
                                                   uint64_t cap, uint32_t F, int64_t lower,
                                                   int64_t upper, uint64_t* __restrict__ out,
-                                                  uint32_t* __restrict__ out_flag,
+                                                  uint32_t* __restrict__ out_flag, bool flag_bit,
                                                   unsigned long long* __restrict__ stat) {
     __shared__ uint32_t ws[NT_H / 64 + 1];
     __shared__ unsigned long long s_base;
+    __shared__ uint64_t stage[NT_H * SEL_R];
+    __shared__ uint8_t sflag[NT_H * SEL_R];
     const uint64_t base = (uint64_t)blockIdx.x * NT_H * SEL_R;
     uint64_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
 #pragma unroll
@@ -1189,7 +1269,14 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
         if (r >= rows) continue;
         int64_t total = 0;
         uint32_t nz = 0;
-        for (uint32_t f = 0; f < F; ++f) {
+#pragma unroll
+        for (uint32_t f = 0; f < 4; ++f)   // the common file counts unrolled: loads issued together
+            if (f < F) {
+                const uint32_t c = cnt[(size_t)f * cap + r];
+                total += c;
+                nz += c > 0;
+            }
+        for (uint32_t f = 4; f < F; ++f) {
             const uint32_t c = cnt[(size_t)f * cap + r];
             total += c;
             nz += c > 0;
@@ -1208,16 +1295,21 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
         s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
         if (dtot) atomicAdd(&stat[1], (unsigned long long)dtot);
     }
-    __syncthreads();
-    uint64_t o = s_base + ex;
+    // kept keys staged in LDS (row order), then written out coalesced
+    uint32_t o = ex;
 #pragma unroll
     for (int q = 0; q < SEL_R; ++q)
         if ((take >> q) & 1ull) {
             const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
-            out[o] = keys[r];
-            out_flag[o] = (uint32_t)((disc >> q) & 1ull);
-            ++o;
+            stage[o++] = keys[r] | (flag_bit ? (((disc >> q) & 1ull) << 63) : 0ull);
+            if (!flag_bit) sflag[o - 1] = (uint8_t)((disc >> q) & 1ull);
         }
+    __syncthreads();
+    const uint64_t ob = s_base;
+    for (uint32_t j = threadIdx.x; j < tot; j += NT_H) {
+        out[ob + j] = stage[j];
+        if (!flag_bit) out_flag[ob + j] = sflag[j];
+    }
 }
 
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
@@ -1367,7 +1459,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const PackFile* d_pf = reinterpret_cast<const PackFile*>(d_tab + sizeof(BinFile) * F);
 
     const size_t esz1 = e1_32 ? 4 : 8, esz = e32 ? 4 : 8;
-    const uint64_t cap = total_bytes / std::max<uint32_t>(1, min_per_file) + 1;
+    const uint64_t cap = (total_bytes / std::max<uint32_t>(1, min_per_file) + 4) & ~3ull;   // x4: 16-B row groups
     s.rows_key.ensure(cap * 8);
     s.rows_cnt.ensure(cap * 4 * F);
     const uint32_t slot_b = (uint32_t)esz + 4u * F;
@@ -1532,7 +1624,8 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     const uint32_t n_thr = (uint32_t)thr.size();
     HGA_REQUIRE(n_thr >= 1 && n_thr <= MAX_THR, HGA_ERR_INVALID, "1..16 thresholds supported");
     const uint64_t over_cap = 1u << 20;
-    const size_t hbytes = (size_t)n_thr * TD * 8;
+    const size_t hbytes = (size_t)MAX_THR * TD * 8;
+    const bool fresh = s.hist_dense.cap == 0;
     char* base = static_cast<char*>(s.hist_dense.ensure(hbytes + over_cap * 8 + 256 + 64));
     auto* hist = reinterpret_cast<unsigned long long*>(base);
     auto* over = reinterpret_cast<unsigned long long*>(base + hbytes);
@@ -1545,15 +1638,15 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     auto* hc = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8);
     auto* hcomp = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8 + 32);
     std::memcpy(hthr, thr.data(), n_thr * 8);
-    HGA_HIP(hipMemsetAsync(base, 0, hbytes, c->stream));
+    if (fresh) HGA_HIP(hipMemsetAsync(base, 0, hbytes, c->stream));   // kept clear by kc_hist_compact
     HGA_HIP(hipMemsetAsync(ctrl, 0, 32, c->stream));
     HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
-    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_for(std::max<uint64_t>(s.rows, 1), NT_H),
-                                                       (uint64_t)c->num_cu * 4);
+    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_for(std::max<uint64_t>((s.rows + 3) / 4, 1), NT_S * SG_S),
+                                                       (uint64_t)c->num_cu);
     c->launch("kc_spec_hist", [&] {
-        hipLaunchKernelGGL(kc_spec_hist, dim3(grid), dim3(NT_H), (size_t)n_thr * TL * 4, c->stream,
+        hipLaunchKernelGGL(kc_spec_hist, dim3(grid), dim3(NT_S), (size_t)n_thr * TL * 4, c->stream,
                            s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, dthr, n_thr,
-                           hist, over, ctrl, over_cap, ctrl + 1);
+                           hist, over, ctrl, over_cap);
     });
     c->check_launch("kc_spec_hist");
     // compact the dense bins on the device: only (threshold, total, count) triples cross PCIe
@@ -1561,12 +1654,12 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     auto* comp = static_cast<unsigned long long*>(s.hist_comp.ensure(ncap * 16 + 64));
     const uint64_t nd = (uint64_t)n_thr * TD;
     c->launch("kc_spec_hist", [&] {
-        hipLaunchKernelGGL(kc_hist_compact, dim3(blocks_for(nd, 256)), dim3(256), 0, c->stream, hist, nd, comp,
-                           ctrl + 2, ncap);
+        hipLaunchKernelGGL(kc_hist_compact, dim3(blocks_for(nd, NT_HC)), dim3(NT_HC), 0, c->stream, hist, n_thr, comp,
+                           ctrl, ncap);
     });
     c->check_launch("kc_hist_compact");
     // one synchronisation: counters and (speculatively) the first chunk of triples together
-    HGA_HIP(hipMemcpyAsync(hc, ctrl, 24, hipMemcpyDeviceToHost, c->stream));
+    HGA_HIP(hipMemcpyAsync(hc, ctrl, 32, hipMemcpyDeviceToHost, c->stream));
     HGA_HIP(hipMemcpyAsync(hcomp, comp, SPEC_CHUNK * 16, hipMemcpyDeviceToHost, c->stream));
     c->sync();
     HGA_REQUIRE(!(hc[1] & 1ull), HGA_ERR_INVALID, "a row's specificity is above the last threshold");
@@ -1605,19 +1698,20 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     uint64_t* out = reinterpret_cast<uint64_t*>(sb);
     uint32_t* flag = reinterpret_cast<uint32_t*>(sb + cap * 8);
     auto* stat = static_cast<unsigned long long*>(s.sel_tmp.ensure(64));
+    const bool flag_bit = s.k <= 31;   // the discriminative flag rides in key bit 63
     HGA_HIP(hipMemsetAsync(stat, 0, 16, c->stream));
     if (s.rows) {
         c->launch("kc_select", [&] {
             hipLaunchKernelGGL(kc_select, dim3(blocks_for(s.rows, NT_H * SEL_R)), dim3(NT_H), 0, c->stream,
                                s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), s.rows,
-                               s.rows_cap, s.n_files, lower, upper, out, flag, stat);
+                               s.rows_cap, s.n_files, lower, upper, out, flag, flag_bit, stat);
         });
         c->check_launch("kc_select");
     }
     unsigned long long hs[2];
     HGA_HIP(hipMemcpyAsync(hs, stat, 16, hipMemcpyDeviceToHost, c->stream));
     c->sync();
-    radix_sort_u64(c, out, flag, hs[0], 2 * s.k, s.scratch);
+    radix_sort_u64(c, out, flag_bit ? nullptr : flag, hs[0], 2 * s.k, s.scratch);
     s.n_sel = hs[0];
     *n_out = hs[0];
     *n_discr = hs[1];
@@ -1626,6 +1720,22 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
 void count_fetch_selected(hga_ctx* c, uint64_t* dst, uint8_t* flags) {
     auto& s = c->count;
     const uint64_t cap = std::max<uint64_t>(s.rows, 1);
+    const bool flag_bit = s.k <= 31;
+    if (flag_bit) {   // flag in bit 63 of each key
+        std::vector<uint64_t> tmp;
+        uint64_t* kd = dst;
+        if (!kd && flags && s.n_sel) {
+            tmp.resize(s.n_sel);
+            kd = tmp.data();
+        }
+        if (s.n_sel && kd) HGA_HIP(hipMemcpyAsync(kd, s.sel_keys.p, s.n_sel * 8, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        for (uint64_t i = 0; kd && i < s.n_sel; ++i) {
+            if (flags) flags[i] = (uint8_t)(kd[i] >> 63);
+            kd[i] &= ~(1ull << 63);
+        }
+        return;
+    }
     if (s.n_sel && dst)
         HGA_HIP(hipMemcpyAsync(dst, s.sel_keys.p, s.n_sel * 8, hipMemcpyDeviceToHost, c->stream));
     std::vector<uint32_t> f;

@@ -179,7 +179,7 @@ void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint6
     HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 rows per merge");
     HGA_REQUIRE(min_c >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
     const uint32_t F = s.n_files;
-    const uint64_t cap = std::max<uint64_t>(n, 1);
+    const uint64_t cap = (std::max<uint64_t>(n, 1) + 3) & ~3ull;   // x4: 16-B row groups (kc_spec_hist)
     s.rows_key.ensure(cap * 8);
     s.rows_cnt.ensure(cap * 4 * F);
     s.rows = 0;
@@ -397,7 +397,7 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
     const PackFmt pf{2 * s.k, cb, s.n_files, (1ull << cb) - 1};
     const uint64_t kmask = pf.kb >= 64 ? ~0ull : ((1ull << pf.kb) - 1);
     const uint32_t F = s.n_files;
-    const uint64_t cap = std::max<uint64_t>(n, 1);
+    const uint64_t cap = (std::max<uint64_t>(n, 1) + 3) & ~3ull;   // x4: 16-B row groups (kc_spec_hist)
     s.rows_key.ensure(cap * 8);
     s.rows_cnt.ensure(cap * 4 * F);
     s.rows = 0;

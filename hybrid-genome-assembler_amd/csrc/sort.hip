@@ -21,6 +21,15 @@ constexpr int RS_T = 256;              // threads per tile
 constexpr int RS_I = 16;               // items per thread
 constexpr int RS_TILE = RS_T * RS_I;   // 4096 keys per tile
 constexpr int SC_T = 1024, SC_I = 4, SC_TILE = SC_T * SC_I;
+#ifndef HGA_EXP_RS_NOLB
+#define HGA_EXP_RS_NOLB 0
+#endif
+#ifndef HGA_EXP_RS_NORANK
+#define HGA_EXP_RS_NORANK 0
+#endif
+#ifndef HGA_LBW
+#define HGA_LBW 8   // predecessor tiles read per look-back step (independent loads per digit thread)
+#endif
 
 // dmask: the pass's digit mask (the last pass may cover fewer than 8 bits: bits above the sort
 // width are payload and must not order the keys).
@@ -188,6 +197,11 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
     }
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
+#if HGA_EXP_RS_NORANK
+        rank[j] = j * 64 + lane;
+        if (lane == 0) wcnt[wave][dig[j] & 255] += 64;
+        continue;
+#endif
         const uint32_t d = dig[j];
         const bool ok = d < 256u;
         uint64_t m = __ballot(ok);
@@ -216,13 +230,13 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
         wcnt[3][d] = ex + c0 + c1 + c2;
         uint32_t* st = status + (uint64_t)tile * 256 + d;
         uint32_t excl = 0;
-        if (tile == 0) {
+        if (tile == 0 || HGA_EXP_RS_NOLB) {
             __hip_atomic_store(st, LB_P | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             __hip_atomic_store(st, LB_A | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // look back LBW tiles per step (independent loads), newest first; restart at the
             // first tile that has not published yet
-            constexpr int LBW = 8;
+            constexpr int LBW = HGA_LBW;
             int64_t t = (int64_t)tile - 1;
             while (true) {
                 uint32_t v[LBW];
