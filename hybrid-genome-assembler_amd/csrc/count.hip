@@ -28,6 +28,57 @@
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
 
+// Timing experiments (tools/build_variants.sh): each disables one part of a kernel; results are
+// wrong with any of them set, the default build has all 0.
+#ifndef HGA_S_NEXT
+#define HGA_S_NEXT 0
+#endif
+#ifndef HGA_EXP_S_HITSTORE
+#define HGA_EXP_S_HITSTORE 0
+#endif
+#ifndef HGA_EXP_S_NOHIT
+#define HGA_EXP_S_NOHIT 0
+#endif
+#ifndef HGA_EXP_LOADONLY
+#define HGA_EXP_LOADONLY 0
+#endif
+#ifndef HGA_EXP_NOADD
+#define HGA_EXP_NOADD 0
+#endif
+#ifndef HGA_EXP_NOMISS
+#define HGA_EXP_NOMISS 0
+#endif
+#ifndef HGA_EXP_NOCLAIM
+#define HGA_EXP_NOCLAIM 0
+#endif
+#ifndef HGA_EXP_B1_COMPUTEONLY
+#define HGA_EXP_B1_COMPUTEONLY 0
+#endif
+#ifndef HGA_EXP_B1_NOFHIST
+#define HGA_EXP_B1_NOFHIST 0
+#endif
+#ifndef HGA_EXP_B1_NOFLUSH
+#define HGA_EXP_B1_NOFLUSH 0
+#endif
+#ifndef HGA_EXP_SH_LOADONLY
+#define HGA_EXP_SH_LOADONLY 0
+#endif
+#ifndef HGA_EXP_SH_NOROWS
+#define HGA_EXP_SH_NOROWS 0
+#endif
+#ifndef HGA_EXP_SH_NODIV
+#define HGA_EXP_SH_NODIV 0
+#endif
+#ifndef HGA_EXP_SH_NOLDS
+#define HGA_EXP_SH_NOLDS 0
+#endif
+#ifndef HGA_EXP_SH_NOFLUSH
+#define HGA_EXP_SH_NOFLUSH 0
+#endif
+#ifndef HGA_EXP_NOEMIT
+#define HGA_EXP_NOEMIT 0
+#endif
+
 namespace hga {
 namespace {
 
@@ -36,7 +87,7 @@ constexpr int P_B = 16;       // window ends per thread
 constexpr int TP_B = NT_B * P_B;       // 8192 window ends per tile
 constexpr uint64_t ST_ALIGN = TP_B;    // super-tiles are whole tiles
 #ifndef HGA_MAX_FB
-#define HGA_MAX_FB 13
+#define HGA_MAX_FB 12
 #endif
 #ifndef HGA_NT_C
 #define HGA_NT_C 1024
@@ -129,8 +180,14 @@ struct BinFile {
     uint32_t w0, pad;
 };
 
+#ifndef HGA_B1_PER_CU
+#define HGA_B1_PER_CU 2   // bin1 super-tiles per CU
+#endif
+#ifndef HGA_B1_WAVES
+#define HGA_B1_WAVES 1
+#endif
 template <class E1>
-__global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk_all,
+__global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __restrict__ pk_all,
                                                 const uint16_t* __restrict__ vd_all,
                                                 const BinFile* __restrict__ files, uint32_t F,
                                                 uint64_t st_pos, KP kp,
@@ -187,12 +244,27 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk_
             dd[j] = region_of(h, kp);
             ee[j] = (E1)(h & kp.r1mask);
             rk[j] = 0;
+#if HGA_EXP_B1_COMPUTEONLY
+            rk[j] = (uint32_t)ee[j] ^ dd[j];
+#else
             if ((wm >> j) & 1u) {
                 rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
+#if !HGA_EXP_B1_NOFHIST
                 atomicAdd(&fhist[bucket_of(h, kp)], 1u);
+#endif
             }
+#endif
         }
         inst += __popc(wm);
+#if HGA_EXP_B1_COMPUTEONLY
+        {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < P_B; ++j) acc += rk[j];
+            if (acc == 0x12345678u) out1[0] = 0;
+            continue;
+        }
+#endif
         lds_barrier();
         if (tid < 64) {   // one wave: scan the <= 64 region counts, place them in the blocks
             const uint32_t c = tid < (int)nb1 ? cnt1[tid] : 0u;
@@ -229,7 +301,11 @@ __global__ void __launch_bounds__(NT_B) kc_bin1(const uint32_t* __restrict__ pk_
             const unsigned long long ba = base_a[d], bb = base_b[d];
             for (uint32_t jj = (uint32_t)(tid & 63); jj < len; jj += 64) {
                 const unsigned long long g = jj < ta ? ba + jj : bb + (jj - ta);
+#if HGA_EXP_B1_NOFLUSH
+                if (g < pool_cap && stage[o + jj] == (E1)0x12345677u) out1[g] = 0;
+#else
                 if (g < pool_cap) out1[g] = stage[o + jj];
+#endif
             }
         }
         lds_barrier();
@@ -478,36 +554,6 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 constexpr uint32_t QN_C = 128;   // miss-queue entries per wave
 #ifndef HGA_CNT_BRANCHLESS
 #define HGA_CNT_BRANCHLESS 0
-#endif
-#ifndef HGA_EXP_LOADONLY
-#define HGA_EXP_LOADONLY 0
-#endif
-#ifndef HGA_EXP_NOADD
-#define HGA_EXP_NOADD 0
-#endif
-#ifndef HGA_EXP_NOMISS
-#define HGA_EXP_NOMISS 0
-#endif
-#ifndef HGA_EXP_NOCLAIM
-#define HGA_EXP_NOCLAIM 0
-#endif
-#ifndef HGA_EXP_SH_LOADONLY
-#define HGA_EXP_SH_LOADONLY 0
-#endif
-#ifndef HGA_EXP_SH_NOROWS
-#define HGA_EXP_SH_NOROWS 0
-#endif
-#ifndef HGA_EXP_SH_NODIV
-#define HGA_EXP_SH_NODIV 0
-#endif
-#ifndef HGA_EXP_SH_NOLDS
-#define HGA_EXP_SH_NOLDS 0
-#endif
-#ifndef HGA_EXP_SH_NOFLUSH
-#define HGA_EXP_SH_NOFLUSH 0
-#endif
-#ifndef HGA_EXP_NOEMIT
-#define HGA_EXP_NOEMIT 0
 #endif
 #ifndef HGA_EMIT_STAGE
 #define HGA_EMIT_STAGE 1
@@ -810,6 +856,9 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 // keys whose home group is full (or that lost a claim race) go through the per-wave queue.
 // 64 KB per workgroup: two workgroups per CU, one's prologue / emit overlaps the other's stream.
 // Buckets this kernel cannot take (a per-file run >= 65536) are listed for kc_count.
+#ifndef HGA_COUNT_SOA
+#define HGA_COUNT_SOA 1   // kc_count_s (SoA keys/counts) rather than kc_count_p (u64 entries)
+#endif
 #ifndef HGA_NT_P
 #define HGA_NT_P 512
 #endif
@@ -821,6 +870,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 #endif
 constexpr int NT_P = HGA_NT_P;
 constexpr int PF_P = HGA_PF_P;          // binned elements per thread per batch
+static_assert(PF_P <= 15, "miss counts are scanned as 4-bit values");
 constexpr int GP_P = HGA_GP_P;          // entries per probe group (2: one ds_read_b128)
 constexpr uint32_t T_P = 8192;          // entries (64 KB)
 constexpr uint32_t G_P = T_P / GP_P;
@@ -1012,8 +1062,8 @@ __global__ void __launch_bounds__(NT_P, 4) kc_count_p(const uint32_t* __restrict
                 const uint32_t nm = (uint32_t)__popc(miss);
                 const uint64_t any = __ballot(nm != 0u);
                 if (any) {
-                    const uint32_t incl = wave_incl_scan(nm, (int)lane);
-                    const uint32_t tot = __shfl(incl, 63);
+                    uint32_t tot;
+                    const uint32_t incl = wave_excl_scan_small<4>(nm, &tot) + nm;   // nm <= PF_P = 8
                     if (qn + tot > QN_P) {   // no room: settle the queue first, then these in place
                         drain(1);
                         bool ok = true;
@@ -1116,6 +1166,309 @@ __global__ void __launch_bounds__(NT_P, 4) kc_count_p(const uint32_t* __restrict
                 } else {
                     out_cnt[base + j] = (uint32_t)(v >> 32) & 0xFFFFu;
                     out_cnt[cap + base + j] = (uint32_t)(v >> 48);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) atomicMax(&gstat[1], (unsigned long long)s_ranges);
+}
+
+// ---------------------------------------------------------------- pass C (packed, SoA)
+// Same contract as kc_count_p, with the keys and the packed counts in two u32 arrays: a probe
+// reads 4 keys with one ds_read_b128, a hit is one ds_add_u32 on the count word (32 banks
+// for the count array instead of the odd half of 64), a claim is ds_cmpst_b32 on the key then
+// the add.
+constexpr uint32_t T_S = 8192;          // slots (32 KB keys + 32 KB counts)
+constexpr uint32_t GS_S = 4;            // keys per probe group (one ds_read_b128)
+constexpr uint32_t G_S = T_S / GS_S;
+
+__device__ __forceinline__ uint4 read_keys_s(const uint32_t* tkey, uint32_t g) {
+    return reinterpret_cast<const uint4*>(tkey)[g];
+}
+__device__ __forceinline__ void match_s(const uint4 kg, uint32_t r, int& w, int& e0) {
+    const uint32_t k[4] = {kg.x, kg.y, kg.z, kg.w};
+    w = -1;
+    e0 = -1;
+#pragma unroll
+    for (int t = 3; t >= 0; --t) {
+        w = k[t] == r ? t : w;
+        e0 = k[t] == 0xFFFFFFFFu ? t : e0;
+    }
+}
+
+// Settle key r (+inc) from its home group; false if MAXPROBE_P groups were full.
+__device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t r, uint32_t inc) {
+    uint32_t g = r & (G_S - 1);
+    for (uint32_t steps = 0; steps < MAXPROBE_P;) {
+        int w, e0;
+        match_s(read_keys_s(tkey, g), r, w, e0);
+        if (w >= 0) {
+            atomicAdd(&tcnt[g * GS_S + w], inc);
+            return true;
+        }
+        if (e0 >= 0) {
+            const uint32_t sl = g * GS_S + (uint32_t)e0;
+            const uint32_t old = atomicCAS(&tkey[sl], 0xFFFFFFFFu, r);
+            if (old == 0xFFFFFFFFu || old == r) {
+                atomicAdd(&tcnt[sl], inc);
+                return true;
+            }
+            continue;   // lost the slot to another key: re-read the same group
+        }
+        g = (g + 1) & (G_S - 1);
+        ++steps;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(NT_P, 4) kc_count_s(const uint32_t* __restrict__ binned,
+                                                      const uint64_t* __restrict__ fs, uint32_t F,
+                                                      uint32_t min_count, KP kp, uint64_t* __restrict__ out_key,
+                                                      uint32_t* __restrict__ out_cnt, uint64_t cap,
+                                                      unsigned long long* __restrict__ gstat,
+                                                      uint32_t* __restrict__ blist) {
+    __shared__ __attribute__((aligned(16))) uint32_t tkey[T_S];
+    __shared__ __attribute__((aligned(16))) uint32_t tcnt[T_S];
+    __shared__ uint32_t qbuf[NT_P / 64][QN_P];
+    __shared__ uint32_t s_ovf, s_sp, s_ranges;
+    __shared__ uint32_t stk_lo[40], stk_hi[40];
+    __shared__ uint32_t ws[NT_P / 64 + 1];
+    __shared__ unsigned long long s_base;
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    uint32_t* myq = qbuf[tid >> 6];
+    const uint32_t b = blockIdx.x;
+    const uint64_t* f = fs + (uint64_t)b * (F + 1);
+    for (uint32_t ff = 0; ff < F; ++ff)
+        if (f[ff + 1] - f[ff] >= 65536u && F > 1) {   // a count could pass 16 bits: kc_count takes it
+            if (tid == 0) blist[atomicAdd(&gstat[5], 1ull)] = b;
+            return;
+        }
+    const uint32_t rbits = kp.rbits;
+    const uint32_t SUBB = rbits < 16 ? rbits : 16;
+    const uint32_t full_hi = 1u << SUBB;
+    const uint32_t mc = min_count ? min_count : 1u;
+    if (tid == 0) {
+        stk_lo[0] = 0;
+        stk_hi[0] = full_hi;
+        s_sp = 1;
+        s_ranges = 0;
+    }
+    __syncthreads();
+    while (true) {
+        const uint32_t sp = s_sp;
+        if (sp == 0) break;
+        const uint32_t lo = stk_lo[sp - 1], hi = stk_hi[sp - 1];
+        __syncthreads();
+        if (tid == 0) {
+            s_sp = sp - 1;
+            s_ovf = 0;
+        }
+        for (uint32_t i = tid; i < T_S; i += NT_P) {
+            tkey[i] = 0xFFFFFFFFu;
+            tcnt[i] = 0;
+        }
+        __syncthreads();
+        const bool filt = !(lo == 0 && hi == full_hi);
+        uint32_t qn = 0;   // this wave's queued keys (uniform)
+        for (uint32_t ff = 0; ff < F; ++ff) {
+            const uint64_t a = f[ff], e = f[ff + 1];
+            const uint32_t inc = F == 1 ? 1u : (1u << (16 * ff));
+            constexpr uint64_t STEP = (uint64_t)NT_P * PF_P;
+            if (a == e) continue;
+            const uint64_t nfull = (e - a) / STEP;
+            uint32_t nx[PF_P];
+            auto load = [&](uint64_t i0, uint64_t bi) {
+                if (bi < nfull) {
+                    const uint32_t* __restrict__ bp = binned + i0;
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) nx[q] = bp[q * NT_P + tid];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) {
+                        const uint64_t i = i0 + (uint64_t)q * NT_P + tid;
+                        nx[q] = i < e ? binned[i] : 0xFFFFFFFFu;
+                    }
+                }
+            };
+            auto drain = [&](uint32_t min_take) {   // while at least min_take (>= 1) are queued
+                while (qn >= min_take && qn > 0) {
+                    const uint32_t take = qn < 64 ? qn : 64;
+                    const uint32_t q0 = qn - take;
+                    bool ok = true;
+                    if (lane < take) ok = probe_s(tkey, tcnt, myq[q0 + lane], inc);
+                    if (!ok) s_ovf = 1u;
+                    qn = q0;
+                    wave_lds_sync();
+                }
+            };
+            load(a, 0);
+            uint64_t bi = 0;
+            for (uint64_t i0 = a; i0 < e; i0 += STEP, ++bi) {
+                uint32_t rv[PF_P];
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q) rv[q] = nx[q];
+                if (i0 + STEP < e) load(i0 + STEP, bi + 1);
+                if (filt) {
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) {
+                        const uint32_t sk = SUBB ? rv[q] >> (rbits - SUBB) : 0u;
+                        rv[q] = (sk >= lo && sk < hi) ? rv[q] : 0xFFFFFFFFu;
+                    }
+                }
+                uint4 kg[PF_P];
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q) kg[q] = read_keys_s(tkey, rv[q] & (G_S - 1));
+                uint32_t claim = 0, miss = 0, slot[PF_P];
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q) {
+                    int w, e0;
+                    match_s(kg[q], rv[q], w, e0);
+                    const bool live = rv[q] != 0xFFFFFFFFu;
+                    slot[q] = (rv[q] & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
+#if HGA_EXP_S_HITSTORE
+                    if (live && w >= 0) tcnt[slot[q]] = inc;
+#elif HGA_EXP_S_NOHIT
+                    if (live && w >= 0 && rv[q] == 0x1234567u) tcnt[slot[q]] = inc;
+#else
+                    if (live && w >= 0) atomicAdd(&tcnt[slot[q]], inc);
+#endif
+                    else if (live && e0 >= 0) claim |= 1u << q;
+                    else if (live) miss |= 1u << q;
+                }
+#if HGA_S_NEXT
+                // home group full without the key: the next group, inline (one displacement
+                // step covers most displaced keys, which would otherwise queue on every occurrence)
+                if (__ballot(miss != 0u)) {
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q)
+                        if ((miss >> q) & 1u) kg[q] = read_keys_s(tkey, (rv[q] + 1) & (G_S - 1));
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q)
+                        if ((miss >> q) & 1u) {
+                            int w, e0;
+                            match_s(kg[q], rv[q], w, e0);
+                            slot[q] = ((rv[q] + 1) & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
+                            if (w >= 0) {
+                                atomicAdd(&tcnt[slot[q]], inc);
+                                miss &= ~(1u << q);
+                            } else if (e0 >= 0) {
+                                claim |= 1u << q;
+                                miss &= ~(1u << q);
+                            }
+                        }
+                }
+#endif
+#pragma unroll
+                for (int q = 0; q < PF_P; ++q)
+                    if ((claim >> q) & 1u) {
+                        const uint32_t old = atomicCAS(&tkey[slot[q]], 0xFFFFFFFFu, rv[q]);
+                        if (old == 0xFFFFFFFFu || old == rv[q]) atomicAdd(&tcnt[slot[q]], inc);
+                        else miss |= 1u << q;
+                    }
+                const uint32_t nm = (uint32_t)__popc(miss);
+                const uint64_t any = __ballot(nm != 0u);
+                if (any) {
+                    uint32_t tot;
+                    const uint32_t incl = wave_excl_scan_small<4>(nm, &tot) + nm;   // nm <= PF_P = 8
+                    if (qn + tot > QN_P) {   // no room: settle the queue first, then these in place
+                        drain(1);
+                        bool ok = true;
+                        while (__any(miss != 0u)) {
+                            if (miss) {
+                                const int q = __builtin_ctz(miss);
+                                miss &= miss - 1u;
+                                uint32_t pick = rv[0];
+#pragma unroll
+                                for (int t = 1; t < PF_P; ++t) pick = q == t ? rv[t] : pick;
+                                ok = probe_s(tkey, tcnt, pick, inc) && ok;
+                            }
+                        }
+                        if (!ok) s_ovf = 1u;
+                    } else {
+                        uint32_t pos = qn + incl - nm;
+#pragma unroll
+                        for (int q = 0; q < PF_P; ++q)   // predicated stores, no per-lane loop
+                            if ((miss >> q) & 1u) myq[pos++] = rv[q];
+                        qn += tot;
+                        wave_lds_sync();
+                        drain(64);
+                    }
+                }
+                if ((i0 - a) % (4 * STEP) == 0 && __atomic_load_n(&s_ovf, __ATOMIC_RELAXED)) break;
+            }
+            drain(1);
+        }
+        __syncthreads();
+        if (s_ovf) {
+            __syncthreads();
+            if (tid == 0) {
+                if (hi - lo <= 1 || s_sp + 2 > 40) {
+                    atomicOr(&gstat[2], 1ull);
+                    s_sp = 0;
+                } else {
+                    const uint32_t mid = lo + (hi - lo) / 2;
+                    stk_lo[s_sp] = mid; stk_hi[s_sp] = hi;
+                    stk_lo[s_sp + 1] = lo; stk_hi[s_sp + 1] = mid;
+                    s_sp += 2;
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        // emit: each thread owns ES consecutive slots; kept rows are compacted in place
+        constexpr int ES = T_S / NT_P;
+        uint32_t kk[ES], cc[ES];
+#pragma unroll
+        for (int j = 0; j < ES; j += 4) {
+            const uint4 k4 = reinterpret_cast<const uint4*>(tkey)[(tid * ES + j) / 4];
+            const uint4 c4 = reinterpret_cast<const uint4*>(tcnt)[(tid * ES + j) / 4];
+            kk[j] = k4.x; kk[j + 1] = k4.y; kk[j + 2] = k4.z; kk[j + 3] = k4.w;
+            cc[j] = c4.x; cc[j + 1] = c4.y; cc[j + 2] = c4.z; cc[j + 3] = c4.w;
+        }
+        uint32_t keep = 0;
+#pragma unroll
+        for (int j = 0; j < ES; ++j) {
+            uint32_t c = cc[j];
+            if (F == 1) {
+                c = c >= mc ? c : 0u;
+            } else {
+                const uint32_t c0 = c & 0xFFFFu, c1 = c >> 16;
+                c = (c0 >= mc ? c0 : 0u) | ((c1 >= mc ? c1 : 0u) << 16);
+            }
+            cc[j] = c;
+            if (kk[j] != 0xFFFFFFFFu && c) keep |= 1u << j;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<NT_P>((uint32_t)__popc(keep), ws, &tot);
+        if (tid == 0) {
+            s_base = tot ? atomicAdd(&gstat[0], (unsigned long long)tot) : 0ull;
+            ++s_ranges;
+        }
+        __syncthreads();   // every slot read: the table becomes the staging area
+        uint32_t o = ex;
+#pragma unroll
+        for (int j = 0; j < ES; ++j)
+            if ((keep >> j) & 1u) {
+                tkey[o] = kk[j];
+                tcnt[o] = cc[j];
+                ++o;
+            }
+        __syncthreads();
+        const uint64_t base = s_base;
+        if (base + tot > cap) {
+            if (tid == 0 && tot) atomicOr(&gstat[2], 2ull);
+        } else {
+            const uint64_t hb = kp.fb ? ((uint64_t)b << rbits) : 0ull;
+            for (uint32_t j = tid; j < tot; j += NT_P) {
+                const uint32_t c = tcnt[j];
+                out_key[base + j] = mix_inv(hb | tkey[j], kp.mix);
+                if (F == 1) {
+                    out_cnt[base + j] = c;
+                } else {
+                    out_cnt[base + j] = c & 0xFFFFu;
+                    out_cnt[cap + base + j] = c >> 16;
                 }
             }
         }
@@ -1416,7 +1769,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
 
     // super-tiles: ~2 per CU over all files (one resident wave of bin1 workgroups, so each
     // (workgroup, region) fills about one level-1 block), whole tiles
-    uint64_t st_pos = total_bytes / ((uint64_t)c->num_cu * 2) + 1;
+    uint64_t st_pos = total_bytes / ((uint64_t)c->num_cu * HGA_B1_PER_CU) + 1;
     st_pos = std::max<uint64_t>(ST_ALIGN, (st_pos + ST_ALIGN - 1) / ST_ALIGN * ST_ALIGN);
     std::vector<uint32_t> n_st(F, 0);
     std::vector<BinFile> bf(F);
@@ -1523,8 +1876,9 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     if (packed && e32) {
         uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nb * 4));
         c->launch("kc_count", [&] {
-            hipLaunchKernelGGL(kc_count_p, dim3(nb), dim3(NT_P), 0, c->stream, static_cast<const uint32_t*>(binned), fs, F,
-                               min_per_file, kp, s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, blist);
+            hipLaunchKernelGGL(HGA_COUNT_SOA ? kc_count_s : kc_count_p, dim3(nb), dim3(NT_P), 0, c->stream,
+                               static_cast<const uint32_t*>(binned), fs, F, min_per_file, kp, s.rows_key.as<uint64_t>(),
+                               s.rows_cnt.as<uint32_t>(), cap, gstat, blist);
             // buckets with a per-file run >= 65536 (listed in blist, count in gstat[5])
             hipLaunchKernelGGL(kc_count<uint32_t>, dim3(std::min<uint32_t>(nb, (uint32_t)c->num_cu)), dim3(NT_C), 0,
                                c->stream, static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,

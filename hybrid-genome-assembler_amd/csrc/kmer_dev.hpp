@@ -245,6 +245,21 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
     return v;
 }
 
+// Wave-wide exclusive scan of small values (v < 2^B) through ballots of the bit planes:
+// no LDS-pipe traffic (a shuffle scan issues ds_bpermute).  *total = the wave sum.
+template <int B>
+__device__ __forceinline__ uint32_t wave_excl_scan_small(uint32_t v, uint32_t* total) {
+    uint32_t ex = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t m = __ballot((v >> b) & 1u);
+        ex += (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+        tot += (uint32_t)__popcll(m) << b;
+    }
+    *total = tot;
+    return ex;
+}
+
 // Block-wide exclusive scan of one value per thread; NT threads (multiple of 64,
 // <= 1024).  `ws` is LDS scratch of >= NT/64 + 1 words.  Returns the exclusive
 // prefix; *total receives the block sum.  Contains __syncthreads().
