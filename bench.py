@@ -60,9 +60,12 @@ def make_c3(ga, gb, rank):
     return bases, offsets
 
 
+PMC_KERNEL = {"kc_count": "kc_count_s"}   # profiler label -> device kernel of the default build
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch measured by a separate rocprofv3 --pmc pass (profiles/), if any."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
+    p = os.path.join(ROOT, "profiles", f"pmc_{PMC_KERNEL.get(kernel, kernel)}.json")
     if os.path.exists(p):
         try:
             return json.load(open(p)).get("hbm_bytes_per_launch")
