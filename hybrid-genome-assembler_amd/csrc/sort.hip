@@ -18,7 +18,10 @@ namespace hga {
 namespace {
 
 constexpr int RS_T = 256;              // threads per tile
-constexpr int RS_I = 16;               // items per thread
+#ifndef HGA_RS_I
+#define HGA_RS_I 16
+#endif
+constexpr int RS_I = HGA_RS_I;         // items per thread
 constexpr int RS_TILE = RS_T * RS_I;   // 4096 keys per tile
 constexpr int SC_T = 1024, SC_I = 4, SC_TILE = SC_T * SC_I;
 #ifndef HGA_EXP_RS_NOLB
@@ -76,7 +79,7 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
     uint32_t rank[RS_I];
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
-        const uint64_t i = base + (uint64_t)wave * 1024 + (uint64_t)j * 64 + lane;
+        const uint64_t i = base + (uint64_t)wave * (RS_I * 64) + (uint64_t)j * 64 + lane;
         const bool ok = i < n;
         key[j] = ok ? kin[i] : K(0);
         if (HAS_V) val[j] = ok ? vin[i] : 0u;
@@ -189,7 +192,7 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
     uint32_t rank[RS_I];
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
-        const uint64_t i = base + (uint64_t)wave * 1024 + (uint64_t)j * 64 + lane;
+        const uint64_t i = base + (uint64_t)wave * (RS_I * 64) + (uint64_t)j * 64 + lane;
         const bool ok = i < n;
         key[j] = ok ? kin[i] : K(0);
         if (HAS_V) val[j] = ok ? vin[i] : 0u;

@@ -81,3 +81,18 @@ def test_jf_occurrences_without_k(tmp_path, hga_mod):
     assert out.stdout == ("\n".join(lines) + "\n0\nEnter lower and upper bounds for exported kmers as well as "
                           f"percentage\n{o['n_discr']} out of {len(o['selected'])} exported kmers are discriminative")
     assert os.path.exists(tmp_path / f"{k}-mers_2_40_100%.txt")
+
+
+@pytest.mark.parametrize("k", [11, 15, 19, 23, 27, 31])
+def test_hll_registers_vs_reference_code(gpu_ctx, k):
+    """GPU registers against the reference's own hll::HyperLogLog (oracle/_ref, tests/test_ref_pin.py)."""
+    import refimpl
+    if not refimpl.available():
+        pytest.skip("oracle/_ref/libref_hll.so not built")
+    bases, offsets = case(1000 + k, 300, 400, "ACGTACGTACGTNacg\r")
+    gpu_ctx.lookup_set_reads(bases, offsets, 1)
+    codes = [oracle.kmer_windows(bases[int(a):int(b)], k)[0] for a, b in zip(offsets[:-1], offsets[1:])]
+    regs_ref, est_ref = refimpl.hll(np.concatenate(codes), 10)
+    regs = gpu_ctx.hll_registers(k, 10)
+    assert np.array_equal(regs, regs_ref)
+    assert oracle.hll_estimate(regs, 10) == est_ref

@@ -13,14 +13,22 @@ sys.path[:0] = [%r, %r]
 import bench, hga
 ga, gb, ra, rb = bench.make_c2(0)
 ctx = hga.Ctx(0); ctx.count_begin(19, 2); ctx.count_add(0, ra.seq); ctx.count_add(1, rb.seq)
-for _ in range(2): bench.count_step(ctx)
+def step():
+    try:
+        return bench.count_step(ctx)
+    except hga.HgaError as e:   # timing-experiment builds (HGA_EXP_*) produce wrong data on purpose
+        return str(e)[:60]
+for _ in range(2): step()
 ctx.profile(True); ctx.profile_reset()
 import time; ctx.sync(); t0 = time.perf_counter()
-for _ in range(10): n = bench.count_step(ctx)
+for _ in range(10): n = step()
 ctx.sync(); dt = (time.perf_counter() - t0) / 10
 names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select")
-h = ctx.spec_hist(bench.THRESHOLDS)
-print(json.dumps({"ms": round(dt * 1e3, 3), "sel": n, "hist_sum": int(h[:, 2].sum()),
+try:
+    hs = int(ctx.spec_hist(bench.THRESHOLDS)[:, 2].sum())
+except hga.HgaError:
+    hs = None
+print(json.dumps({"ms": round(dt * 1e3, 3), "sel": n, "hist_sum": hs,
                   "k": {x: round(ctx.profile_get(x)[0] / 10, 4) for x in names}}))
 ''' % (ROOT, os.path.join(ROOT, "hybrid-genome-assembler_amd"))
 
