@@ -342,7 +342,7 @@ def main():
     stats = {"bytes": st.bytes, "instances": st.instances, "rows": st.distinct_rows, "files": 2}
     # 1) untimed profiled pass: per-kernel breakdown (events around every launch)
     names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
-             "kx_partition", "kx_merge", "radix_upsweep", "radix_downsweep", "scan")
+             "kx_partition", "kx_merge", "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
     ctx.profile(True)
     ctx.profile_reset()
     for _ in range(args.steps):

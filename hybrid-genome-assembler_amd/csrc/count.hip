@@ -1603,17 +1603,21 @@ __global__ void __launch_bounds__(NT_HC) kc_hist_compact(unsigned long long* __r
     }
 }
 
+static_assert(NT_H == 256, "kc_select: one top-digit bin per thread");
 constexpr int SEL_R = 16;   // rows per thread: one cursor atomic (and one count atomic) per 4096 rows
 __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ keys,
                                                   const uint32_t* __restrict__ cnt, uint64_t rows,
                                                   uint64_t cap, uint32_t F, int64_t lower,
                                                   int64_t upper, uint64_t* __restrict__ out,
                                                   uint32_t* __restrict__ out_flag, bool flag_bit,
-                                                  unsigned long long* __restrict__ stat) {
+                                                  unsigned long long* __restrict__ stat,
+                                                  uint32_t* __restrict__ dhist_rows, int dshift) {
     __shared__ uint32_t ws[NT_H / 64 + 1];
     __shared__ unsigned long long s_base;
     __shared__ uint64_t stage[NT_H * SEL_R];
     __shared__ uint8_t sflag[NT_H * SEL_R];
+    __shared__ uint32_t dh[256];   // top-digit histogram of the kept keys (the export sort's MSD pass)
+    dh[threadIdx.x] = 0;
     const uint64_t base = (uint64_t)blockIdx.x * NT_H * SEL_R;
     uint64_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
 #pragma unroll
@@ -1660,9 +1664,23 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
     __syncthreads();
     const uint64_t ob = s_base;
     for (uint32_t j = threadIdx.x; j < tot; j += NT_H) {
-        out[ob + j] = stage[j];
+        const uint64_t v = stage[j];
+        out[ob + j] = v;
         if (!flag_bit) out_flag[ob + j] = sflag[j];
+        if (dhist_rows) atomicAdd(&dh[(uint32_t)(v >> dshift) & 255u], 1u);
     }
+    if (dhist_rows) {
+        __syncthreads();
+        dhist_rows[(uint64_t)blockIdx.x * 256 + threadIdx.x] = dh[threadIdx.x];
+    }
+}
+
+// hist[d] = sum over kc_select workgroups of their top-digit counts (rows x 256, row-major).
+__global__ void __launch_bounds__(256) kc_dhist_reduce(const uint32_t* __restrict__ rows, uint32_t n_rows,
+                                                       uint32_t* __restrict__ hist) {
+    uint32_t s = 0;
+    for (uint32_t r = blockIdx.x; r < n_rows; r += gridDim.x) s += rows[(uint64_t)r * 256 + threadIdx.x];
+    if (s) atomicAdd(&hist[threadIdx.x], s);
 }
 
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
@@ -2019,7 +2037,10 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     HGA_REQUIRE(!(hc[1] & 1ull), HGA_ERR_INVALID, "a row's specificity is above the last threshold");
     HGA_REQUIRE(!(hc[1] & 2ull), HGA_ERR_OOM, "histogram overflow list full");
     HGA_REQUIRE(hc[2] <= ncap, HGA_ERR_OOM, "histogram compaction buffer full");
-    std::map<std::pair<uint32_t, uint64_t>, uint64_t> bins;
+    // (threshold << 56 | total, count) pairs: the dense bins are unique, overflow rows add 1 each;
+    // sorted by the packed key = std::map<double, std::map<int, int>> order (threshold, then total)
+    std::vector<std::pair<uint64_t, uint64_t>> bins;
+    bins.reserve(hc[2] + std::min<uint64_t>(hc[0], over_cap));
     if (hc[2]) {
         const unsigned long long* cv = hcomp;
         std::vector<unsigned long long> rest;
@@ -2028,19 +2049,23 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
             HGA_HIP(hipMemcpy(rest.data(), comp, hc[2] * 16, hipMemcpyDeviceToHost));
             cv = rest.data();
         }
-        for (uint64_t i = 0; i < hc[2]; ++i)
-            bins[{(uint32_t)(cv[2 * i] >> 56), cv[2 * i] & ((1ull << 56) - 1)}] += cv[2 * i + 1];
+        for (uint64_t i = 0; i < hc[2]; ++i) bins.emplace_back(cv[2 * i], cv[2 * i + 1]);
     }
     if (hc[0]) {
         std::vector<unsigned long long> ov(std::min<uint64_t>(hc[0], over_cap));
         HGA_HIP(hipMemcpy(ov.data(), over, ov.size() * 8, hipMemcpyDeviceToHost));
-        for (auto v : ov) bins[{(uint32_t)(v >> 56), v & ((1ull << 56) - 1)}] += 1;
+        for (auto v : ov) bins.emplace_back(v, 1ull);
     }
+    std::sort(bins.begin(), bins.end());
     out.clear();
-    for (auto& kv : bins) {   // std::map order: threshold, then total
-        out.push_back(kv.first.first);
-        out.push_back((int64_t)kv.first.second);
-        out.push_back((int64_t)kv.second);
+    out.reserve(3 * bins.size());
+    for (size_t i = 0; i < bins.size();) {
+        const uint64_t key = bins[i].first;
+        uint64_t cnt = 0;
+        for (; i < bins.size() && bins[i].first == key; ++i) cnt += bins[i].second;
+        out.push_back((int64_t)(key >> 56));
+        out.push_back((int64_t)(key & ((1ull << 56) - 1)));
+        out.push_back((int64_t)cnt);
     }
 }
 
@@ -2051,23 +2076,39 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     char* sb = static_cast<char*>(s.sel_keys.ensure(cap * 12 + 256));
     uint64_t* out = reinterpret_cast<uint64_t*>(sb);
     uint32_t* flag = reinterpret_cast<uint32_t*>(sb + cap * 8);
-    auto* stat = static_cast<unsigned long long*>(s.sel_tmp.ensure(64));
     const bool flag_bit = s.k <= 31;   // the discriminative flag rides in key bit 63
-    HGA_HIP(hipMemsetAsync(stat, 0, 16, c->stream));
+    const int bits = 2 * s.k;
+    // export sort: one MSD pass on the top 8 bits + per-segment LDS sorts (sort_export_u64) when
+    // the flag rides in the key; the top-digit histogram comes out of kc_select
+    const bool msd = flag_bit && bits >= 16 && s.rows >= (1u << 15);
+    const unsigned grid = (unsigned)blocks_for(std::max<uint64_t>(s.rows, 1), NT_H * SEL_R);
+    auto* stat = static_cast<unsigned long long*>(s.sel_tmp.ensure(64 + 1024 + (msd ? (size_t)grid * 1024 : 0)));
+    uint32_t* dhist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(stat) + 64);
+    uint32_t* dhist_rows = msd ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(stat) + 64 + 1024) : nullptr;
+    HGA_HIP(hipMemsetAsync(stat, 0, 64 + 1024, c->stream));
     if (s.rows) {
         c->launch("kc_select", [&] {
-            hipLaunchKernelGGL(kc_select, dim3(blocks_for(s.rows, NT_H * SEL_R)), dim3(NT_H), 0, c->stream,
-                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), s.rows,
-                               s.rows_cap, s.n_files, lower, upper, out, flag, flag_bit, stat);
+            hipLaunchKernelGGL(kc_select, dim3(grid), dim3(NT_H), 0, c->stream, s.rows_key.as<uint64_t>(),
+                               s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, lower, upper, out, flag,
+                               flag_bit, stat, dhist_rows, bits - 8);
+            if (msd)
+                hipLaunchKernelGGL(kc_dhist_reduce, dim3(std::min<unsigned>(grid, 64)), dim3(256), 0, c->stream,
+                                   dhist_rows, grid, dhist);
         });
         c->check_launch("kc_select");
     }
-    unsigned long long hs[2];
-    HGA_HIP(hipMemcpyAsync(hs, stat, 16, hipMemcpyDeviceToHost, c->stream));
+    // one synchronisation: counts and the top-digit histogram together (pinned staging)
+    auto* hs = static_cast<unsigned long long*>(c->pinned_sel.ensure(64 + 1024));
+    HGA_HIP(hipMemcpyAsync(hs, stat, 64 + 1024, hipMemcpyDeviceToHost, c->stream));
     c->sync();
-    radix_sort_u64(c, out, flag_bit ? nullptr : flag, hs[0], 2 * s.k, s.scratch);
-    s.n_sel = hs[0];
-    *n_out = hs[0];
+    const uint64_t n = hs[0];
+    if (msd && n > 1)
+        sort_export_u64(c, out, n, bits, dhist, reinterpret_cast<const uint32_t*>(reinterpret_cast<char*>(hs) + 64),
+                        s.scratch);
+    else
+        radix_sort_u64(c, out, flag_bit ? nullptr : flag, n, bits, s.scratch);
+    s.n_sel = n;
+    *n_out = n;
     *n_discr = hs[1];
 }
 

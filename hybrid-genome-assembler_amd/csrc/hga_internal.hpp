@@ -172,6 +172,7 @@ struct hga_ctx {
     hga::LookupState lookup;
     hga::ConnState conn;
     hga::PinnedBuf pinned;   // small host<->device staging (see count_spec_hist)
+    hga::PinnedBuf pinned_sel;   // count_select counters + top-digit histogram
 
     // Launch helper: records events around the launch when profiling is on.
     template <class F>
@@ -232,4 +233,6 @@ void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int 
                     DevBuf& scratch);
 // exclusive scan of u64 in place (sort.hip)
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
+void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int bits, const uint32_t* d_hist,
+                     const uint32_t* h_hist, DevBuf& scratch);
 }  // namespace hga

@@ -285,6 +285,104 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
     }
 }
 
+// ---- export sort: one MSD digit pass, then every digit's segment sorted in LDS --------------
+// The exported k-mers (count_select) are ~10^6-10^7 keys of 2k <= 62 bits: one onesweep pass on
+// the top 8 bits of the sort width scatters them into 256 segments, each of which one workgroup
+// sorts in LDS by the remaining bits (stable LSD passes over 8-bit digits: ballot-matched ranks
+// inside each wave, waves in order), instead of ceil(2k/8) global passes.  Segments larger than
+// the LDS (rare: a prefix holding > 16384 keys) are sorted by the global radix sort.
+constexpr int SS_T = 1024, SS_I = 16, SS_CAP = SS_T * SS_I;
+
+__global__ void __launch_bounds__(SS_T) ss_segsort(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
+                                                   const uint32_t* __restrict__ ghist, int bits_low) {
+    __shared__ uint64_t sk[SS_CAP];
+    __shared__ uint32_t wcnt[SS_T / 64][256];
+    __shared__ uint32_t ws[SS_T / 64 + 1];
+    __shared__ uint32_t s_start, s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t seg = blockIdx.x;
+    {   // this segment's start: exclusive prefix of the digit totals
+        uint32_t tot;
+        const uint32_t h = tid < 256 ? ghist[tid] : 0u;
+        const uint32_t ex = block_excl_scan<SS_T>(h, ws, &tot);
+        if (tid == (int)seg) {
+            s_start = ex;
+            s_cnt = h;
+        }
+        __syncthreads();
+    }
+    const uint32_t start = s_start, cnt = s_cnt;
+    if (cnt == 0 || cnt > (uint32_t)SS_CAP) return;   // empty, or left to the global fallback
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t key[SS_I];
+#pragma unroll
+    for (int j = 0; j < SS_I; ++j) {
+        const uint32_t i = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64 + lane;
+        key[j] = i < cnt ? kin[(uint64_t)start + i] : 0ull;
+    }
+    for (int sh = 0; sh < bits_low; sh += 8) {
+        const uint32_t dm = bits_low - sh >= 8 ? 255u : ((1u << (bits_low - sh)) - 1u);
+        for (int i = tid; i < (SS_T / 64) * 256; i += SS_T) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t dig[SS_I], rank[SS_I];
+#pragma unroll
+        for (int j = 0; j < SS_I; ++j) {   // stable rank inside the wave, items in (j, lane) order
+            const uint32_t i0 = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64;   // wave-uniform
+            const uint32_t i = i0 + lane;
+            const bool ok = i < cnt;
+            const uint32_t d = ok ? ((uint32_t)(key[j] >> sh) & dm) : 256u;
+            dig[j] = d;
+            rank[j] = 0;
+            if (i0 >= cnt) continue;   // no item of this row: skip its ballots
+            uint64_t m = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            uint32_t before = 0;
+            if (ok) before = wcnt[wave][d];
+            rank[j] = before + (uint32_t)__popcll(m & lt);
+            if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
+            wave_lds_sync();
+        }
+        __syncthreads();
+        {   // digit starts, then each wave's start inside its digit (waves in order: stable)
+            const uint32_t d = (uint32_t)tid & 255u;
+            uint32_t tot_d = 0;
+            if (tid < 256)
+                for (int w = 0; w < SS_T / 64; ++w) tot_d += wcnt[w][d];
+            uint32_t tt;
+            const uint32_t exd = block_excl_scan<SS_T>(tid < 256 ? tot_d : 0u, ws, &tt);
+            if (tid < 256) {
+                uint32_t o = exd;
+                for (int w = 0; w < SS_T / 64; ++w) {
+                    const uint32_t c = wcnt[w][d];
+                    wcnt[w][d] = o;
+                    o += c;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SS_I; ++j)
+            if (dig[j] < 256u) sk[wcnt[wave][dig[j]] + rank[j]] = key[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SS_I; ++j) {
+            const uint32_t i = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64 + lane;
+            if (i < cnt) key[j] = sk[i];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < SS_I; ++j) {
+        const uint32_t i = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64 + lane;
+        if (i < cnt) kout[(uint64_t)start + i] = key[j];
+    }
+}
+
 // ---- exclusive scans --------------------------------------------------------------
 template <class T>
 __global__ void __launch_bounds__(SC_T) sc_reduce(const T* __restrict__ in, uint64_t n,
@@ -480,6 +578,40 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
 void radix_sort_u64(hga_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n, int bits,
                     DevBuf& scratch) {
     radix_sort_impl<uint64_t>(c, keys, vals, n, bits, scratch);
+}
+// keys: n keys whose sort width is `bits` (16..62; bits above it are payload), d_hist / h_hist: the
+// device / host copies of the 256 counts of the top digit (bits-8 .. bits-1).  Sorted in place.
+void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int bits, const uint32_t* d_hist,
+                     const uint32_t* h_hist, DevBuf& scratch) {
+    if (n <= 1) return;
+    HGA_REQUIRE(bits >= 16 && bits <= 62 && n < (1ull << 32), HGA_ERR_INVALID, "export sort: bad width");
+    const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    const size_t kb = ((n * 8 + 255) & ~255ull), stb = (size_t)n_tiles * 256 * 4, tcb = 64;
+    char* base = static_cast<char*>(scratch.ensure(kb + stb + tcb));
+    uint64_t* k2 = reinterpret_cast<uint64_t*>(base);
+    uint32_t* status = reinterpret_cast<uint32_t*>(base + kb);
+    uint32_t* tctr = reinterpret_cast<uint32_t*>(base + kb + stb);
+    HGA_HIP(hipMemsetAsync(status, 0, stb + tcb, c->stream));
+    const int shift = bits - 8;
+    c->launch("radix_downsweep", [&] {
+        hipLaunchKernelGGL((rs_onesweep<uint64_t, false>), dim3(n_tiles), dim3(RS_T), 0, c->stream, keys,
+                           (const uint32_t*)nullptr, k2, (uint32_t*)nullptr, n, shift, 255u, d_hist, status, tctr);
+    });
+    c->check_launch("rs_onesweep");
+    c->launch("radix_segsort", [&] {
+        hipLaunchKernelGGL(ss_segsort, dim3(256), dim3(SS_T), 0, c->stream, k2, keys, d_hist, shift);
+    });
+    c->check_launch("ss_segsort");
+    uint64_t st = 0;
+    for (int d = 0; d < 256; ++d) {   // segments too large for one workgroup's LDS
+        if (h_hist[d] > (uint32_t)SS_CAP) {
+            DevBuf tmp;
+            radix_sort_u64(c, k2 + st, nullptr, h_hist[d], shift, tmp);
+            HGA_HIP(hipMemcpyAsync(keys + st, k2 + st, (size_t)h_hist[d] * 8, hipMemcpyDeviceToDevice, c->stream));
+            c->sync();   // tmp is freed on return
+        }
+        st += h_hist[d];
+    }
 }
 void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int bits,
                     DevBuf& scratch) {

@@ -1,0 +1,71 @@
+"""Export order on the MI355X: count_select's MSD sort (one onesweep pass on the top 8 bits of the
+2k-bit code, then every top-digit segment sorted in LDS; segments over 16384 keys by the global
+radix sort) against the oracle's selection (export_kmers, JellyfishOccurrenceReader.cpp:110-135:
+ascending code == LC_ALL=C order).  Sizes put s.rows above the MSD threshold (32768)."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def genome(n, alphabet, seed):
+    rng = random.Random(seed)
+    return "".join(rng.choice(alphabet) for _ in range(n)).encode()
+
+
+def reads_of(g, n, length, seed):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        s = rng.randrange(0, len(g) - length)
+        out.append(g[s:s + length])
+    return b"\n".join(out)
+
+
+def check(ctx, streams, k, lower, upper, min_count):
+    ctx.count_begin(k, len(streams))
+    for f, s in enumerate(streams):
+        ctx.count_add(f, s)
+    ctx.count_run(min_count)
+    assert ctx.count_stats().distinct_rows >= 32768
+    sel, flags, nd = ctx.select(lower, upper)
+    dumps = [oracle.count_stream(s, k, min_count, threads=8) for s in streams]
+    keys, counts = oracle.merge(dumps)
+    o_sel, o_nd = oracle.select(keys, counts, lower, upper)
+    assert np.array_equal(sel, o_sel)
+    assert nd == o_nd
+    nz = (counts > 0).sum(1)
+    idx = np.searchsorted(keys, sel)
+    assert np.array_equal(flags.astype(bool), nz[idx] == 1)
+    return len(sel)
+
+
+@pytest.mark.parametrize("k", [8, 11, 16, 19, 21, 27, 31])
+def test_export_sort_random(gpu_ctx, k):
+    ga = genome(300_000, "ACGT", k)
+    gb = bytearray(ga)
+    rng = random.Random(k + 100)
+    for i in range(0, len(gb), 50):
+        gb[i] = ord(rng.choice("ACGT"))
+    streams = [reads_of(ga, 12_000, 150, 2 * k), reads_of(bytes(gb), 12_000, 150, 2 * k + 1)]
+    n = check(gpu_ctx, streams, k, 1, 1 << 30, 1)
+    assert n >= 32768
+
+
+def test_export_sort_skewed_segments_fallback(gpu_ctx):
+    # A/C-only sequence: every canonical 19-mer starts with A/C, so only 16 of the 256 top digits
+    # are used and each holds more than 16384 keys -> the global-radix fallback per segment
+    g = genome(600_000, "AC", 7)
+    n = check(gpu_ctx, [reads_of(g, 30_000, 150, 8)], 19, 1, 1 << 30, 1)
+    assert n > 16 * 16384
+
+
+def test_export_sort_range_subset(gpu_ctx, hga_mod):
+    ga = hga_mod.gen_genome(400_000, 21)
+    gb = hga_mod.gen_haplotype(ga, 0.02, 0, 22)
+    streams = [hga_mod.gen_art(ga, 60_000, 150, 23).seq, hga_mod.gen_art(gb, 60_000, 150, 24).seq]
+    check(gpu_ctx, streams, 19, 10, 25, 2)
