@@ -138,6 +138,7 @@ hga_status hga_count_get_stats(hga_ctx* c, hga_count_stats* out) {
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(out, HGA_ERR_INVALID, "null out pointer");
         auto& s = c->count;
+        hga::count_settle(c);
         HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
         out->instances = s.instances;
         out->distinct_rows = s.rows;

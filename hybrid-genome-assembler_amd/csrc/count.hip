@@ -178,10 +178,14 @@ struct BinFile {
     uint64_t woff;   // first word of the file's region in the packed buffers
     uint64_t n;      // bases
     uint32_t w0, pad;
+    const uint8_t* seq;   // the file's ASCII bases (HGA_B1_ASCII: bin1 packs its own frames)
 };
 
 #ifndef HGA_B1_PER_CU
 #define HGA_B1_PER_CU 2   // bin1 super-tiles per CU
+#endif
+#ifndef HGA_B1_ASCII
+#define HGA_B1_ASCII 0    // 1: bin1 packs its frames from the ASCII bases itself (no kc_pack; measured slower)
 #endif
 #ifndef HGA_B1_WAVES
 #define HGA_B1_WAVES 1
@@ -211,8 +215,8 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
     const uint32_t w = blockIdx.x;
     uint32_t file = 0;
     while (file + 1 < F && files[file + 1].w0 <= w) ++file;
-    const uint32_t* __restrict__ pk = pk_all + files[file].woff;
-    const uint16_t* __restrict__ vd = vd_all + files[file].woff;
+    [[maybe_unused]] const uint32_t* __restrict__ pk = pk_all + files[file].woff;
+    [[maybe_unused]] const uint16_t* __restrict__ vd = vd_all + files[file].woff;
     const uint64_t n = files[file].n;
     const uint32_t tag0 = w << 8;
     for (uint32_t b = tid; b < nb; b += NT_B) fhist[b] = 0;
@@ -231,10 +235,22 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
     const uint64_t start = (uint64_t)(w - files[file].w0) * st_pos;
     const uint64_t end = start + st_pos < n ? start + st_pos : n;
     uint32_t inst = 0;
+#if HGA_B1_ASCII
+    const uint8_t* __restrict__ seq = files[file].seq;
+#endif
     for (uint64_t t0 = start; t0 < end; t0 += TP_B) {
         const uint64_t p0 = t0 + (uint64_t)tid * P_B;
         Frame<P_B> f;
+#if HGA_B1_ASCII
+        // bases [p0-32, p0+16) straight from the ASCII stream (bytes outside the file are no base)
+        FrameRaw<P_B> raw;
+#pragma unroll
+        for (int i = 0; i < FrameRaw<P_B>::NW; ++i)
+            pack_bytes<false>(load16(seq, (int64_t)p0 - 32 + 16 * i, n), raw.x[i], raw.v[i]);
+        const uint64_t v64 = build_frame<P_B, false>(raw, kp.k, f);
+#else
         const uint64_t v64 = load_frame<P_B, false>(pk, vd, PAD_WORDS + p0 / 16 - 2, kp.k, f);
+#endif
         const uint32_t wm = (uint32_t)(runs_of(v64, kp.k) >> 32);   // bit j: window at p0+j valid
         uint32_t dd[P_B], rk[P_B];
         E1 ee[P_B];
@@ -358,6 +374,11 @@ __global__ void kc_pack_files(const PackFile* __restrict__ files, uint32_t F, ui
         pk[g] = code;
         vd[g] = (uint16_t)valid;
     }
+}
+
+// Pipeline counters when there is no pack pass: gstat[3] = the first spill block, the rest 0.
+__global__ void kc_init_stat(unsigned long long* __restrict__ gstat, uint64_t n_first) {
+    if (threadIdx.x < 8) gstat[threadIdx.x] = threadIdx.x == 3 ? (unsigned long long)n_first : 0ull;
 }
 
 // ---------------------------------------------------------------- layout
@@ -1505,6 +1526,7 @@ __device__ __forceinline__ uint32_t spec_index(uint32_t prev, uint32_t total, co
 // one global atomic per nonzero bin.  Totals in [TL, TD) (rare) go to the dense global
 // histogram directly (ctrl[3] counts them), >= TD to an overflow list.
 __global__ void __launch_bounds__(NT_S) kc_spec_hist(const uint32_t* __restrict__ cnt, uint64_t rows,
+                                                     const unsigned long long* __restrict__ rows_dev,
                                                      uint64_t cap, uint32_t F,
                                                      const double* __restrict__ thr, uint32_t n_thr,
                                                      unsigned long long* __restrict__ hist,
@@ -1513,6 +1535,10 @@ __global__ void __launch_bounds__(NT_S) kc_spec_hist(const uint32_t* __restrict_
                                                      uint64_t over_cap) {
     extern __shared__ uint32_t lh[];   // n_thr * TL counters (sized at launch)
     for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_S) lh[i] = 0;
+    if (rows_dev) {   // count_run not settled yet: the row cursor it left on the device (<= cap)
+        const uint64_t r = *rows_dev;
+        rows = r < cap ? r : cap;
+    }
     __syncthreads();
     const uint64_t groups = (rows + 3) / 4;
     const uint64_t stride = (uint64_t)gridDim.x * NT_S;
@@ -1719,6 +1745,7 @@ void count_begin(hga_ctx* c, int k, uint32_t n_files) {
     s.begun = true;
     s.ran = false;
     s.rows = s.instances = s.n_sel = 0;
+    s.pending = false;
 }
 
 void count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n) {
@@ -1750,6 +1777,7 @@ void count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n) {
 void count_run(hga_ctx* c, uint32_t min_per_file) {
     auto& s = c->count;
     HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
+    count_settle(c);   // a previous run nobody consumed still reports its errors
     const uint32_t F = s.n_files;
     s.min_per_file = min_per_file;
     uint64_t total_bytes = 0;
@@ -1809,12 +1837,13 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const uint64_t tail_words = ST_ALIGN / 16 + 8;
     std::vector<uint64_t> woff(F + 1, 0);
     for (uint32_t f = 0; f < F; ++f) woff[f + 1] = woff[f] + PAD_WORDS + (s.seq_len[f] + 15) / 16 + tail_words;
-    uint32_t* pk_all = static_cast<uint32_t*>(s.pk_all.ensure(woff[F] * 4));
-    uint16_t* vd_all = static_cast<uint16_t*>(s.vd_all.ensure(woff[F] * 2));
+    uint32_t* pk_all = static_cast<uint32_t*>(s.pk_all.ensure(HGA_B1_ASCII ? 64 : woff[F] * 4));
+    uint16_t* vd_all = static_cast<uint16_t*>(s.vd_all.ensure(HGA_B1_ASCII ? 64 : woff[F] * 2));
     std::vector<PackFile> pf(F);
     for (uint32_t f = 0; f < F; ++f) {
         pf[f] = PackFile{s.seq[f]->as<uint8_t>(), s.seq_len[f], woff[f], (s.seq_len[f] + 15) / 16};
         bf[f].woff = woff[f];
+        bf[f].seq = s.seq[f]->as<uint8_t>();
     }
     // per-file tables: uploaded only when they change (they are fixed for repeated runs)
     const size_t tb = sizeof(BinFile) * F + sizeof(PackFile) * F;
@@ -1847,11 +1876,16 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     void* binned1 = s.binned1.ensure(pool_cap * esz1);
     Blk* table = static_cast<Blk*>(s.regions.ensure(table_cap * sizeof(Blk)));
     // P: pack all files + counter init, one launch
-    c->launch("kc_pack", [&] {
-        hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256 * PK_W)), dim3(256), 0,
-                           c->stream, d_pf, F, woff[F], pk_all, vd_all, gstat, n_first);
-    });
-    c->check_launch("kc_pack");
+    if (HGA_B1_ASCII) {
+        hipLaunchKernelGGL(kc_init_stat, dim3(1), dim3(64), 0, c->stream, gstat, n_first);
+        c->check_launch("kc_init_stat");
+    } else {
+        c->launch("kc_pack", [&] {
+            hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256 * PK_W)), dim3(256),
+                               0, c->stream, d_pf, F, woff[F], pk_all, vd_all, gstat, n_first);
+        });
+        c->check_launch("kc_pack");
+    }
 
     // B1: level-1 binning of every file into pool blocks + per-workgroup fine histograms
     if (W) {
@@ -1916,18 +1950,36 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
                                s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, (const uint32_t*)nullptr);
     });
     c->check_launch("kc_count");
-    unsigned long long h_stat[8];
-    HGA_HIP(hipMemcpyAsync(h_stat, gstat, sizeof(h_stat), hipMemcpyDeviceToHost, c->stream));
-    c->sync();
-    HGA_REQUIRE(!(h_stat[2] & 4ull), HGA_ERR_OOM, "level-1 block pool exhausted");
-    HGA_REQUIRE(!(h_stat[2] & 1ull), HGA_ERR_INVALID, "a bucket could not be split to fit the LDS table");
-    HGA_REQUIRE(!(h_stat[2] & 2ull), HGA_ERR_OOM, "row capacity exceeded");
-    s.rows = h_stat[0];
-    s.max_split = (uint32_t)h_stat[1];
-    s.instances = h_stat[4];
+    // No synchronisation here: the counters stay on the device until the next call that needs
+    // them (count_settle), so the following spec_hist queues behind the count without a gap.
     s.rows_cap = cap;
     s.ran = true;
     s.n_sel = 0;
+    s.pending = true;
+    bool dumps = false;
+    for (auto& v : s.dump_keys) dumps = dumps || !v.empty();
+    if (dumps) count_settle(c);   // the cached rows are merged on the host side now
+}
+
+// Read back the counters of a count_run that has not been settled yet (one D2H + sync, or the
+// caller's copy `h` of them), report its errors, publish rows / instances and merge dump rows.
+void count_settle(hga_ctx* c, const unsigned long long* h) {
+    auto& s = c->count;
+    if (!s.pending) return;
+    unsigned long long h_stat[8];
+    if (!h) {
+        HGA_HIP(hipMemcpyAsync(h_stat, s.cursor.p, sizeof(h_stat), hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        h = h_stat;
+    }
+    s.pending = false;
+    if (h[2] & 7ull) s.ran = false;   // a failed run has no rows to consume
+    HGA_REQUIRE(!(h[2] & 4ull), HGA_ERR_OOM, "level-1 block pool exhausted");
+    HGA_REQUIRE(!(h[2] & 1ull), HGA_ERR_INVALID, "a bucket could not be split to fit the LDS table");
+    HGA_REQUIRE(!(h[2] & 2ull), HGA_ERR_OOM, "row capacity exceeded");
+    s.rows = h[0];
+    s.max_split = (uint32_t)h[1];
+    s.instances = h[4];
     merge_dump_rows(c);
 }
 
@@ -1935,6 +1987,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
 // (JellyfishOccurrenceReader.cpp:19-24 skips jellyfish for it and reads the dump verbatim).
 void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts, uint64_t n) {
     auto& s = c->count;
+    count_settle(c);
     HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
     HGA_REQUIRE(file < s.n_files, HGA_ERR_INVALID, "file index out of range");
     HGA_REQUIRE(n == 0 || (keys && counts), HGA_ERR_INVALID, "null rows pointer");
@@ -2005,19 +2058,25 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     double* dthr = reinterpret_cast<double*>(ctrl + 4);
     // pinned staging: [thresholds | ctrl readback (4 u64) | first SPEC_CHUNK compacted triples]
     constexpr uint64_t SPEC_CHUNK = 1u << 12;
-    char* hp = static_cast<char*>(c->pinned.ensure(MAX_THR * 8 + 32 + SPEC_CHUNK * 16));
+    char* hp = static_cast<char*>(c->pinned.ensure(MAX_THR * 8 + 32 + SPEC_CHUNK * 16 + 64));
     double* hthr = reinterpret_cast<double*>(hp);
     auto* hc = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8);
     auto* hcomp = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8 + 32);
+    auto* hrun = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8 + 32 + SPEC_CHUNK * 16);
     std::memcpy(hthr, thr.data(), n_thr * 8);
     if (fresh) HGA_HIP(hipMemsetAsync(base, 0, hbytes, c->stream));   // kept clear by kc_hist_compact
     HGA_HIP(hipMemsetAsync(ctrl, 0, 32, c->stream));
     HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
-    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_for(std::max<uint64_t>((s.rows + 3) / 4, 1), NT_S * SG_S),
+    // an unsettled count_run: rows come from its device cursor, the counters ride in this readback
+    const bool pend = s.pending;
+    const uint64_t rows_hint = pend ? s.rows_cap : s.rows;
+    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_for(std::max<uint64_t>((rows_hint + 3) / 4, 1), NT_S * SG_S),
                                                        (uint64_t)c->num_cu);
     c->launch("kc_spec_hist", [&] {
         hipLaunchKernelGGL(kc_spec_hist, dim3(grid), dim3(NT_S), (size_t)n_thr * TL * 4, c->stream,
-                           s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, dthr, n_thr,
+                           s.rows_cnt.as<uint32_t>(), rows_hint,
+                           pend ? static_cast<const unsigned long long*>(s.cursor.p) : nullptr, s.rows_cap, s.n_files,
+                           dthr, n_thr,
                            hist, over, ctrl, over_cap);
     });
     c->check_launch("kc_spec_hist");
@@ -2033,7 +2092,9 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     // one synchronisation: counters and (speculatively) the first chunk of triples together
     HGA_HIP(hipMemcpyAsync(hc, ctrl, 32, hipMemcpyDeviceToHost, c->stream));
     HGA_HIP(hipMemcpyAsync(hcomp, comp, SPEC_CHUNK * 16, hipMemcpyDeviceToHost, c->stream));
+    if (pend) HGA_HIP(hipMemcpyAsync(hrun, s.cursor.p, 64, hipMemcpyDeviceToHost, c->stream));
     c->sync();
+    if (pend) count_settle(c, hrun);
     HGA_REQUIRE(!(hc[1] & 1ull), HGA_ERR_INVALID, "a row's specificity is above the last threshold");
     HGA_REQUIRE(!(hc[1] & 2ull), HGA_ERR_OOM, "histogram overflow list full");
     HGA_REQUIRE(hc[2] <= ncap, HGA_ERR_OOM, "histogram compaction buffer full");
@@ -2071,6 +2132,7 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
 
 void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uint64_t* n_discr) {
     auto& s = c->count;
+    count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
     const uint64_t cap = std::max<uint64_t>(s.rows, 1);
     char* sb = static_cast<char*>(s.sel_keys.ensure(cap * 12 + 256));
@@ -2114,6 +2176,7 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
 
 void count_fetch_selected(hga_ctx* c, uint64_t* dst, uint8_t* flags) {
     auto& s = c->count;
+    count_settle(c);
     const uint64_t cap = std::max<uint64_t>(s.rows, 1);
     const bool flag_bit = s.k <= 31;
     if (flag_bit) {   // flag in bit 63 of each key
@@ -2147,6 +2210,7 @@ void count_fetch_selected(hga_ctx* c, uint64_t* dst, uint8_t* flags) {
 // All merged rows ascending (file < 0), or one file's dump rows (file >= 0).
 void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
     auto& s = c->count;
+    count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
     HGA_REQUIRE(file < (int)s.n_files, HGA_ERR_INVALID, "file index out of range");
     const uint64_t rows = s.rows;

@@ -137,6 +137,7 @@ __global__ void kx_merge_emit(const uint64_t* __restrict__ sk, const uint32_t* _
 void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* keys_out,
                      uint32_t* counts_out, uint64_t* rows_per_owner) {
     auto& s = c->count;
+    count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
     HGA_REQUIRE(n_own >= 1 && n_own <= KX_MAX_OWN, HGA_ERR_INVALID, "n_owners must be in [1, 1024]");
     for (uint32_t o = 1; o + 1 < n_own; ++o)
@@ -175,6 +176,7 @@ void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint
 
 void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min_c) {
     auto& s = c->count;
+    count_settle(c);
     HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
     HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 rows per merge");
     HGA_REQUIRE(min_c >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
@@ -331,6 +333,7 @@ __global__ void kx_pk_emit(const uint64_t* __restrict__ sk, uint64_t n, PackFmt 
 // Bits per file count in the packed form (0 = not packable: use the wide exchange).
 int count_pack_bits(hga_ctx* c) {
     auto& s = c->count;
+    count_settle(c);
     const int kb = 2 * s.k;
     const int cb = s.n_files ? (64 - kb) / (int)s.n_files : 0;
     return (s.n_files <= 8 && cb >= 4) ? (cb > 32 ? 32 : cb) : 0;
@@ -341,6 +344,7 @@ int count_pack_bits(hga_ctx* c) {
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,
                                 uint64_t cap_out, uint64_t* pieces_per_owner) {
     auto& s = c->count;
+    count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
     HGA_REQUIRE(n_own >= 1 && n_own <= KX_MAX_OWN, HGA_ERR_INVALID, "n_owners must be in [1, 1024]");
     const int cb = count_pack_bits(c);
@@ -390,6 +394,7 @@ uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t 
 // Owner side: pieces from every rank (device pointer, any order) -> merged ctx rows.
 void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t min_c) {
     auto& s = c->count;
+    count_settle(c);
     HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
     HGA_REQUIRE(min_c >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
     const int cb = count_pack_bits(c);

@@ -133,6 +133,7 @@ struct CountState {
     std::vector<std::vector<uint64_t>> dump_keys;
     std::vector<std::vector<uint32_t>> dump_cnt;
     uint32_t buckets = 0, fb = 0, max_split = 1;
+    bool pending = false;   // count_run's counters not read back yet (count_settle)
     ~CountState() {
         for (auto* b : seq) delete b;
     }
@@ -233,6 +234,7 @@ void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int 
                     DevBuf& scratch);
 // exclusive scan of u64 in place (sort.hip)
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
+void count_settle(hga_ctx* c, const unsigned long long* h = nullptr);
 void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int bits, const uint32_t* d_hist,
                      const uint32_t* h_hist, DevBuf& scratch);
 }  // namespace hga

@@ -143,27 +143,31 @@ struct Frame {
     uint32_t r[NW];
 };
 
+// The raw words of a frame (what load_frame reads, or what a kernel packs from ASCII itself).
+template <int P>
+struct FrameRaw {
+    static constexpr int NW = Frame<P>::NW;
+    uint32_t x[NW];
+    uint32_t v[NW];
+};
+
 // REF = KmerIterator semantics (non-bases contribute 0 to both strands); otherwise the
 // counting semantics (a window with a non-base is never used, so rc = revcomp(fwd)).
-// w0 = index (with padding) of the frame's first word.  Returns the frame's valid bits.
+// Returns the frame's valid bits.
 template <int P, bool REF>
-__device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
-                                               const uint16_t* __restrict__ vd, uint64_t w0, int k,
-                                               Frame<P>& f) {
+__device__ __forceinline__ uint64_t build_frame(const FrameRaw<P>& raw, int k, Frame<P>& f) {
     constexpr int NW = Frame<P>::NW;
     uint64_t v64 = 0;
-    uint32_t vw[NW];
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
-        f.x[i] = pk[w0 + i];
-        vw[i] = vd[w0 + i];
-        v64 |= (uint64_t)vw[i] << (16 * i);
+        f.x[i] = raw.x[i];
+        v64 |= (uint64_t)raw.v[i] << (16 * i);
     }
     uint32_t R[NW];
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
         uint32_t c = ~f.x[NW - 1 - i];
-        if (REF) c &= expand2(vw[NW - 1 - i]);
+        if (REF) c &= expand2(raw.v[NW - 1 - i]);
         R[i] = rev2(c);
     }
     // f.r = R >> (66 - 2k)   (v in [2, 64]; a and b are uniform across the wave)
@@ -180,6 +184,20 @@ __device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
         f.r[NW - 1 - i] = __builtin_amdgcn_alignbit(hi, lo, b);
     }
     return v64;
+}
+
+// w0 = index (with padding) of the frame's first word in the packed stream.
+template <int P, bool REF>
+__device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
+                                               const uint16_t* __restrict__ vd, uint64_t w0, int k,
+                                               Frame<P>& f) {
+    FrameRaw<P> r;
+#pragma unroll
+    for (int i = 0; i < FrameRaw<P>::NW; ++i) {
+        r.x[i] = pk[w0 + i];
+        r.v[i] = vd[w0 + i];
+    }
+    return build_frame<P, REF>(r, k, f);
 }
 
 // ASCII -> packed frames (kc_pack / lk_pack).  REF = KmerIterator semantics (upper-case

@@ -75,7 +75,11 @@ hga_status hga_count_add_rows(hga_ctx* ctx, uint32_t file, const uint64_t* keys,
 
 /* Runs the device pipeline on everything added: canonical k-mers, per-file exact
  * counts, per-file drop of k-mers whose count is < min_per_file (2 = jellyfish
- * `--bc`), merge across files.  May be re-run (bench). */
+ * `--bc`), merge across files.  May be re-run (bench).  Asynchronous: the launches are
+ * queued and the call returns; the run's own failures (level-1 pool, unsplittable bucket,
+ * row capacity) are reported by the next count call that consumes its rows
+ * (hga_count_spec_hist, _select*, _rows, _dump, _get_stats, the exchange calls), which
+ * then fails with that status. */
 hga_status hga_count_run(hga_ctx* ctx, uint32_t min_per_file);
 
 typedef struct hga_count_stats {
