@@ -1629,84 +1629,99 @@ __global__ void __launch_bounds__(NT_HC) kc_hist_compact(unsigned long long* __r
     }
 }
 
-static_assert(NT_H == 256, "kc_select: one top-digit bin per thread");
+#ifndef HGA_SEL_GRID
+#define HGA_SEL_GRID 1024u   // kc_select workgroups (each loops over the chunks beyond the grid)
+#endif
 constexpr int SEL_R = 16;   // rows per thread: one cursor atomic (and one count atomic) per 4096 rows
+constexpr uint32_t SEL_HB = 4096;   // top-12-bit histogram of the kept keys (the export sort's MSD pass)
+// Persistent over chunks of NT_H * SEL_R rows (each chunk: one cursor atomic pair); with dhist_rows
+// the workgroup also counts its kept keys by the top 12 bits of the sort width (hshift = 2k - 12),
+// written as one row of SEL_HB counts per workgroup.
 __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ keys,
                                                   const uint32_t* __restrict__ cnt, uint64_t rows,
                                                   uint64_t cap, uint32_t F, int64_t lower,
                                                   int64_t upper, uint64_t* __restrict__ out,
                                                   uint32_t* __restrict__ out_flag, bool flag_bit,
                                                   unsigned long long* __restrict__ stat,
-                                                  uint32_t* __restrict__ dhist_rows, int dshift) {
+                                                  uint32_t* __restrict__ dhist_rows, int hshift) {
     __shared__ uint32_t ws[NT_H / 64 + 1];
     __shared__ unsigned long long s_base;
     __shared__ uint64_t stage[NT_H * SEL_R];
     __shared__ uint8_t sflag[NT_H * SEL_R];
-    __shared__ uint32_t dh[256];   // top-digit histogram of the kept keys (the export sort's MSD pass)
-    dh[threadIdx.x] = 0;
-    const uint64_t base = (uint64_t)blockIdx.x * NT_H * SEL_R;
-    uint64_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
+    __shared__ uint32_t dh[SEL_HB];
+    if (dhist_rows)
+        for (uint32_t i = threadIdx.x; i < SEL_HB; i += NT_H) dh[i] = 0;
+    const uint64_t chunks = (rows + NT_H * SEL_R - 1) / (NT_H * SEL_R);
+    for (uint64_t ch = blockIdx.x; ch < chunks; ch += gridDim.x) {
+        const uint64_t base = ch * NT_H * SEL_R;
+        uint64_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
 #pragma unroll
-    for (int q = 0; q < SEL_R; ++q) {
-        const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
-        if (r >= rows) continue;
-        int64_t total = 0;
-        uint32_t nz = 0;
+        for (int q = 0; q < SEL_R; ++q) {
+            const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
+            if (r >= rows) continue;
+            int64_t total = 0;
+            uint32_t nz = 0;
 #pragma unroll
-        for (uint32_t f = 0; f < 4; ++f)   // the common file counts unrolled: loads issued together
-            if (f < F) {
+            for (uint32_t f = 0; f < 4; ++f)   // the common file counts unrolled: loads issued together
+                if (f < F) {
+                    const uint32_t c = cnt[(size_t)f * cap + r];
+                    total += c;
+                    nz += c > 0;
+                }
+            for (uint32_t f = 4; f < F; ++f) {
                 const uint32_t c = cnt[(size_t)f * cap + r];
                 total += c;
                 nz += c > 0;
             }
-        for (uint32_t f = 4; f < F; ++f) {
-            const uint32_t c = cnt[(size_t)f * cap + r];
-            total += c;
-            nz += c > 0;
+            if (lower <= total && total <= upper) {
+                take |= 1ull << q;
+                if (nz == 1) disc |= 1ull << q;
+            }
         }
-        if (lower <= total && total <= upper) {
-            take |= 1ull << q;
-            if (nz == 1) disc |= 1ull << q;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popcll(take), ws, &tot);
+        // same-address device atomics serialise (≈88/µs chip-wide): one pair per chunk
+        uint32_t dtot;
+        (void)block_excl_scan<NT_H>((uint32_t)__popcll(disc), ws, &dtot);
+        if (threadIdx.x == 0) {
+            s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
+            if (dtot) atomicAdd(&stat[1], (unsigned long long)dtot);
         }
-    }
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popcll(take), ws, &tot);
-    // same-address device atomics serialise (≈88/µs chip-wide): one pair per workgroup
-    uint32_t dtot;
-    (void)block_excl_scan<NT_H>((uint32_t)__popcll(disc), ws, &dtot);
-    if (threadIdx.x == 0) {
-        s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
-        if (dtot) atomicAdd(&stat[1], (unsigned long long)dtot);
-    }
-    // kept keys staged in LDS (row order), then written out coalesced
-    uint32_t o = ex;
+        // kept keys staged in LDS (row order), then written out coalesced
+        uint32_t o = ex;
 #pragma unroll
-    for (int q = 0; q < SEL_R; ++q)
-        if ((take >> q) & 1ull) {
-            const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
-            stage[o++] = keys[r] | (flag_bit ? (((disc >> q) & 1ull) << 63) : 0ull);
-            if (!flag_bit) sflag[o - 1] = (uint8_t)((disc >> q) & 1ull);
+        for (int q = 0; q < SEL_R; ++q)
+            if ((take >> q) & 1ull) {
+                const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
+                const uint64_t kv = keys[r];
+                stage[o++] = kv | (flag_bit ? (((disc >> q) & 1ull) << 63) : 0ull);
+                if (!flag_bit) sflag[o - 1] = (uint8_t)((disc >> q) & 1ull);
+                if (dhist_rows) atomicAdd(&dh[(uint32_t)(kv >> hshift) & (SEL_HB - 1)], 1u);
+            }
+        __syncthreads();
+        const uint64_t ob = s_base;
+        for (uint32_t j = threadIdx.x; j < tot; j += NT_H) {
+            out[ob + j] = stage[j];
+            if (!flag_bit) out_flag[ob + j] = sflag[j];
         }
-    __syncthreads();
-    const uint64_t ob = s_base;
-    for (uint32_t j = threadIdx.x; j < tot; j += NT_H) {
-        const uint64_t v = stage[j];
-        out[ob + j] = v;
-        if (!flag_bit) out_flag[ob + j] = sflag[j];
-        if (dhist_rows) atomicAdd(&dh[(uint32_t)(v >> dshift) & 255u], 1u);
+        __syncthreads();   // stage and s_base are reused by the next chunk
     }
     if (dhist_rows) {
         __syncthreads();
-        dhist_rows[(uint64_t)blockIdx.x * 256 + threadIdx.x] = dh[threadIdx.x];
+        for (uint32_t i = threadIdx.x; i < SEL_HB; i += NT_H) dhist_rows[(uint64_t)blockIdx.x * SEL_HB + i] = dh[i];
     }
 }
 
-// hist[d] = sum over kc_select workgroups of their top-digit counts (rows x 256, row-major).
+// hist[b] += sum over a group of 32 kc_select workgroups' top-12-bit counts (rows x SEL_HB,
+// row-major); grid (SEL_HB / 256, row groups), hist zeroed beforehand.
 __global__ void __launch_bounds__(256) kc_dhist_reduce(const uint32_t* __restrict__ rows, uint32_t n_rows,
                                                        uint32_t* __restrict__ hist) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t r0 = blockIdx.y * 32, r1 = r0 + 32 < n_rows ? r0 + 32 : n_rows;
     uint32_t s = 0;
-    for (uint32_t r = blockIdx.x; r < n_rows; r += gridDim.x) s += rows[(uint64_t)r * 256 + threadIdx.x];
-    if (s) atomicAdd(&hist[threadIdx.x], s);
+#pragma unroll 8
+    for (uint32_t r = r0; r < r1; ++r) s += rows[(uint64_t)r * SEL_HB + b];
+    if (s) atomicAdd(&hist[b], s);
 }
 
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
@@ -2140,35 +2155,54 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     uint32_t* flag = reinterpret_cast<uint32_t*>(sb + cap * 8);
     const bool flag_bit = s.k <= 31;   // the discriminative flag rides in key bit 63
     const int bits = 2 * s.k;
-    // export sort: one MSD pass on the top 8 bits + per-segment LDS sorts (sort_export_u64) when
-    // the flag rides in the key; the top-digit histogram comes out of kc_select
+    // export sort: one MSD pass over the span the kept keys actually occupy (an owner's range on a
+    // multi-GPU run, the whole code space on one) + per-segment LDS sorts (sort_export_u64) when the
+    // flag rides in the key; kc_select counts the kept keys by the top 12 bits of the code
     const bool msd = flag_bit && bits >= 16 && s.rows >= (1u << 15);
-    const unsigned grid = (unsigned)blocks_for(std::max<uint64_t>(s.rows, 1), NT_H * SEL_R);
-    auto* stat = static_cast<unsigned long long*>(s.sel_tmp.ensure(64 + 1024 + (msd ? (size_t)grid * 1024 : 0)));
-    uint32_t* dhist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(stat) + 64);
-    uint32_t* dhist_rows = msd ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(stat) + 64 + 1024) : nullptr;
-    HGA_HIP(hipMemsetAsync(stat, 0, 64 + 1024, c->stream));
+    const uint64_t chunks = blocks_for(std::max<uint64_t>(s.rows, 1), NT_H * SEL_R);
+    const unsigned grid = (unsigned)std::min<uint64_t>(chunks, (uint64_t)HGA_SEL_GRID);
+    const size_t hb = (size_t)SEL_HB * 4;
+    char* tb = static_cast<char*>(s.sel_tmp.ensure(64 + hb + 1024 + (msd ? (size_t)grid * hb : 0)));
+    auto* stat = reinterpret_cast<unsigned long long*>(tb);
+    uint32_t* dhist = reinterpret_cast<uint32_t*>(tb + 64);                // SEL_HB top-12-bit counts
+    uint32_t* dig256 = reinterpret_cast<uint32_t*>(tb + 64 + hb);          // the MSD digit counts
+    uint32_t* dhist_rows = msd ? reinterpret_cast<uint32_t*>(tb + 64 + hb + 1024) : nullptr;
+    HGA_HIP(hipMemsetAsync(stat, 0, 64 + (msd ? hb : 0), c->stream));
     if (s.rows) {
         c->launch("kc_select", [&] {
             hipLaunchKernelGGL(kc_select, dim3(grid), dim3(NT_H), 0, c->stream, s.rows_key.as<uint64_t>(),
                                s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, lower, upper, out, flag,
-                               flag_bit, stat, dhist_rows, bits - 8);
+                               flag_bit, stat, dhist_rows, bits - 12);
             if (msd)
-                hipLaunchKernelGGL(kc_dhist_reduce, dim3(std::min<unsigned>(grid, 64)), dim3(256), 0, c->stream,
+                hipLaunchKernelGGL(kc_dhist_reduce, dim3(SEL_HB / 256, (grid + 31) / 32), dim3(256), 0, c->stream,
                                    dhist_rows, grid, dhist);
         });
         c->check_launch("kc_select");
     }
-    // one synchronisation: counts and the top-digit histogram together (pinned staging)
-    auto* hs = static_cast<unsigned long long*>(c->pinned_sel.ensure(64 + 1024));
-    HGA_HIP(hipMemcpyAsync(hs, stat, 64 + 1024, hipMemcpyDeviceToHost, c->stream));
+    // one synchronisation: counts and the top-12-bit histogram together (pinned staging)
+    char* hp = static_cast<char*>(c->pinned_sel.ensure(64 + hb + 1024));
+    auto* hs = reinterpret_cast<unsigned long long*>(hp);
+    const uint32_t* h12 = reinterpret_cast<const uint32_t*>(hp + 64);
+    uint32_t* h256 = reinterpret_cast<uint32_t*>(hp + 64 + hb);
+    HGA_HIP(hipMemcpyAsync(hs, stat, msd ? 64 + hb : 64, hipMemcpyDeviceToHost, c->stream));
     c->sync();
     const uint64_t n = hs[0];
-    if (msd && n > 1)
-        sort_export_u64(c, out, n, bits, dhist, reinterpret_cast<const uint32_t*>(reinterpret_cast<char*>(hs) + 64),
-                        s.scratch);
-    else
+    if (msd && n > 1) {
+        // digit = (code >> shift) - dbase over the occupied 12-bit bins [lo, hi], <= 256 digits
+        uint32_t lo = 0, hi = SEL_HB - 1;
+        while (lo < hi && !h12[lo]) ++lo;
+        while (hi > lo && !h12[hi]) --hi;
+        int lg = 0;
+        while ((hi >> lg) - (lo >> lg) + 1 > 256) ++lg;
+        const int shift = bits - 12 + lg;
+        const uint32_t dbase = lo >> lg;
+        std::memset(h256, 0, 1024);
+        for (uint32_t b = lo; b <= hi; ++b) h256[(b >> lg) - dbase] += h12[b];
+        HGA_HIP(hipMemcpyAsync(dig256, h256, 1024, hipMemcpyHostToDevice, c->stream));
+        sort_export_u64(c, out, n, shift, dbase, dig256, h256, s.scratch);
+    } else {
         radix_sort_u64(c, out, flag_bit ? nullptr : flag, n, bits, s.scratch);
+    }
     s.n_sel = n;
     *n_out = n;
     *n_discr = hs[1];

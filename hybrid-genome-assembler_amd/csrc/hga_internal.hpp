@@ -235,6 +235,6 @@ void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int 
 // exclusive scan of u64 in place (sort.hip)
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
 void count_settle(hga_ctx* c, const unsigned long long* h = nullptr);
-void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int bits, const uint32_t* d_hist,
+void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t dbase, const uint32_t* d_hist,
                      const uint32_t* h_hist, DevBuf& scratch);
 }  // namespace hga

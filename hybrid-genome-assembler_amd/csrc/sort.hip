@@ -169,7 +169,8 @@ template <class K, bool HAS_V>
 __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     K* __restrict__ kout, uint32_t* __restrict__ vout, uint64_t n,
                                                     int shift, uint32_t dmask, const uint32_t* __restrict__ ghist,
-                                                    uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr) {
+                                                    uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr,
+                                                    uint32_t dbase = 0u) {
     __shared__ uint32_t wcnt[4][256];
     __shared__ uint32_t gofs[256];
     __shared__ uint32_t ws[8];
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
         const bool ok = i < n;
         key[j] = ok ? kin[i] : K(0);
         if (HAS_V) val[j] = ok ? vin[i] : 0u;
-        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & dmask) : 256u;
+        dig[j] = ok ? (((uint32_t)(key[j] >> shift) - dbase) & dmask) : 256u;
     }
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
@@ -279,7 +280,7 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
     const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
     for (uint32_t i = tid; i < cnt; i += RS_T) {
         const K kk = sk[i];
-        const uint64_t g = (uint64_t)gofs[(uint32_t)(kk >> shift) & dmask] + i;
+        const uint64_t g = (uint64_t)gofs[((uint32_t)(kk >> shift) - dbase) & dmask] + i;
         kout[g] = kk;
         if (HAS_V) vout[g] = sv[i];
     }
@@ -579,12 +580,13 @@ void radix_sort_u64(hga_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n, int 
                     DevBuf& scratch) {
     radix_sort_impl<uint64_t>(c, keys, vals, n, bits, scratch);
 }
-// keys: n keys whose sort width is `bits` (16..62; bits above it are payload), d_hist / h_hist: the
-// device / host copies of the 256 counts of the top digit (bits-8 .. bits-1).  Sorted in place.
-void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int bits, const uint32_t* d_hist,
+// keys: n keys, all with ((key >> shift) - dbase) in [0, 256) (the MSD digit; bits of key above the
+// sort width are payload and vanish in the 8-bit difference), d_hist / h_hist: the device / host
+// copies of the 256 digit counts.  Sorted in place by the digit, then by the low `shift` bits.
+void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t dbase, const uint32_t* d_hist,
                      const uint32_t* h_hist, DevBuf& scratch) {
     if (n <= 1) return;
-    HGA_REQUIRE(bits >= 16 && bits <= 62 && n < (1ull << 32), HGA_ERR_INVALID, "export sort: bad width");
+    HGA_REQUIRE(shift >= 0 && shift <= 54 && n < (1ull << 32), HGA_ERR_INVALID, "export sort: bad width");
     const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     const size_t kb = ((n * 8 + 255) & ~255ull), stb = (size_t)n_tiles * 256 * 4, tcb = 64;
     char* base = static_cast<char*>(scratch.ensure(kb + stb + tcb));
@@ -592,10 +594,10 @@ void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int bits, const uin
     uint32_t* status = reinterpret_cast<uint32_t*>(base + kb);
     uint32_t* tctr = reinterpret_cast<uint32_t*>(base + kb + stb);
     HGA_HIP(hipMemsetAsync(status, 0, stb + tcb, c->stream));
-    const int shift = bits - 8;
     c->launch("radix_downsweep", [&] {
         hipLaunchKernelGGL((rs_onesweep<uint64_t, false>), dim3(n_tiles), dim3(RS_T), 0, c->stream, keys,
-                           (const uint32_t*)nullptr, k2, (uint32_t*)nullptr, n, shift, 255u, d_hist, status, tctr);
+                           (const uint32_t*)nullptr, k2, (uint32_t*)nullptr, n, shift, 255u, d_hist, status, tctr,
+                           dbase);
     });
     c->check_launch("rs_onesweep");
     c->launch("radix_segsort", [&] {
@@ -606,7 +608,7 @@ void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int bits, const uin
     for (int d = 0; d < 256; ++d) {   // segments too large for one workgroup's LDS
         if (h_hist[d] > (uint32_t)SS_CAP) {
             DevBuf tmp;
-            radix_sort_u64(c, k2 + st, nullptr, h_hist[d], shift, tmp);
+            if (shift > 0) radix_sort_u64(c, k2 + st, nullptr, h_hist[d], shift, tmp);
             HGA_HIP(hipMemcpyAsync(keys + st, k2 + st, (size_t)h_hist[d] * 8, hipMemcpyDeviceToDevice, c->stream));
             c->sync();   // tmp is freed on return
         }

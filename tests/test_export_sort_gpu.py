@@ -69,3 +69,19 @@ def test_export_sort_range_subset(gpu_ctx, hga_mod):
     gb = hga_mod.gen_haplotype(ga, 0.02, 0, 22)
     streams = [hga_mod.gen_art(ga, 60_000, 150, 23).seq, hga_mod.gen_art(gb, 60_000, 150, 24).seq]
     check(gpu_ctx, streams, 19, 10, 25, 2)
+
+
+@pytest.mark.parametrize("lo,width", [(1 << 35, 1 << 31), (5 << 30, 1 << 24), (0, 1 << 38)])
+def test_export_sort_owner_like_ranges(gpu_ctx, lo, width):
+    # rows confined to a key range, as on one owner of a multi-GPU run: the MSD digit spans only the
+    # occupied range (12-bit bins lo..hi), not the whole code space
+    rng = np.random.default_rng(lo % 1000 + width % 997)
+    keys = np.unique(rng.integers(lo, lo + width, 120_000, dtype=np.uint64))
+    counts = rng.integers(10, 30, len(keys), dtype=np.uint32)
+    gpu_ctx.count_begin(19, 1)
+    gpu_ctx.count_add_rows(0, keys, counts)
+    gpu_ctx.count_run(2)
+    sel, flags, nd = gpu_ctx.select(10, 25)
+    want = keys[(counts >= 10) & (counts <= 25)]
+    assert np.array_equal(sel, want)
+    assert nd == len(want) and np.all(flags == 1)
