@@ -166,12 +166,15 @@ class OwnerExchange:
         """Global specificity histogram (std::map order), identical on every rank."""
         local = np.ascontiguousarray(self.e.spec_hist(thresholds), dtype=np.int64).reshape(-1, 3)
         parts = self._all_gather_var(local.reshape(-1))
-        acc = {}
-        for p in parts:
-            for t, tot, c in p.reshape(-1, 3):
-                acc[(int(t), int(tot))] = acc.get((int(t), int(tot)), 0) + int(c)
-        keys = sorted(acc)
-        return np.array([[t, tot, acc[(t, tot)]] for t, tot in keys], dtype=np.int64).reshape(-1, 3)
+        allp = np.concatenate([p.reshape(-1, 3) for p in parts]) if parts else np.zeros((0, 3), np.int64)
+        if len(allp) == 0:
+            return np.zeros((0, 3), np.int64)
+        # sum the counts of equal (threshold, total) bins; np.unique sorts = std::map order
+        packed = (allp[:, 0] << 40) | allp[:, 1]
+        u, inv = np.unique(packed, return_inverse=True)
+        cnt = np.zeros(len(u), np.int64)
+        np.add.at(cnt, inv, allp[:, 2])
+        return np.stack([u >> 40, u & ((1 << 40) - 1), cnt], axis=1).astype(np.int64)
 
     def select(self, lower: int, upper: int, root: int = 0):
         """Export keys (ascending) and discriminative flags gathered on `root` (None elsewhere)."""
