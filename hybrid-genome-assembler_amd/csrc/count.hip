@@ -75,6 +75,9 @@
 #ifndef HGA_EXP_SH_NOFLUSH
 #define HGA_EXP_SH_NOFLUSH 0
 #endif
+#ifndef HGA_EXP_PK_NOVD
+#define HGA_EXP_PK_NOVD 0
+#endif
 #ifndef HGA_EXP_NOEMIT
 #define HGA_EXP_NOEMIT 0
 #endif
@@ -97,9 +100,13 @@ constexpr uint64_t ST_ALIGN = TP_B;    // super-tiles are whole tiles
 #endif
 constexpr int MAX_FB = HGA_MAX_FB;
 constexpr int MAX_NB = 1 << MAX_FB;
-constexpr int MAX_FB1 = 6;    // level-1 fan-out <= 64
+#ifndef HGA_MAX_FB1
+#define HGA_MAX_FB1 6
+#endif
+constexpr int MAX_FB1 = HGA_MAX_FB1;    // level-1 fan-out <= 64
 constexpr int NB1_MAX = 1 << MAX_FB1;
 constexpr int NB2_MAX = 1 << (MAX_FB - MAX_FB1 > 6 ? MAX_FB - MAX_FB1 : 6);   // level-2 fan-out
+static_assert(NB1_MAX <= 64 && NB2_MAX <= 128, "bin1 scans <= 64 regions with one wave, rebin <= 128 digits with two");
 constexpr int NT_R = 512;     // re-bin workgroup
 constexpr int CH_R = NT_R * 16;        // 8192 elements per re-bin chunk
 constexpr int NT_C = HGA_NT_C;   // threads of the per-bucket count workgroup
@@ -344,7 +351,10 @@ struct PackFile {
     const uint8_t* seq;
     uint64_t n, woff, nw;
 };
-constexpr int PK_W = 4;   // words per thread (grid-strided: every load instruction coalesced)
+#ifndef HGA_PK_W
+#define HGA_PK_W 4
+#endif
+constexpr int PK_W = HGA_PK_W;   // words per thread (grid-strided: every load instruction coalesced)
 __global__ void kc_pack_files(const PackFile* __restrict__ files, uint32_t F, uint64_t total_words,
                               uint32_t* __restrict__ pk, uint16_t* __restrict__ vd,
                               unsigned long long* __restrict__ gstat, uint64_t n_first) {
@@ -372,6 +382,9 @@ __global__ void kc_pack_files(const PackFile* __restrict__ files, uint32_t F, ui
         uint32_t code = 0, valid = 0;
         if (in[u]) pack_bytes<false>(raw[u], code, valid);
         pk[g] = code;
+#if HGA_EXP_PK_NOVD
+        if (valid == 0x12345u)
+#endif
         vd[g] = (uint16_t)valid;
     }
 }
