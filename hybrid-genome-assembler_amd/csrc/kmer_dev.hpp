@@ -206,18 +206,28 @@ __device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
 // 16 bases starting at 16w -> 2-bit codes (MSB-first) + valid bits.
 template <bool REF>
 __device__ __forceinline__ void pack_bytes(const uint4 v, uint32_t& code, uint32_t& valid) {
+    // four bytes per 32-bit word at a time (SWAR): a byte is a base iff it equals one of 'A' 'C'
+    // 'G' 'T' (after the case fold of the counting semantics) — exact per-byte zero tests of the
+    // xor with each; codes ((u >> 1) ^ (u >> 2)) & 3, forced to 0 for non-bases
     const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
     code = 0;
     valid = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t b = (ws[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-        const uint32_t u = REF ? b : (b & 0xDFu);
-        const uint32_t d = u - 0x41u;
-        const bool ok = d < 20u && ((kBaseBits >> d) & 1u);
-        const uint32_t c = ok ? (((u >> 1) ^ (u >> 2)) & 3u) : 0u;
-        code |= c << (30 - 2 * j);
-        valid |= (ok ? 1u : 0u) << j;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t u = REF ? ws[i] : (ws[i] & 0xDFDFDFDFu);
+        uint32_t c4 = ((u >> 1) ^ (u >> 2)) & 0x03030303u;
+        uint32_t f = 0;
+#pragma unroll
+        for (uint32_t X : {0x41u, 0x43u, 0x47u, 0x54u}) {
+            const uint32_t t = u ^ (X * 0x01010101u);
+            f |= ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;   // bit 7: byte == X
+        }
+        const uint32_t m = f >> 7;                        // bits 0, 8, 16, 24
+        c4 &= m * 3u;
+        const uint32_t r = __builtin_bswap32(c4);         // first base in the top byte
+        const uint32_t t = (r | (r >> 6)) & 0x000F000Fu;
+        code |= ((t | (t >> 12)) & 0xFFu) << (24 - 8 * i);
+        valid |= ((m * 0x01020408u) >> 24) << (4 * i);    // byte b -> bit b
     }
 }
 
