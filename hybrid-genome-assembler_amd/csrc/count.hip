@@ -893,6 +893,9 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 #ifndef HGA_COUNT_SOA
 #define HGA_COUNT_SOA 1   // kc_count_s (SoA keys/counts) rather than kc_count_p (u64 entries)
 #endif
+#ifndef HGA_S_BRANCHLESS
+#define HGA_S_BRANCHLESS 1   // kc_count_s: hits added by every lane (non-hits into per-lane dummy words)
+#endif
 #ifndef HGA_NT_P
 #define HGA_NT_P 512
 #endif
@@ -1263,7 +1266,7 @@ __global__ void __launch_bounds__(NT_P, 4) kc_count_s(const uint32_t* __restrict
                                                       unsigned long long* __restrict__ gstat,
                                                       uint32_t* __restrict__ blist) {
     __shared__ __attribute__((aligned(16))) uint32_t tkey[T_S];
-    __shared__ __attribute__((aligned(16))) uint32_t tcnt[T_S];
+    __shared__ __attribute__((aligned(16))) uint32_t tcnt[T_S + 64];   // + per-lane dummies (branch-free hits)
     __shared__ uint32_t qbuf[NT_P / 64][QN_P];
     __shared__ uint32_t s_ovf, s_sp, s_ranges;
     __shared__ uint32_t stk_lo[40], stk_hi[40];
@@ -1361,15 +1364,26 @@ __global__ void __launch_bounds__(NT_P, 4) kc_count_s(const uint32_t* __restrict
                     match_s(kg[q], rv[q], w, e0);
                     const bool live = rv[q] != 0xFFFFFFFFu;
                     slot[q] = (rv[q] & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
-#if HGA_EXP_S_HITSTORE
+#if HGA_S_BRANCHLESS
+                    {   // every lane adds: a hit to its slot, anything else to its own dummy word
+                        const bool hit = live && w >= 0;
+                        atomicAdd(&tcnt[hit ? slot[q] : T_S + lane], inc);
+                        claim |= (live && !hit && e0 >= 0) ? 1u << q : 0u;
+                        miss |= (live && !hit && e0 < 0) ? 1u << q : 0u;
+                    }
+#elif HGA_EXP_S_HITSTORE
                     if (live && w >= 0) tcnt[slot[q]] = inc;
-#elif HGA_EXP_S_NOHIT
-                    if (live && w >= 0 && rv[q] == 0x1234567u) tcnt[slot[q]] = inc;
-#else
-                    if (live && w >= 0) atomicAdd(&tcnt[slot[q]], inc);
-#endif
                     else if (live && e0 >= 0) claim |= 1u << q;
                     else if (live) miss |= 1u << q;
+#elif HGA_EXP_S_NOHIT
+                    if (live && w >= 0 && rv[q] == 0x1234567u) tcnt[slot[q]] = inc;
+                    else if (live && e0 >= 0) claim |= 1u << q;
+                    else if (live) miss |= 1u << q;
+#else
+                    if (live && w >= 0) atomicAdd(&tcnt[slot[q]], inc);
+                    else if (live && e0 >= 0) claim |= 1u << q;
+                    else if (live) miss |= 1u << q;
+#endif
                 }
 #if HGA_S_NEXT
                 // home group full without the key: the next group, inline (one displacement
