@@ -55,15 +55,19 @@ __device__ __forceinline__ uint32_t murmur3_u64(uint64_t key, uint32_t seed) {
     return h;
 }
 
+// K > 0: k known at compile time (frame offsets and masks fold; for K <= 16 the high 4-byte block
+// of the key is zero and its murmur round folds to constants); K == 0: any k.
+template <int K>
 __global__ void __launch_bounds__(HL_T) hll_scan(const uint32_t* __restrict__ pk, const uint16_t* __restrict__ vd,
-                                                 const unsigned int* __restrict__ sb, uint64_t nbases, int k,
+                                                 const unsigned int* __restrict__ sb, uint64_t nbases, int k_rt,
                                                  int b, uint64_t n_threads, uint8_t* __restrict__ part) {
     extern __shared__ uint32_t reg[];
+    const int k = K ? K : k_rt;
     const uint32_t m = 1u << b;
     for (uint32_t i = threadIdx.x; i < m; i += HL_T) reg[i] = 0;
     __syncthreads();
     const uint64_t mask = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1);
-    const int rb = 32 - b;
+    const uint32_t rb = 32u - (uint32_t)b;
     for (uint64_t gt = (uint64_t)blockIdx.x * HL_T + threadIdx.x; gt < n_threads;
          gt += (uint64_t)gridDim.x * HL_T) {
         const uint64_t p0 = gt * HL_P;
@@ -80,8 +84,8 @@ __global__ void __launch_bounds__(HL_T) hll_scan(const uint32_t* __restrict__ pk
             const uint64_t rc = field64<NW>(f.r, 2 * j) & mask;
             const uint32_t h = murmur3_u64(fwd < rc ? fwd : rc, HLL_SEED);
             const uint32_t idx = h >> rb;
-            const uint32_t x = h << b;
-            const uint32_t rank = (x ? min((uint32_t)rb, (uint32_t)__builtin_clz(x)) : (uint32_t)rb) + 1u;
+            // rank = min(32 - b, clz(h << b)) + 1, with clz(0) = 32 (see the header)
+            const uint32_t rank = min(rb, (uint32_t)__clz((int)(h << b))) + 1u;
             if (((wm >> j) & 1u) && rank > reg[idx]) atomicMax(&reg[idx], rank);
         }
     }
@@ -125,8 +129,25 @@ void hll_registers(hga_ctx* c, int k, int b, uint8_t* regs) {
     uint32_t* dout = reinterpret_cast<uint32_t*>(part + (uint64_t)nblk * m);
     HGA_HIP(hipMemsetAsync(dout, 0, 4ull * m, c->stream));
     c->launch("hll_scan", [&] {
-        hipLaunchKernelGGL(hll_scan, dim3(nblk), dim3(HL_T), m * 4, c->stream, L.packed.as<uint32_t>(),
-                           L.valid.as<uint16_t>(), L.starts.as<unsigned int>(), nb, k, b, n_threads, part);
+        // compile-time k for the auto-k sweep (k = 11, 13, ..., 31: KmerAnalysis.cpp:41-56)
+#define HGA_HLL(KK)                                                                                           \
+    hipLaunchKernelGGL(hll_scan<KK>, dim3(nblk), dim3(HL_T), m * 4, c->stream, L.packed.as<uint32_t>(),        \
+                       L.valid.as<uint16_t>(), L.starts.as<unsigned int>(), nb, k, b, n_threads, part)
+        switch (k) {
+            case 11: HGA_HLL(11); break;
+            case 13: HGA_HLL(13); break;
+            case 15: HGA_HLL(15); break;
+            case 17: HGA_HLL(17); break;
+            case 19: HGA_HLL(19); break;
+            case 21: HGA_HLL(21); break;
+            case 23: HGA_HLL(23); break;
+            case 25: HGA_HLL(25); break;
+            case 27: HGA_HLL(27); break;
+            case 29: HGA_HLL(29); break;
+            case 31: HGA_HLL(31); break;
+            default: HGA_HLL(0); break;
+        }
+#undef HGA_HLL
     });
     c->check_launch("hll_scan");
     c->launch("hll_reduce", [&] {
