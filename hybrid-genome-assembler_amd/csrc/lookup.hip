@@ -228,10 +228,12 @@ __device__ __forceinline__ uint64_t lk_canon_rt(const Frame<LK_P>& f, int j, uin
     return fwd < rc ? fwd : rc;
 }
 
-template <bool EMIT, int KM>
+// K > 0: k known at compile time (masks and the m-mer / k-mer widths fold, narrowing the 64-bit
+// hash multiplies); K == 0: any k.
+template <bool EMIT, int KM, int K = 0>
 __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk, const uint16_t* __restrict__ vd,
                                                 const unsigned int* __restrict__ sb, uint64_t nbases,
-                                                const uint64_t* __restrict__ offs, uint64_t nreads, int k,
+                                                const uint64_t* __restrict__ offs, uint64_t nreads, int k_rt,
                                                 const uint32_t* __restrict__ word_read,
                                                 LkTab tab, uint32_t* __restrict__ hmask,
                                                 uint32_t* __restrict__ win_kid,
@@ -239,6 +241,7 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
                                                 uint32_t* __restrict__ h_read, uint32_t* __restrict__ h_kid,
                                                 uint32_t* __restrict__ h_pos) {
     __shared__ uint32_t ws[LK_T / 64 + 1];
+    const int k = K ? K : k_rt;
     const uint64_t gt = (uint64_t)blockIdx.x * LK_T + threadIdx.x;
     const uint64_t p0 = gt * LK_P;
     const uint64_t mask = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1);
@@ -631,12 +634,15 @@ void lookup_run(hga_ctx* c) {
     uint64_t H = 0;
     if (n_tiles) {
         c->launch("lk_count", [&] {
-#define HGA_LK_SCAN(KMV)                                                                                       \
-    hipLaunchKernelGGL((lk_scan<false, KMV>), dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, nb, \
-                       offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, (uint32_t*)nullptr,          \
+#define HGA_LK_SCAN(KMV, KK)                                                                                 \
+    hipLaunchKernelGGL((lk_scan<false, KMV, KK>), dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, \
+                       nb, offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, (uint32_t*)nullptr,      \
                        (uint32_t*)nullptr, (uint32_t*)nullptr)
-            if (L.km == LK_KM) HGA_LK_SCAN(LK_KM);
-            else HGA_LK_SCAN(0);
+            if (L.km == LK_KM && k == 19) HGA_LK_SCAN(LK_KM, 19);   // compile-time k for the usual SDK k
+            else if (L.km == LK_KM && k == 17) HGA_LK_SCAN(LK_KM, 17);
+            else if (L.km == LK_KM && k == 21) HGA_LK_SCAN(LK_KM, 21);
+            else if (L.km == LK_KM) HGA_LK_SCAN(LK_KM, 0);
+            else HGA_LK_SCAN(0, 0);
 #undef HGA_LK_SCAN
         });
         c->check_launch("lk_count");
