@@ -10,6 +10,9 @@
 //                                keys (one row per source rank at most), apply the per-file
 //                                `--bc` drop (run_jellyfish.sh:3-6, count >= min), and rebuild the
 //                                ctx rows so spec_hist / select / rows / dump run unchanged.
+// The packed form (one u64 piece per row, the default exchange) partitions with one LDS atomic
+// per owner per wave (kx_piece_hist / kx_pack_scatter) and merges without a sort: pieces are
+// binned by a hash of the key and every bin is summed in an LDS table (kx_mb_*).
 // Owners hold disjoint ascending code ranges, so per-owner exports concatenated in rank order
 // are the reference's LC_ALL=C export order (JellyfishOccurrenceReader.cpp:110-135).
 #include "hga_internal.hpp"
@@ -236,13 +239,75 @@ struct PackFmt {
 
 __device__ __forceinline__ uint64_t pieces_of(const uint32_t* __restrict__ cnt, uint64_t cap, uint64_t i,
                                               const PackFmt& pf) {
-    uint64_t p = 1;
+    uint32_t big = 0;   // the largest count; one piece unless it passes 2^cb - 1 (cb <= 32)
     for (uint32_t f = 0; f < pf.F; ++f) {
-        const uint64_t c = cnt[(uint64_t)f * cap + i];
-        const uint64_t q = (c + pf.cmax - 1) / pf.cmax;
-        p = q > p ? q : p;
+        const uint32_t c = cnt[(uint64_t)f * cap + i];
+        big = c > big ? c : big;
     }
-    return p;
+    if (big <= pf.cmax) return 1;
+    return ((uint64_t)big + pf.cmax - 1) / pf.cmax;
+}
+
+// Wave-aggregated owner counters (rows go to random owners, so per-lane adds on n_own <= 64
+// counters would serialise): the owner ids' bit planes are balloted once, lane j builds owner
+// j's lane mask from them and makes that owner's one LDS add, every live lane gets its
+// position (in lane order) from its owner's mask.  nbits = ceil(log2(n_own)) <= 6.
+__device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long* ctr, uint32_t o, bool live,
+                                                             uint32_t n_own, int nbits) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t L = __ballot(live);
+    uint64_t m = L, mo = L;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        if (b >= nbits) break;
+        const uint64_t B = __ballot(live && ((o >> b) & 1u));
+        m &= ((o >> b) & 1u) ? B : ~B;
+        mo &= ((lane >> b) & 1u) ? B : ~B;
+    }
+    unsigned long long base = 0;
+    if (lane < n_own && mo) base = atomicAdd(&ctr[lane], (unsigned long long)__popcll(mo));
+    base = __shfl(base, (int)(o & 63u), 64);
+    return base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int owner_bits(uint32_t n_own) {
+    int b = 0;
+    while ((1u << b) < n_own) ++b;
+    return b;
+}
+
+// A tile's rows, loads issued together: keys, their packed single piece (valid when every
+// count <= 2^cb - 1) and the largest count; splitters staged in LDS for the owner search.
+struct RowTile {
+    uint64_t key[KX_R], pk[KX_R];
+    uint32_t big[KX_R];
+};
+__device__ __forceinline__ void load_row_tile(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ cnt,
+                                              uint64_t cap, uint64_t rows, uint64_t t0, const PackFmt& pf,
+                                              RowTile& rt) {
+#pragma unroll
+    for (int r = 0; r < KX_R; ++r) {
+        const uint64_t i = t0 + (uint64_t)r * KX_T + threadIdx.x;
+        rt.key[r] = i < rows ? keys[i] : 0ull;
+        rt.big[r] = 0;
+    }
+#pragma unroll
+    for (int r = 0; r < KX_R; ++r) rt.pk[r] = rt.key[r];
+    for (uint32_t f = 0; f < pf.F; ++f) {
+        uint32_t c[KX_R];
+#pragma unroll
+        for (int r = 0; r < KX_R; ++r) {
+            const uint64_t i = t0 + (uint64_t)r * KX_T + threadIdx.x;
+            c[r] = i < rows ? cnt[(uint64_t)f * cap + i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < KX_R; ++r) {
+            rt.big[r] = c[r] > rt.big[r] ? c[r] : rt.big[r];
+            rt.pk[r] |= (uint64_t)c[r] << (pf.kb + (int)f * pf.cb);
+        }
+    }
+}
+__device__ __forceinline__ void stage_splitters(const uint64_t* __restrict__ spl, uint32_t n_own, uint64_t* ls) {
+    for (uint32_t o = threadIdx.x; o + 1 < n_own; o += KX_T) ls[o] = spl[o];
 }
 
 __global__ void __launch_bounds__(KX_T) kx_piece_hist(const uint64_t* __restrict__ keys,
@@ -251,14 +316,24 @@ __global__ void __launch_bounds__(KX_T) kx_piece_hist(const uint64_t* __restrict
                                                       uint32_t n_own, PackFmt pf, uint64_t* __restrict__ hist,
                                                       uint64_t n_tiles) {
     __shared__ unsigned long long h[KX_MAX_OWN];
+    __shared__ uint64_t ls[KX_MAX_OWN];
     for (uint32_t o = threadIdx.x; o < n_own; o += KX_T) h[o] = 0;
+    stage_splitters(spl, n_own, ls);
+    const uint64_t t0 = (uint64_t)blockIdx.x * KX_TILE;
+    const int nbits = owner_bits(n_own);
+    RowTile rt;
+    load_row_tile(keys, cnt, cap, rows, t0, pf, rt);
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * KX_TILE;
-#pragma unroll 4
+#pragma unroll
     for (int r = 0; r < KX_R; ++r) {
-        const uint64_t i = base + (uint64_t)r * KX_T + threadIdx.x;
-        if (i < rows)
-            atomicAdd(&h[kx_owner(keys[i], spl, n_own - 1)], (unsigned long long)pieces_of(cnt, cap, i, pf));
+        const bool live = t0 + (uint64_t)r * KX_T + threadIdx.x < rows;
+        const uint32_t o = kx_owner(rt.key[r], ls, n_own - 1);
+        if (nbits > 6 || __ballot(live && rt.big[r] > pf.cmax)) {   // split rows / many owners: per-lane adds
+            if (live) atomicAdd(&h[o], (unsigned long long)(rt.big[r] <= pf.cmax ? 1ull
+                                                             : ((uint64_t)rt.big[r] + pf.cmax - 1) / pf.cmax));
+        } else {
+            (void)wave_owner_add(h, o, live, n_own, nbits);
+        }
     }
     __syncthreads();
     for (uint32_t o = threadIdx.x; o < n_own; o += KX_T) hist[(uint64_t)o * n_tiles + blockIdx.x] = h[o];
@@ -271,60 +346,277 @@ __global__ void __launch_bounds__(KX_T) kx_pack_scatter(const uint64_t* __restri
                                                         const uint64_t* __restrict__ base,
                                                         uint64_t n_tiles, uint64_t* __restrict__ out) {
     __shared__ unsigned long long cur[KX_MAX_OWN];
-    for (uint32_t o = threadIdx.x; o < n_own; o += KX_T) cur[o] = 0;
-    __syncthreads();
+    __shared__ uint64_t ls[KX_MAX_OWN];
+    for (uint32_t o = threadIdx.x; o < n_own; o += KX_T) cur[o] = base[(uint64_t)o * n_tiles + blockIdx.x];
+    stage_splitters(spl, n_own, ls);
     const uint64_t t0 = (uint64_t)blockIdx.x * KX_TILE;
-#pragma unroll 4
+    const int nbits = owner_bits(n_own);
+    RowTile rt;
+    load_row_tile(keys, cnt, cap, rows, t0, pf, rt);
+    __syncthreads();
+#pragma unroll
     for (int r = 0; r < KX_R; ++r) {
         const uint64_t i = t0 + (uint64_t)r * KX_T + threadIdx.x;
-        if (i >= rows) continue;
-        const uint64_t key = keys[i];
-        const uint32_t o = kx_owner(key, spl, n_own - 1);
-        const uint64_t np = pieces_of(cnt, cap, i, pf);
-        uint64_t pos = base[(uint64_t)o * n_tiles + blockIdx.x] + atomicAdd(&cur[o], (unsigned long long)np);
-        uint64_t left[8];   // F <= 8 on this path
-        for (uint32_t f = 0; f < pf.F; ++f) left[f] = cnt[(uint64_t)f * cap + i];
-        for (uint64_t p = 0; p < np; ++p) {
-            uint64_t v = key;
-            for (uint32_t f = 0; f < pf.F; ++f) {
-                const uint64_t c = left[f] < pf.cmax ? left[f] : pf.cmax;
-                left[f] -= c;
-                v |= c << (pf.kb + (int)f * pf.cb);
+        const bool live = i < rows;
+        const uint32_t o = kx_owner(rt.key[r], ls, n_own - 1);
+        if (nbits > 6 || __ballot(live && rt.big[r] > pf.cmax)) {   // per-lane reservation, pieces one by one
+            if (!live) continue;
+            const uint64_t np = pieces_of(cnt, cap, i, pf);
+            uint64_t pos = atomicAdd(&cur[o], (unsigned long long)np);
+            uint64_t left[8];   // F <= 8 on this path
+            for (uint32_t f = 0; f < pf.F; ++f) left[f] = cnt[(uint64_t)f * cap + i];
+            for (uint64_t p = 0; p < np; ++p) {
+                uint64_t v = rt.key[r];
+                for (uint32_t f = 0; f < pf.F; ++f) {
+                    const uint64_t c = left[f] < pf.cmax ? left[f] : pf.cmax;
+                    left[f] -= c;
+                    v |= c << (pf.kb + (int)f * pf.cb);
+                }
+                out[pos++] = v;
             }
-            out[pos++] = v;
+        } else {
+            const unsigned long long at = wave_owner_add(cur, o, live, n_own, nbits);
+            if (live) out[at] = rt.pk[r];
         }
     }
 }
 
-// keep[i] = 1 iff piece i heads a key run and some file's summed count passes the drop.
-__global__ void kx_pk_flags(const uint64_t* __restrict__ sk, uint64_t n, PackFmt pf, uint64_t kmask, uint32_t min_c,
-                            uint64_t* __restrict__ keep) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    uint64_t k = 0;
-    if (i < n && (i == 0 || ((sk[i] ^ sk[i - 1]) & kmask) != 0)) {
-        const uint64_t key = sk[i] & kmask;
-        for (uint32_t f = 0; f < pf.F && !k; ++f) {
-            uint64_t c = 0;
-            for (uint64_t j = i; j < n && (sk[j] & kmask) == key; ++j) c += (sk[j] >> (pf.kb + (int)f * pf.cb)) & pf.cmax;
-            k = c >= min_c;
-        }
-    }
-    keep[i] = k;
+// ---------------------------------------------------------------- owner merge by hash buckets
+// The owner's pieces (any order, one key split over up to one piece per sender and count
+// overflow) are grouped by the top mb bits of the counting mix (kmer_dev.hpp Mix: the senders'
+// rows come out of kc_count_s in runs of one fine bucket, so with mb = their fb the scatter
+// moves whole runs) — kx_mb_hist counts them per
+// (bucket, tile), one exclusive scan gives every (bucket, tile) its output run, kx_mb_scatter
+// writes them — and each bucket (about T/2 pieces) is summed in an LDS hash table by one
+// workgroup (kx_mb_merge), which applies the per-file drop and writes the kept rows.  No sort:
+// spec_hist is order-free and the export sort (kc_select + sort_export_u64) orders the keys.
+constexpr int MB_NT = 1024;
+constexpr int MB_R = 16;                       // pieces per thread per tile
+constexpr uint64_t MB_TILE = (uint64_t)MB_NT * MB_R;
+constexpr int MB_MAXB = 14;                    // <= 16384 buckets
+constexpr int MG_NT = 512;
+constexpr int MG_R = 8;                        // pieces per thread in flight
+constexpr uint64_t MG_EMPTY = ~0ull;           // keys are < 2^60 on this path
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {   // MurmurHash3's 64-bit finaliser
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+__device__ __forceinline__ uint32_t mb_bucket(uint64_t key, const Mix& mx, int mb) {
+    return mb ? (uint32_t)(mix_fwd(key, mx) >> (mx.n - mb)) : 0u;
 }
 
-__global__ void kx_pk_emit(const uint64_t* __restrict__ sk, uint64_t n, PackFmt pf, uint64_t kmask, uint32_t min_c,
-                           const uint64_t* __restrict__ pos, uint64_t* __restrict__ rkey,
-                           uint32_t* __restrict__ rcnt, uint64_t cap) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || pos[i + 1] == pos[i]) return;
-    const uint64_t p = pos[i], key = sk[i] & kmask;
-    rkey[p] = key;
-    for (uint32_t f = 0; f < pf.F; ++f) {
-        uint64_t c = 0;
-        for (uint64_t j = i; j < n && (sk[j] & kmask) == key; ++j) c += (sk[j] >> (pf.kb + (int)f * pf.cb)) & pf.cmax;
-        const uint32_t cc = c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c;
-        rcnt[(uint64_t)f * cap + p] = cc >= min_c ? cc : 0u;
+// LDS counter add for pieces that arrive in runs of one bucket (the senders' fine-bucket
+// runs): the buckets of lane 0 and lane 63 take one add each for all their lanes, the rest
+// (a third bucket inside one wave is rare) add per lane.  Returns the lane's position.
+__device__ __forceinline__ uint32_t run_add(uint32_t* ctr, uint32_t b, bool live) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t pos = 0;
+    bool done = !live;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const uint32_t lb = __shfl(b, e ? 63 : 0, 64);
+        const uint64_t m = __ballot(!done && b == lb);
+        if (!m) continue;
+        const int first = __builtin_ctzll(m);
+        uint32_t base = 0;
+        if ((int)lane == first) base = atomicAdd(&ctr[lb], (uint32_t)__popcll(m));
+        base = __shfl(base, first, 64);
+        if (!done && b == lb) {
+            pos = base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            done = true;
+        }
+    }
+    if (!done) pos = atomicAdd(&ctr[b], 1u);
+    return pos;
+}
+
+// tot[b] += pieces of this tile in bucket b (one device atomic per nonzero bucket: the pieces
+// arrive in runs, so a tile touches few buckets).
+__global__ void __launch_bounds__(MB_NT) kx_mb_hist(const uint64_t* __restrict__ pieces, uint64_t n, uint64_t kmask,
+                                                    Mix mx, int mb, unsigned long long* __restrict__ tot) {
+    __shared__ uint32_t h[1 << MB_MAXB];
+    const uint32_t nb = 1u << mb;
+    for (uint32_t b = threadIdx.x; b < nb; b += MB_NT) h[b] = 0;
+    const uint64_t t0 = (uint64_t)blockIdx.x * MB_TILE;
+    uint64_t v[MB_R];
+#pragma unroll
+    for (int r = 0; r < MB_R; ++r) {
+        const uint64_t i = t0 + (uint64_t)r * MB_NT + threadIdx.x;
+        v[r] = i < n ? pieces[i] : 0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < MB_R; ++r) {
+        const bool live = t0 + (uint64_t)r * MB_NT + threadIdx.x < n;
+        (void)run_add(h, live ? mb_bucket(v[r] & kmask, mx, mb) : 0u, live);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += MB_NT)
+        if (h[b]) atomicAdd(&tot[b], (unsigned long long)h[b]);
+}
+
+// Pieces to their buckets: ranks within the tile in LDS, one device atomic per nonzero bucket on
+// `cursor` (initialised to the bucket starts) reserves the tile's run, then the run is written.
+__global__ void __launch_bounds__(MB_NT) kx_mb_scatter(const uint64_t* __restrict__ pieces, uint64_t n,
+                                                       uint64_t kmask, Mix mx, int mb,
+                                                       unsigned long long* __restrict__ cursor,
+                                                       uint64_t* __restrict__ out) {
+    __shared__ uint32_t cnt[1 << MB_MAXB];
+    __shared__ uint32_t start[1 << MB_MAXB];   // n < 2^32 (count_merge_packed)
+    const uint32_t nb = 1u << mb;
+    for (uint32_t b = threadIdx.x; b < nb; b += MB_NT) cnt[b] = 0;
+    const uint64_t t0 = (uint64_t)blockIdx.x * MB_TILE;
+    uint64_t v[MB_R];
+#pragma unroll
+    for (int r = 0; r < MB_R; ++r) {
+        const uint64_t i = t0 + (uint64_t)r * MB_NT + threadIdx.x;
+        v[r] = i < n ? pieces[i] : 0ull;
+    }
+    __syncthreads();
+    uint32_t bk[MB_R], at[MB_R];
+#pragma unroll
+    for (int r = 0; r < MB_R; ++r) {
+        const bool live = t0 + (uint64_t)r * MB_NT + threadIdx.x < n;
+        bk[r] = live ? mb_bucket(v[r] & kmask, mx, mb) : 0u;
+        at[r] = run_add(cnt, bk[r], live);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += MB_NT)
+        if (cnt[b]) start[b] = (uint32_t)atomicAdd(&cursor[b], (unsigned long long)cnt[b]);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < MB_R; ++r)
+        if (t0 + (uint64_t)r * MB_NT + threadIdx.x < n) out[(uint64_t)start[bk[r]] + at[r]] = v[r];
+}
+
+// One workgroup per bucket: pieces summed per key in an LDS table of T slots (u64 key + FMAX u32
+// counts), P passes over the bucket when it holds more than 3T/4 pieces (pass p takes the keys
+// whose top 8 bits of fmix64(key) fall in its share; slots from its low bits), per-file drop,
+// kept rows staged in LDS and written coalesced into the bucket's own piece range of wkey /
+// wcnt (rows <= pieces), kept[b] = its rows.  No device-wide cursor: same-address device atomics
+// serialise, one per workgroup would bound the kernel.  gstat[1] |= 1 when a table filled (the
+// host reruns with pmul doubled).
+template <int T, int FMAX>
+__global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ bstart,
+                                                     PackFmt pf, uint64_t kmask, int mb,
+                                                     uint32_t min_c, uint32_t pmul, uint64_t* __restrict__ wkey,
+                                                     uint32_t* __restrict__ wcnt, uint64_t n,
+                                                     uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
+    static_assert(T % MG_NT == 0 && T / MG_NT <= 32, "each thread owns T / MG_NT <= 32 slots");
+    __shared__ unsigned long long tkey[T];
+    __shared__ uint32_t tcnt[FMAX * T];
+    __shared__ uint32_t ws[MG_NT / 64 + 1];
+    __shared__ uint32_t s_ovf;
+    const int tid = threadIdx.x;
+    uint64_t rb = 0;   // rows written so far (uniform)
+    const uint32_t b = blockIdx.x;
+    const uint64_t a = bstart[b], e = bstart[b + 1];
+    const uint32_t F = pf.F;
+    uint32_t P = (uint32_t)(((e - a) * 4 + 3 * T - 1) / (3 * T));   // <= 3/4 load per pass
+    P = (P ? P : 1u) * pmul;
+    P = P < 256u ? P : 256u;
+    if (tid == 0) s_ovf = 0;
+    for (uint32_t p = 0; p < P; ++p) {
+        for (uint32_t j = tid; j < T; j += MG_NT) tkey[j] = MG_EMPTY;
+        for (uint32_t j = tid; j < F * T; j += MG_NT) tcnt[j] = 0;
+        __syncthreads();
+        for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)MG_NT * MG_R) {
+            uint64_t v[MG_R];
+#pragma unroll
+            for (int q = 0; q < MG_R; ++q) {   // all loads issued before the table work
+                const uint64_t i = i0 + (uint64_t)q * MG_NT + tid;
+                v[q] = i < e ? sk[i] : 0ull;
+            }
+#pragma unroll
+            for (int q = 0; q < MG_R; ++q) {
+                if (i0 + (uint64_t)q * MG_NT + tid >= e) continue;
+                const uint64_t key = v[q] & kmask, g = fmix64(key);
+                if (P > 1 && (((uint32_t)(g >> 56) * P) >> 8) != p) continue;   // this pass's share
+                uint32_t slot = (uint32_t)g & (T - 1);
+                uint32_t t = 0;
+                for (; t < T; ++t) {
+                    const unsigned long long old = atomicCAS(&tkey[slot], MG_EMPTY, (unsigned long long)key);
+                    if (old == MG_EMPTY || old == key) break;
+                    slot = (slot + 1) & (T - 1);
+                }
+                if (t == T) {
+                    s_ovf = 1;
+                    continue;
+                }
+                for (uint32_t f = 0; f < F; ++f) {
+                    const uint32_t c = (uint32_t)((v[q] >> (pf.kb + (int)f * pf.cb)) & pf.cmax);
+                    if (c) atomicAdd(&tcnt[f * T + slot], c);
+                }
+            }
+        }
+        __syncthreads();
+        if (s_ovf) {
+            if (tid == 0) atomicOr(&gstat[1], 1ull);
+            return;   // uniform: every thread read s_ovf after the barrier
+        }
+        constexpr int ES = T / MG_NT;   // slots j * MG_NT + tid: lanes on consecutive banks
+        uint32_t keep = 0;
+#pragma unroll
+        for (int j = 0; j < ES; ++j) {
+            const uint32_t s = j * MG_NT + tid;
+            bool any = false;
+            for (uint32_t f = 0; f < F; ++f) {
+                uint32_t c = tcnt[f * T + s];
+                c = c >= min_c ? c : 0u;
+                tcnt[f * T + s] = c;
+                any |= c != 0u;
+            }
+            if (tkey[s] != MG_EMPTY && any) keep |= 1u << j;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<MG_NT>((uint32_t)__popc(keep), ws, &tot);
+        // compaction in place: every source is read into registers before the barrier
+        unsigned long long kk[ES];
+        uint32_t cc[ES * FMAX];
+#pragma unroll
+        for (int j = 0; j < ES; ++j) {
+            kk[j] = tkey[j * MG_NT + tid];
+#pragma unroll
+            for (int f = 0; f < FMAX; ++f) cc[j * FMAX + f] = f < (int)F ? tcnt[f * T + j * MG_NT + tid] : 0u;
+        }
+        __syncthreads();
+        uint32_t o = ex;
+#pragma unroll
+        for (int j = 0; j < ES; ++j)
+            if ((keep >> j) & 1u) {
+                tkey[o] = kk[j];
+#pragma unroll
+                for (int f = 0; f < FMAX; ++f)
+                    if (f < (int)F) tcnt[f * T + o] = cc[j * FMAX + f];
+                ++o;
+            }
+        __syncthreads();
+        for (uint32_t j = tid; j < tot; j += MG_NT) {
+            wkey[a + rb + j] = tkey[j];
+            for (uint32_t f = 0; f < F; ++f) wcnt[(uint64_t)f * n + a + rb + j] = tcnt[f * T + j];
+        }
+        rb += tot;
+        __syncthreads();
+    }
+    if (tid == 0) kept[b] = rb;
+}
+
+// Rows of bucket b from its piece range to the scanned row offset off[b] (one workgroup per bucket).
+__global__ void __launch_bounds__(256) kx_mb_compact(const uint64_t* __restrict__ wkey, const uint32_t* __restrict__ wcnt,
+                                                     uint64_t n, uint32_t F, const uint64_t* __restrict__ bstart,
+                                                     const uint64_t* __restrict__ off, uint64_t* __restrict__ rkey,
+                                                     uint32_t* __restrict__ rcnt, uint64_t cap) {
+    const uint32_t b = blockIdx.x;
+    const uint64_t a = bstart[b], o = off[b], m = off[b + 1] - o;
+    for (uint64_t j = threadIdx.x; j < m; j += 256) {
+        rkey[o + j] = wkey[a + j];
+        for (uint32_t f = 0; f < F; ++f) rcnt[(uint64_t)f * cap + o + j] = wcnt[(uint64_t)f * n + a + j];
     }
 }
 
@@ -366,7 +658,7 @@ uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t 
         return 0;
     }
     HGA_HIP(hipMemsetAsync(hist + nh, 0, 8, c->stream));
-    c->launch("kx_partition", [&] {
+    c->launch("kx_piece_hist", [&] {
         hipLaunchKernelGGL(kx_piece_hist, dim3(n_tiles), dim3(KX_T), 0, c->stream, s.rows_key.as<uint64_t>(),
                            s.rows_cnt.as<uint32_t>(), s.rows_cap, rows, spl, n_own, pf, hist, n_tiles);
     });
@@ -382,7 +674,7 @@ uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t 
     for (uint32_t o = 0; o < n_own; ++o) total += pieces_per_owner[o];
     if (total > cap_out) return total;
     HGA_REQUIRE(out, HGA_ERR_INVALID, "output buffer required");
-    c->launch("kx_partition", [&] {
+    c->launch("kx_pack_scatter", [&] {
         hipLaunchKernelGGL(kx_pack_scatter, dim3(n_tiles), dim3(KX_T), 0, c->stream, s.rows_key.as<uint64_t>(),
                            s.rows_cnt.as<uint32_t>(), s.rows_cap, rows, spl, n_own, pf, hist, n_tiles, out);
     });
@@ -409,26 +701,65 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
     s.rows_cap = cap;
     if (n) {
         HGA_REQUIRE(pieces, HGA_ERR_INVALID, "input buffer required");
-        char* w = static_cast<char*>(s.xch2.ensure(n * 8 + (n + 1) * 8 + 64));
+        // table slots per bucket (u64 key + F u32 counts): 32 KB for F <= 2, so four workgroups share a CU
+        HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per merge");
+        const uint32_t T = F <= 2 ? 2048u : 1024u;
+        const Mix mx = make_mix(s.k);
+        int mb = 0;   // about T/2 pieces per bucket
+        while (mb < MB_MAXB && mb < (int)mx.n && ((uint64_t)T / 2 << mb) < n) ++mb;
+        const uint64_t nb = 1ull << mb;
+        const uint64_t n_tiles = kx_blocks(n, MB_TILE);
+        char* w = static_cast<char*>(s.xch2.ensure(n * (16 + 4 * F) + (3 * nb + 2) * 8 + 16 + 64));
         uint64_t* sk = reinterpret_cast<uint64_t*>(w);
-        uint64_t* keep = reinterpret_cast<uint64_t*>(w + n * 8);
-        HGA_HIP(hipMemcpyAsync(sk, pieces, n * 8, hipMemcpyDeviceToDevice, c->stream));
-        radix_sort_u64(c, sk, nullptr, n, pf.kb, s.scratch);   // by the key bits only; counts ride along
-        c->launch("kx_merge", [&] {
-            hipLaunchKernelGGL(kx_pk_flags, dim3(kx_blocks(n + 1, 256)), dim3(256), 0, c->stream, sk, n, pf, kmask,
-                               min_c, keep);
+        uint64_t* wkey = sk + n;                                     // rows per bucket range
+        auto* tot = reinterpret_cast<unsigned long long*>(wkey + n);   // nb + 1: scanned = bucket starts
+        auto* cursor = tot + nb + 1;
+        auto* gstat = cursor + nb;
+        uint64_t* kept = reinterpret_cast<uint64_t*>(gstat + 2);     // nb + 1: scanned = row offsets
+        uint32_t* wcnt = reinterpret_cast<uint32_t*>(kept + nb + 1);
+        HGA_HIP(hipMemsetAsync(tot, 0, (nb + 1) * 8, c->stream));
+        c->launch("kx_mb_hist", [&] {
+            hipLaunchKernelGGL(kx_mb_hist, dim3(n_tiles), dim3(MB_NT), 0, c->stream, pieces, n, kmask, mx, mb, tot);
         });
-        c->check_launch("kx_pk_flags");
-        exclusive_scan_u64(c, keep, n + 1, s.scratch);
-        c->launch("kx_merge", [&] {
-            hipLaunchKernelGGL(kx_pk_emit, dim3(kx_blocks(n, 256)), dim3(256), 0, c->stream, sk, n, pf, kmask, min_c,
-                               keep, s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap);
+        c->check_launch("kx_mb_hist");
+        exclusive_scan_u64(c, reinterpret_cast<uint64_t*>(tot), nb + 1, s.scratch);
+        HGA_HIP(hipMemcpyAsync(cursor, tot, nb * 8, hipMemcpyDeviceToDevice, c->stream));
+        c->launch("kx_mb_scatter", [&] {
+            hipLaunchKernelGGL(kx_mb_scatter, dim3(n_tiles), dim3(MB_NT), 0, c->stream, pieces, n, kmask, mx, mb,
+                               cursor, sk);
         });
-        c->check_launch("kx_pk_emit");
-        uint64_t rows = 0;
-        HGA_HIP(hipMemcpyAsync(&rows, keep + n, 8, hipMemcpyDeviceToHost, c->stream));
+        c->check_launch("kx_mb_scatter");
+        const uint64_t* hist = reinterpret_cast<const uint64_t*>(tot);
+        unsigned long long* hs = static_cast<unsigned long long*>(c->pinned.ensure(16));
+        for (uint32_t pmul = 1;; pmul *= 2) {
+            HGA_REQUIRE(pmul <= 256, HGA_ERR_OOM, "owner merge: a bucket does not fit its LDS table");
+            HGA_HIP(hipMemsetAsync(gstat, 0, 16, c->stream));
+            c->launch("kx_mb_merge", [&] {
+                if (F <= 2)
+                    hipLaunchKernelGGL((kx_mb_merge<2048, 2>), dim3(nb), dim3(MG_NT), 0, c->stream, sk, hist,
+                                       pf, kmask, mb, min_c, pmul, wkey, wcnt, n, kept, gstat);
+                else if (F <= 4)
+                    hipLaunchKernelGGL((kx_mb_merge<1024, 4>), dim3(nb), dim3(MG_NT), 0, c->stream, sk, hist,
+                                       pf, kmask, mb, min_c, pmul, wkey, wcnt, n, kept, gstat);
+                else
+                    hipLaunchKernelGGL((kx_mb_merge<1024, 8>), dim3(nb), dim3(MG_NT), 0, c->stream, sk, hist,
+                                       pf, kmask, mb, min_c, pmul, wkey, wcnt, n, kept, gstat);
+            });
+            c->check_launch("kx_mb_merge");
+            HGA_HIP(hipMemcpyAsync(hs, gstat, 16, hipMemcpyDeviceToHost, c->stream));
+            c->sync();
+            if (!hs[1]) break;
+        }
+        HGA_HIP(hipMemsetAsync(kept + nb, 0, 8, c->stream));
+        exclusive_scan_u64(c, kept, nb + 1, s.scratch);
+        c->launch("kx_mb_compact", [&] {
+            hipLaunchKernelGGL(kx_mb_compact, dim3(nb), dim3(256), 0, c->stream, wkey, wcnt, n, F, hist, kept,
+                               s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap);
+        });
+        c->check_launch("kx_mb_compact");
+        HGA_HIP(hipMemcpyAsync(hs, kept + nb, 8, hipMemcpyDeviceToHost, c->stream));
         c->sync();
-        s.rows = rows;
+        s.rows = hs[0];
     }
     s.min_per_file = min_c;
     s.ran = true;

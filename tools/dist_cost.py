@@ -28,7 +28,8 @@ def main():
     ctx.count_add(1, rb.seq)
     e = hga_dist.HgaEngine(ctx, bench.K, 2, "cuda:0")
     spl = hga_dist.owner_splitters(bench.K, a.owners)
-    names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kx_partition", "kx_merge",
+    names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kx_partition", "kx_merge", "kx_piece_hist",
+             "kx_pack_scatter", "kx_mb_hist", "kx_mb_scatter", "kx_mb_merge", "kx_mb_compact",
              "kc_spec_hist", "kc_select", "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
     t = {"count_local": 0.0, "partition": 0.0, "merge": 0.0, "hist+select": 0.0}
     for rep in range(a.reps + 1):
