@@ -175,3 +175,58 @@ def test_packed_partition_merge_equals_oracle(k, G, min_c):
     assert np.array_equal(counts, rc)
     if k == 27:
         assert int(counts.max()) > 31
+
+
+def _mix_inv(h, k):
+    """Inverse of kmer_dev.hpp's Mix on 2k bits (the owner merge bins pieces by its top bits)."""
+    n = 2 * k
+    mask = np.uint64((1 << n) - 1)
+    s = np.uint64((n + 1) // 2)
+    c1 = 0x9E3779B97F4A7C15
+    c1i = pow(c1, -1, 1 << 64)
+    h = h ^ (h >> s)
+    return (h * np.uint64(c1i)) & mask
+
+
+@pytest.mark.parametrize("skew", [False, True])
+def test_merge_packed_many_pieces(skew):
+    """Owner merge at scale against a numpy group-by: 3 M pieces (many buckets, repeated keys,
+    split rows); with skew, a twelfth of them in ONE bucket of the merge's mix binning, so that
+    bucket is summed in several passes over its LDS table."""
+    k, F, min_c = 19, 2, 2
+    rng = np.random.default_rng(7)
+    n = 3_000_000
+    n_keys = 1_200_000
+    if skew:
+        mb = 12   # the merge's bucket bits for this n (about 1024 pieces per bucket)
+        low = rng.integers(0, 1 << (2 * k - mb), n_keys // 12, dtype=np.uint64)
+        hot = _mix_inv((np.uint64(5) << np.uint64(2 * k - mb)) | low, k)
+        keys = np.concatenate([rng.integers(0, 1 << (2 * k), n_keys - len(hot), dtype=np.uint64), hot])
+    else:
+        keys = rng.integers(0, 1 << (2 * k), n_keys, dtype=np.uint64)
+    pk = keys[rng.integers(0, n_keys, n)]
+    cb = (64 - 2 * k) // F
+    cnt = rng.integers(0, 4, (n, F)).astype(np.uint64)
+    cnt[rng.random(n) < 0.001, 0] = (1 << cb) - 1          # saturated pieces of split rows
+    cnt[cnt.sum(axis=1) == 0, 1] = 1
+    pieces = pk.copy()
+    for f in range(F):
+        pieces |= cnt[:, f] << np.uint64(2 * k + f * cb)
+    u, inv = np.unique(pk, return_inverse=True)
+    tot = np.zeros((len(u), F), np.int64)
+    for f in range(F):
+        np.add.at(tot[:, f], inv, cnt[:, f].astype(np.int64))
+    tot[tot < min_c] = 0
+    keep = tot.any(axis=1)
+    c = hga.Ctx(0)
+    try:
+        c.count_begin(k, F)
+        assert c.count_pack_bits() == cb
+        buf = torch.from_numpy(pieces.view(np.int64)).to("cuda:0")
+        torch.cuda.synchronize()
+        c.count_merge_packed(buf.data_ptr(), n, min_c)
+        kk, cc = c.rows()
+    finally:
+        c.close()
+    assert np.array_equal(kk, u[keep])
+    assert np.array_equal(cc.reshape(-1, F).astype(np.int64), tot[keep])
