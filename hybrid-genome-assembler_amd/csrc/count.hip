@@ -425,6 +425,86 @@ __global__ void kc_fs(const uint64_t* __restrict__ off, const BinFile* __restric
     fs[i] = f == F ? off[(b + 1) * W] : off[b * W + files[f].w0];
 }
 
+// ---------------------------------------------------------------- pass B3 (large inputs)
+// Inputs with far more than 2^MAX_FB x 65536 instances (a C4 rank shard: ~800 K per fine bucket)
+// would make every count workgroup re-read its bucket once per LDS-sized sub-range.  One more
+// level instead: one workgroup per fine bucket b splits each file's run by the top fb3 bits of
+// the remainder into S = 2^fb3 sub-buckets, laid out (sub-bucket, file)-major, and strips those
+// bits, so the count kernels run unchanged on nb * S buckets of rbits - fb3 bit remainders
+// (((b << fb3 | s) << (rbits - fb3)) | rem == (b << rbits) | v).  fs3 is fs for the sub-buckets.
+constexpr int NT_3 = 1024;
+constexpr int R_3 = 8;   // elements per thread in flight
+constexpr uint32_t MAX_SF3 = 4096;
+template <class E>
+__global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, const uint64_t* __restrict__ fs,
+                                                  uint32_t F, uint32_t fb3, uint32_t rbits, E* __restrict__ out,
+                                                  uint64_t* __restrict__ fs3) {
+    __shared__ uint32_t h[MAX_SF3];
+    __shared__ uint32_t ws[NT_3 / 64 + 1];
+    const uint32_t tid = threadIdx.x, b = blockIdx.x, S = 1u << fb3, SF = S * F;
+    const uint64_t* f = fs + (uint64_t)b * (F + 1);
+    const uint32_t sh = rbits - fb3;
+    const E rm = (E)(((E)1 << sh) - 1);
+    for (uint32_t j = tid; j < SF; j += NT_3) h[j] = 0;
+    __syncthreads();
+    for (uint32_t ff = 0; ff < F; ++ff) {
+        const uint64_t a = f[ff], e = f[ff + 1];
+        for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)NT_3 * R_3) {
+            E v[R_3];
+#pragma unroll
+            for (int q = 0; q < R_3; ++q) {
+                const uint64_t i = i0 + (uint64_t)q * NT_3 + tid;
+                v[q] = i < e ? in[i] : (E)0;
+            }
+#pragma unroll
+            for (int q = 0; q < R_3; ++q)
+                if (i0 + (uint64_t)q * NT_3 + tid < e) atomicAdd(&h[(uint32_t)(v[q] >> sh) * F + ff], 1u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan in (sub-bucket, file) order: 4 consecutive entries per thread (SF <= 4096)
+    uint32_t loc[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t j = tid * 4 + q;
+        loc[q] = j < SF ? h[j] : 0u;
+        sum += loc[q];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<NT_3>(sum, ws, &tot);
+    const uint64_t base = f[0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t j = tid * 4 + q;
+        if (j < SF) {
+            h[j] = run;
+            fs3[((uint64_t)b * S + j / F) * (F + 1) + j % F] = base + run;
+            run += loc[q];
+        }
+    }
+    __syncthreads();
+    for (uint32_t sb = tid; sb < S; sb += NT_3)
+        fs3[((uint64_t)b * S + sb) * (F + 1) + F] = sb + 1 < S ? base + h[(sb + 1) * F] : f[F];
+    __syncthreads();
+    for (uint32_t ff = 0; ff < F; ++ff) {
+        const uint64_t a = f[ff], e = f[ff + 1];
+        for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)NT_3 * R_3) {
+            E v[R_3];
+#pragma unroll
+            for (int q = 0; q < R_3; ++q) {
+                const uint64_t i = i0 + (uint64_t)q * NT_3 + tid;
+                v[q] = i < e ? in[i] : (E)0;
+            }
+#pragma unroll
+            for (int q = 0; q < R_3; ++q)
+                if (i0 + (uint64_t)q * NT_3 + tid < e) {
+                    const uint32_t p = atomicAdd(&h[(uint32_t)(v[q] >> sh) * F + ff], 1u);
+                    out[base + p] = v[q] & rm;
+                }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- pass B2
 // One workgroup per level-1 block: the next fb2 bits pick the fine bucket (<= 64-way,
 // ranked through LDS so each bucket's run is one coalesced segment).
@@ -1966,15 +2046,54 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
 #undef HGA_REBIN
     });
     c->check_launch("kc_rebin");
+    // B3: one more split level for inputs whose fine buckets hold far more than one LDS table
+    // (the per-bucket estimate, total bytes >> fb, passes 2 x per_bucket only with fb at MAX_FB)
+    uint32_t fb3 = 0;
+    {
+        const uint64_t avg = total_bytes >> fb;
+        const char* te = std::getenv("HGA_SPLIT3_TARGET");
+        const char* fe = std::getenv("HGA_SPLIT3_FORCE");   // tests: split small inputs too
+        const uint64_t target = te ? std::strtoull(te, nullptr, 10) : 32768;
+        if (fe) {
+            const uint32_t want = (uint32_t)std::atoi(fe);
+            while (fb3 < want && fb3 < 8 && ((2u << fb3) * F) <= MAX_SF3 && kp.rbits - fb3 > 1) ++fb3;
+        } else if (avg > 2 * per_bucket && fb == MAX_FB) {
+            while (fb3 < 8 && (avg >> fb3) > target && ((2u << fb3) * F) <= MAX_SF3 && kp.rbits - fb3 > 16) ++fb3;
+        }
+    }
+    if (fb3) {
+        const uint32_t S = 1u << fb3;
+        void* binned3 = s.binned3.ensure(std::max<size_t>(total_bytes, 1) * esz);
+        uint64_t* fs3 = static_cast<uint64_t*>(s.file_start3.ensure((size_t)nb * S * (F + 1) * 8));
+        c->launch("kc_split3", [&] {
+            if (e32)
+                hipLaunchKernelGGL(kc_split3<uint32_t>, dim3(nb), dim3(NT_3), 0, c->stream,
+                                   static_cast<const uint32_t*>(binned), fs, F, fb3, kp.rbits,
+                                   static_cast<uint32_t*>(binned3), fs3);
+            else
+                hipLaunchKernelGGL(kc_split3<uint64_t>, dim3(nb), dim3(NT_3), 0, c->stream,
+                                   static_cast<const uint64_t*>(binned), fs, F, fb3, kp.rbits,
+                                   static_cast<uint64_t*>(binned3), fs3);
+        });
+        c->check_launch("kc_split3");
+        kp.fb += fb3;
+        kp.nb <<= fb3;
+        kp.rbits -= fb3;
+        kp.rmask = kp.rbits >= 64 ? ~0ull : ((1ull << kp.rbits) - 1);
+        binned = binned3;
+        fs = fs3;
+        s.buckets = kp.nb;
+    }
+    const uint32_t nbc = kp.nb;   // count buckets
     // C: per-bucket count
     if (packed && e32) {
-        uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nb * 4));
+        uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nbc * 4));
         c->launch("kc_count", [&] {
-            hipLaunchKernelGGL(HGA_COUNT_SOA ? kc_count_s : kc_count_p, dim3(nb), dim3(NT_P), 0, c->stream,
+            hipLaunchKernelGGL(HGA_COUNT_SOA ? kc_count_s : kc_count_p, dim3(nbc), dim3(NT_P), 0, c->stream,
                                static_cast<const uint32_t*>(binned), fs, F, min_per_file, kp, s.rows_key.as<uint64_t>(),
                                s.rows_cnt.as<uint32_t>(), cap, gstat, blist);
             // buckets with a per-file run >= 65536 (listed in blist, count in gstat[5])
-            hipLaunchKernelGGL(kc_count<uint32_t>, dim3(std::min<uint32_t>(nb, (uint32_t)c->num_cu)), dim3(NT_C), 0,
+            hipLaunchKernelGGL(kc_count<uint32_t>, dim3(std::min<uint32_t>(nbc, (uint32_t)c->num_cu)), dim3(NT_C), 0,
                                c->stream, static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
                                s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat,
                                (const uint32_t*)blist);
@@ -1983,11 +2102,11 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     } else
     c->launch("kc_count", [&] {
         if (e32)
-            hipLaunchKernelGGL(kc_count<uint32_t>, dim3(nb), dim3(NT_C), 0, c->stream,
+            hipLaunchKernelGGL(kc_count<uint32_t>, dim3(nbc), dim3(NT_C), 0, c->stream,
                                static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
                                s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, (const uint32_t*)nullptr);
         else
-            hipLaunchKernelGGL(kc_count<uint64_t>, dim3(nb), dim3(NT_C), 0, c->stream,
+            hipLaunchKernelGGL(kc_count<uint64_t>, dim3(nbc), dim3(NT_C), 0, c->stream,
                                static_cast<const uint64_t*>(binned), fs, F, T, maxload, min_per_file, kp,
                                s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, (const uint32_t*)nullptr);
     });

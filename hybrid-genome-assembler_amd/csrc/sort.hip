@@ -587,6 +587,12 @@ void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t
                      const uint32_t* h_hist, DevBuf& scratch) {
     if (n <= 1) return;
     HGA_REQUIRE(shift >= 0 && shift <= 54 && n < (1ull << 32), HGA_ERR_INVALID, "export sort: bad width");
+    uint32_t n_big = 0;
+    for (int d = 0; d < 256; ++d) n_big += h_hist[d] > (uint32_t)SS_CAP;
+    // Many segments past the LDS (a large export, e.g. a C4 rank shard's): one global LSD sort of
+    // the low `shift` bits first, then the stable digit pass below finishes the order.
+    const bool global_low = n_big > 8;
+    if (global_low && shift > 0) radix_sort_u64(c, keys, nullptr, n, shift, scratch);
     const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     const size_t kb = ((n * 8 + 255) & ~255ull), stb = (size_t)n_tiles * 256 * 4, tcb = 64;
     char* base = static_cast<char*>(scratch.ensure(kb + stb + tcb));
@@ -600,6 +606,10 @@ void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t
                            dbase);
     });
     c->check_launch("rs_onesweep");
+    if (global_low) {
+        HGA_HIP(hipMemcpyAsync(keys, k2, n * 8, hipMemcpyDeviceToDevice, c->stream));
+        return;
+    }
     c->launch("radix_segsort", [&] {
         hipLaunchKernelGGL(ss_segsort, dim3(256), dim3(SS_T), 0, c->stream, k2, keys, d_hist, shift);
     });

@@ -225,3 +225,29 @@ def test_count_add_rows_only(gpu_ctx):
 def hga_err():
     import hga
     return hga.HgaError
+
+
+@pytest.mark.parametrize("fb3,k,n_files", [(1, 19, 2), (4, 19, 2), (8, 25, 1), (3, 31, 3), (2, 32, 2)])
+def test_count_split3_forced_vs_oracle(gpu_ctx, monkeypatch, fb3, k, n_files):
+    # the third partition level (kc_split3, normally only for inputs of a C4 rank shard's size)
+    # forced onto small inputs: sub-buckets of u32 and u64 remainders, 1-3 files
+    monkeypatch.setenv("HGA_SPLIT3_FORCE", str(fb3))
+    streams = random_streams(200 + fb3, n_files, 400, 120, "ACGTACGTACGTNacgt")
+    o = oracle.count_pipeline(streams, k, 2, 6)
+    r = run_gpu(gpu_ctx, streams, k, 2, 6)
+    assert_same(r, o)
+    assert r["stats"].buckets > 1
+
+
+def test_count_split3_c1_scale(gpu_ctx, hga_mod, monkeypatch):
+    monkeypatch.setenv("HGA_SPLIT3_FORCE", "6")
+    ga = hga_mod.gen_genome(500_000, 1)
+    gb = hga_mod.gen_haplotype(ga, 0.03, 0, 2)
+    streams = [hga_mod.gen_art(ga, 100_000, 150, 3).seq, hga_mod.gen_art(gb, 100_000, 150, 4).seq]
+    o = {"dumps": [oracle.count_stream(s, 19, 2, threads=8) for s in streams]}
+    o["keys"], o["counts"] = oracle.merge(o["dumps"])
+    o["hist"] = oracle.specificity(o["counts"], oracle.THRESHOLDS)
+    o["selected"], o["n_discr"] = oracle.select(o["keys"], o["counts"], 10, 25)
+    r = run_gpu(gpu_ctx, streams, 19, 10, 25)
+    assert_same(r, o)
+    assert r["stats"].buckets == 64 * r["stats"].buckets // 64 and r["stats"].buckets >= 64

@@ -85,3 +85,20 @@ def test_export_sort_owner_like_ranges(gpu_ctx, lo, width):
     want = keys[(counts >= 10) & (counts <= 25)]
     assert np.array_equal(sel, want)
     assert nd == len(want) and np.all(flags == 1)
+
+
+def test_export_sort_few_big_segments(gpu_ctx):
+    # 150 K keys spread over the code space plus 60 K inside one top digit: ONE segment passes the
+    # LDS capacity (per-segment global sort) while the rest are sorted in LDS
+    rng = np.random.default_rng(5)
+    spread = rng.integers(0, 1 << 38, 150_000, dtype=np.uint64)
+    hot = rng.integers(77 << 30, (77 << 30) + (1 << 29), 60_000, dtype=np.uint64)
+    keys = np.unique(np.concatenate([spread, hot]))
+    counts = rng.integers(10, 30, len(keys), dtype=np.uint32)
+    gpu_ctx.count_begin(19, 1)
+    gpu_ctx.count_add_rows(0, keys, counts)
+    gpu_ctx.count_run(2)
+    sel, flags, nd = gpu_ctx.select(10, 25)
+    want = keys[(counts >= 10) & (counts <= 25)]
+    assert np.array_equal(sel, want)
+    assert nd == len(want) and np.all(flags == 1)
