@@ -439,7 +439,10 @@ template <class E>
 __global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, const uint64_t* __restrict__ fs,
                                                   uint32_t F, uint32_t fb3, uint32_t rbits, E* __restrict__ out,
                                                   uint64_t* __restrict__ fs3) {
-    __shared__ uint32_t h[MAX_SF3];
+    constexpr uint32_t BT = (uint32_t)NT_3 * R_3;   // batch: staged in LDS, written in sub-bucket runs
+    __shared__ uint32_t h[MAX_SF3];                   // counts, then output cursors, per (sub-bucket, file)
+    __shared__ uint32_t bc[256], bo[256];             // per-batch sub-bucket counts / offsets
+    __shared__ E stage[BT];
     __shared__ uint32_t ws[NT_3 / 64 + 1];
     const uint32_t tid = threadIdx.x, b = blockIdx.x, S = 1u << fb3, SF = S * F;
     const uint64_t* f = fs + (uint64_t)b * (F + 1);
@@ -449,7 +452,7 @@ __global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, cons
     __syncthreads();
     for (uint32_t ff = 0; ff < F; ++ff) {
         const uint64_t a = f[ff], e = f[ff + 1];
-        for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)NT_3 * R_3) {
+        for (uint64_t i0 = a; i0 < e; i0 += BT) {
             E v[R_3];
 #pragma unroll
             for (int q = 0; q < R_3; ++q) {
@@ -485,22 +488,44 @@ __global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, cons
     __syncthreads();
     for (uint32_t sb = tid; sb < S; sb += NT_3)
         fs3[((uint64_t)b * S + sb) * (F + 1) + F] = sb + 1 < S ? base + h[(sb + 1) * F] : f[F];
-    __syncthreads();
     for (uint32_t ff = 0; ff < F; ++ff) {
         const uint64_t a = f[ff], e = f[ff + 1];
-        for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)NT_3 * R_3) {
+        for (uint64_t i0 = a; i0 < e; i0 += BT) {
             E v[R_3];
+            uint32_t sb[R_3], rk[R_3];
 #pragma unroll
             for (int q = 0; q < R_3; ++q) {
                 const uint64_t i = i0 + (uint64_t)q * NT_3 + tid;
                 v[q] = i < e ? in[i] : (E)0;
             }
+            for (uint32_t j = tid; j < S; j += NT_3) bc[j] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < R_3; ++q) {
+                sb[q] = (uint32_t)(v[q] >> sh);
+                rk[q] = i0 + (uint64_t)q * NT_3 + tid < e ? atomicAdd(&bc[sb[q]], 1u) : 0u;
+            }
+            __syncthreads();
+            {   // batch offsets per sub-bucket (S <= 256: the first 256 threads)
+                const uint32_t c0 = tid < S ? bc[tid] : 0u;
+                uint32_t bt;
+                const uint32_t ex = block_excl_scan<NT_3>(c0, ws, &bt);
+                if (tid < S) bo[tid] = ex;
+            }
+            __syncthreads();
 #pragma unroll
             for (int q = 0; q < R_3; ++q)
-                if (i0 + (uint64_t)q * NT_3 + tid < e) {
-                    const uint32_t p = atomicAdd(&h[(uint32_t)(v[q] >> sh) * F + ff], 1u);
-                    out[base + p] = v[q] & rm;
-                }
+                if (i0 + (uint64_t)q * NT_3 + tid < e) stage[bo[sb[q]] + rk[q]] = v[q];
+            __syncthreads();
+            const uint32_t m = (uint32_t)((e - i0) < (uint64_t)BT ? (e - i0) : BT);
+            for (uint32_t j = tid; j < m; j += NT_3) {   // staged order: one run per sub-bucket
+                const E x = stage[j];
+                const uint32_t t = (uint32_t)(x >> sh);
+                out[base + h[t * F + ff] + (j - bo[t])] = x & rm;
+            }
+            __syncthreads();
+            for (uint32_t t = tid; t < S; t += NT_3) h[t * F + ff] += bc[t];
+            __syncthreads();
         }
     }
 }
