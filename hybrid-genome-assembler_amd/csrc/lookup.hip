@@ -31,6 +31,7 @@ namespace {
 constexpr int LK_T = 256;
 constexpr int LK_P = 32;                  // window ends per thread (frame of 4 words)
 constexpr int LK_QN = 256;                // filter-pass queue entries per wave
+constexpr int LK_ST = 2048;               // emit pass: hits per tile staged in LDS (more: direct stores)
 constexpr uint64_t EMPTY_KEY = ~0ull;     // never canonical: min(fwd, rc) of all-T is 0
 constexpr int SB_PAD = 1;                 // leading zero words of the read-start bitmap
 
@@ -392,11 +393,39 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
     uint32_t hits = p0 < nbases ? hmask[gt] : 0u;
     uint32_t tot;
     const uint32_t ex = block_excl_scan<LK_T>((uint32_t)__popc(hits), ws, &tot);
-    if (!hits) return;
-    uint64_t o = tile_cnt[blockIdx.x] + ex;
+    if (tot == 0) return;   // uniform
+    const uint64_t tb = tile_cnt[blockIdx.x];
     // read containing p0 (p0 is 32-aligned): precomputed per word, no search
-    uint64_t r = word_read[p0 / 32], re = offs[r + 1];
+    uint64_t r = 0, re = 0;
+    if (hits) {
+        r = word_read[p0 / 32];
+        re = offs[r + 1];
+    }
     const uint32_t* __restrict__ wk = win_kid + gt * LK_P;
+    if (tot <= (uint32_t)LK_ST) {
+        // the tile's hits staged in LDS at their tile offsets, then written as three coalesced runs
+        // (each lane's hits are consecutive in the output: direct stores would be 4-B scatters)
+        __shared__ uint32_t s_r[LK_ST], s_k[LK_ST], s_p[LK_ST];
+        uint32_t o = ex;
+        while (hits) {
+            const int j = __builtin_ctz(hits);
+            hits &= hits - 1u;
+            const uint64_t e = p0 + j;
+            while (re <= e) re = offs[++r + 1];
+            s_r[o] = (uint32_t)r;
+            s_k[o] = wk[j];
+            s_p[o] = (uint32_t)(e + 1 - offs[r]);
+            ++o;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < tot; i += LK_T) {
+            h_read[tb + i] = s_r[i];
+            h_kid[tb + i] = s_k[i];
+            h_pos[tb + i] = s_p[i];
+        }
+        return;
+    }
+    uint64_t o = tb + ex;
     while (hits) {
         const int j = __builtin_ctz(hits);
         hits &= hits - 1u;
