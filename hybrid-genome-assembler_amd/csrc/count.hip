@@ -2083,7 +2083,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
             const uint32_t want = (uint32_t)std::atoi(fe);
             while (fb3 < want && fb3 < 8 && ((2u << fb3) * F) <= MAX_SF3 && kp.rbits - fb3 > 1) ++fb3;
         } else if (avg > 2 * per_bucket && fb == MAX_FB) {
-            while (fb3 < 8 && (avg >> fb3) > target && ((2u << fb3) * F) <= MAX_SF3 && kp.rbits - fb3 > 16) ++fb3;
+            while (fb3 < 8 && (avg >> fb3) > target && ((2u << fb3) * F) <= MAX_SF3 && kp.rbits - fb3 > 10) ++fb3;
         }
     }
     if (fb3) {

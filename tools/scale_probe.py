@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--cov", type=float, default=30.0)
     ap.add_argument("--div", type=float, default=0.005)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--k", type=str, default="19", help="comma-separated k values (SURVEY.md C5: 15,17,19,21)")
     a = ap.parse_args()
     t0 = time.time()
     ga = hga.gen_genome(a.len, 11)
@@ -29,11 +30,16 @@ def main():
     rb = hga.gen_art(gb, n, 150, 14)
     print(f"generated {2 * n} reads, {len(ra.seq) + len(rb.seq)} bytes in {time.time() - t0:.1f}s", flush=True)
     ctx = hga.Ctx(0)
-    ctx.count_begin(19, 2)
+    for k in [int(x) for x in a.k.split(",")]:
+        run_k(ctx, k, ra, rb, a.reps)
+    ctx.close()
+
+
+def run_k(ctx, k, ra, rb, reps):
+    ctx.count_begin(k, 2)
     ctx.count_add(0, ra.seq)
     ctx.count_add(1, rb.seq)
-    del ra, rb
-    for rep in range(a.reps):
+    for rep in range(reps):
         ctx.profile(True)
         ctx.profile_reset()
         ctx.sync()
@@ -47,16 +53,15 @@ def main():
         names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
                  "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
         ker = {nm: round(ctx.profile_get(nm)[0], 3) for nm in names if ctx.profile_get(nm)[1]}
-        print(f"rep {rep}: {ms:.2f} ms, {st.instances / ms / 1e6:.1f} G k-mers/s, instances {st.instances}, "
+        print(f"k={k} rep {rep}: {ms:.2f} ms, {st.instances / ms / 1e6:.1f} G k-mers/s, instances {st.instances}, "
               f"rows {st.distinct_rows}, buckets {st.buckets}, max_split {st.max_split}, selected {sel} {ker}",
               flush=True)
     ctx.count_run(1)
     st = ctx.count_stats()
     keys, cnts = ctx.rows()
     tot = int(cnts.astype("uint64").sum())
-    print(f"min-1 rows {st.distinct_rows}, sum of counts {tot}, instances {st.instances}, identity "
+    print(f"k={k} min-1 rows {st.distinct_rows}, sum of counts {tot}, instances {st.instances}, identity "
           f"{'OK' if tot == st.instances else 'FAIL'}", flush=True)
-    ctx.close()
 
 
 if __name__ == "__main__":
