@@ -474,51 +474,179 @@ __global__ void lk_big_reads(const uint64_t* __restrict__ hptr, uint64_t n, uint
 }
 
 // Per-read sort of the (read << kbits | KmerID, position) pairs: one workgroup per read with
-// 2 <= hits <= CAP, bitonic in LDS on (KmerID << 32 | position) — unique inside a read and
-// ordered like the stable (read, KmerID) sort with window order kept among equal ids
-// (ReadClusteringEngine.cpp:262-272: sorted ids; :267 first occurrence).
-// Element i lives with thread i % NT, so partners at distance j < 64 are in the same wave: those
-// stages need no workgroup barrier (a wave's LDS accesses are ordered).  `list` (optional)
-// names the reads to sort.
-template <int NT, int CAP>
+// 2 <= hits <= NT * IPT.  The hits of a read arrive in window order (positions ascending), so a
+// STABLE sort by KmerID alone gives the (KmerID, position) order of the stable (read, KmerID)
+// sort (ReadClusteringEngine.cpp:262-272: sorted ids; :267 first occurrence): LSD passes over
+// 8-bit digits of the KmerID in LDS, ranks by ballot-matched digits inside each wave (items in
+// (row, lane) order, waves in order).  `list` (optional) names the reads to sort.
+template <int NT, int IPT>
 __global__ void __launch_bounds__(NT) lk_segsort(const uint64_t* __restrict__ hptr, uint64_t nreads, int kbits,
                                                  uint64_t* __restrict__ sk, uint32_t* __restrict__ sv,
                                                  uint32_t lo_excl, const uint32_t* __restrict__ list) {
-    __shared__ uint64_t v[CAP];
+    static_assert(NT >= 256 && NT % 64 == 0, "digit scan: one thread per digit");
+    constexpr int NW = NT / 64, CAP = NT * IPT;
+    __shared__ uint64_t buf[CAP];
+    __shared__ uint32_t wcnt[NW][256];
+    __shared__ uint32_t ws[NW + 1];
     const uint64_t r = list ? list[blockIdx.x] : blockIdx.x;
     if (r >= nreads) return;
-    const uint64_t b = hptr[r], cnt = hptr[r + 1] - b;
-    if (cnt <= lo_excl || cnt > (uint64_t)CAP) return;
-    uint32_t P = 2;
-    while (P < cnt) P <<= 1;
+    const uint64_t b = hptr[r], cnt64 = hptr[r + 1] - b;
+    if (cnt64 <= lo_excl || cnt64 > (uint64_t)CAP) return;
+    const uint32_t cnt = (uint32_t)cnt64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t kmask = (1ull << kbits) - 1;
-    for (uint32_t i = threadIdx.x; i < P; i += NT)
-        v[i] = i < cnt ? ((sk[b + i] & kmask) << 32) | sv[b + i] : ~0ull;
-    __syncthreads();
-    bool cross = false;   // the previous stage wrote elements of other waves
-    for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            if (j >= 64 || cross) {
-                __syncthreads();
-            } else {
-                wave_lds_sync();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t key[IPT];   // position << 32 | KmerID
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint32_t i = (uint32_t)wave * (IPT * 64) + (uint32_t)j * 64 + lane;
+        key[j] = i < cnt ? ((uint64_t)sv[b + i] << 32) | (sk[b + i] & kmask) : 0ull;
+    }
+    for (int sh = 0; sh < kbits; sh += 8) {
+        const uint32_t dm = kbits - sh >= 8 ? 255u : ((1u << (kbits - sh)) - 1u);
+        for (int i = tid; i < NW * 256; i += NT) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t dig[IPT], rank[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint32_t i0 = (uint32_t)wave * (IPT * 64) + (uint32_t)j * 64;   // wave-uniform
+            const bool ok = i0 + lane < cnt;
+            const uint32_t d = ok ? ((uint32_t)(key[j] >> sh) & dm) : 256u;
+            dig[j] = d;
+            rank[j] = 0;
+            if (i0 >= cnt) continue;
+            uint64_t m = __ballot(ok);
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb) {
+                const bool bit = (d >> bb) & 1u;
+                const uint64_t mb = __ballot(bit);
+                m &= bit ? mb : ~mb;
             }
-            cross = j >= 64;
-            for (uint32_t i = threadIdx.x; i < P; i += NT) {
-                const uint32_t x = i ^ j;
-                if (x > i) {
-                    const uint64_t a = v[i], c = v[x];
-                    if ((a > c) == ((i & k) == 0)) { v[i] = c; v[x] = a; }
+            uint32_t before = 0;
+            if (ok) before = wcnt[wave][d];
+            rank[j] = before + (uint32_t)__popcll(m & lt);
+            if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
+            wave_lds_sync();
+        }
+        __syncthreads();
+        {   // digit starts, then each wave's start inside its digit (waves in order: stable)
+            const uint32_t d = (uint32_t)tid & 255u;
+            uint32_t tot_d = 0;
+            if (tid < 256)
+                for (int w = 0; w < NW; ++w) tot_d += wcnt[w][d];
+            uint32_t tt;
+            const uint32_t exd = block_excl_scan<NT>(tid < 256 ? tot_d : 0u, ws, &tt);
+            if (tid < 256) {
+                uint32_t o = exd;
+                for (int w = 0; w < NW; ++w) {
+                    const uint32_t c = wcnt[w][d];
+                    wcnt[w][d] = o;
+                    o += c;
                 }
             }
         }
-    if (cross) __syncthreads();
-    wave_lds_sync();
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            if (dig[j] < 256u) buf[wcnt[wave][dig[j]] + rank[j]] = key[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint32_t i = (uint32_t)wave * (IPT * 64) + (uint32_t)j * 64 + lane;
+            if (i < cnt) key[j] = buf[i];
+        }
+        __syncthreads();
+    }
     const uint64_t rk = r << kbits;
-    for (uint32_t i = threadIdx.x; i < cnt; i += NT) {
-        const uint64_t x = v[i];
-        sk[b + i] = rk | (x >> 32);
-        sv[b + i] = (uint32_t)x;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint32_t i = (uint32_t)wave * (IPT * 64) + (uint32_t)j * 64 + lane;
+        if (i < cnt) {
+            sk[b + i] = rk | (key[j] & kmask);
+            sv[b + i] = (uint32_t)(key[j] >> 32);
+        }
+    }
+}
+
+// The same sort for reads of at most 64 * WIPT hits, one wave per read and no workgroup barrier:
+// the 256 digit counts live four per lane and are scanned with shuffles (most reads, ~220 hits
+// at C3, fit; a 256-thread workgroup would leave three waves idle behind its barriers).
+constexpr int WIPT = 8;
+__global__ void __launch_bounds__(64) lk_wsort(const uint64_t* __restrict__ hptr, uint64_t nreads, int kbits,
+                                               uint64_t* __restrict__ sk, uint32_t* __restrict__ sv) {
+    __shared__ uint64_t buf[64 * WIPT];
+    __shared__ uint32_t wcnt[256];
+    const uint64_t r = blockIdx.x;
+    if (r >= nreads) return;
+    const uint64_t b = hptr[r], cnt64 = hptr[r + 1] - b;
+    if (cnt64 < 2 || cnt64 > 64u * WIPT) return;
+    const uint32_t cnt = (uint32_t)cnt64;
+    const int lane = threadIdx.x;
+    const uint64_t kmask = (1ull << kbits) - 1;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t key[WIPT];   // position << 32 | KmerID, item i = j * 64 + lane
+#pragma unroll
+    for (int j = 0; j < WIPT; ++j) {
+        const uint32_t i = (uint32_t)j * 64 + lane;
+        key[j] = i < cnt ? ((uint64_t)sv[b + i] << 32) | (sk[b + i] & kmask) : 0ull;
+    }
+    for (int sh = 0; sh < kbits; sh += 8) {
+        const uint32_t dm = kbits - sh >= 8 ? 255u : ((1u << (kbits - sh)) - 1u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wcnt[q * 64 + lane] = 0;
+        wave_lds_sync();
+        uint32_t dig[WIPT], rank[WIPT];
+#pragma unroll
+        for (int j = 0; j < WIPT; ++j) {
+            const bool ok = (uint32_t)j * 64 + lane < cnt;
+            const uint32_t d = ok ? ((uint32_t)(key[j] >> sh) & dm) : 256u;
+            dig[j] = d;
+            rank[j] = 0;
+            if ((uint32_t)j * 64 >= cnt) continue;   // wave-uniform
+            uint64_t m = __ballot(ok);
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb) {
+                const bool bit = (d >> bb) & 1u;
+                const uint64_t mb = __ballot(bit);
+                m &= bit ? mb : ~mb;
+            }
+            uint32_t before = 0;
+            if (ok) before = wcnt[d];
+            rank[j] = before + (uint32_t)__popcll(m & lt);
+            if (ok && (m & lt) == 0ull) wcnt[d] = before + (uint32_t)__popcll(m);
+            wave_lds_sync();
+        }
+        {   // exclusive scan of the 256 digit counts: lane l holds digits 4l..4l+3
+            const uint32_t c0 = wcnt[4 * lane], c1 = wcnt[4 * lane + 1], c2 = wcnt[4 * lane + 2],
+                           c3 = wcnt[4 * lane + 3];
+            const uint32_t s4 = c0 + c1 + c2 + c3;
+            const uint32_t ex = wave_incl_scan(s4, lane) - s4;
+            wave_lds_sync();
+            wcnt[4 * lane] = ex;
+            wcnt[4 * lane + 1] = ex + c0;
+            wcnt[4 * lane + 2] = ex + c0 + c1;
+            wcnt[4 * lane + 3] = ex + c0 + c1 + c2;
+            wave_lds_sync();
+        }
+#pragma unroll
+        for (int j = 0; j < WIPT; ++j)
+            if (dig[j] < 256u) buf[wcnt[dig[j]] + rank[j]] = key[j];
+        wave_lds_sync();
+#pragma unroll
+        for (int j = 0; j < WIPT; ++j) {
+            const uint32_t i = (uint32_t)j * 64 + lane;
+            if (i < cnt) key[j] = buf[i];
+        }
+        wave_lds_sync();
+    }
+    const uint64_t rk = r << kbits;
+#pragma unroll
+    for (int j = 0; j < WIPT; ++j) {
+        const uint32_t i = (uint32_t)j * 64 + lane;
+        if (i < cnt) {
+            sk[b + i] = rk | (key[j] & kmask);
+            sv[b + i] = (uint32_t)(key[j] >> 32);
+        }
     }
 }
 
@@ -717,21 +845,32 @@ void lookup_run(hga_ctx* c) {
         HGA_HIP(hipMemcpyAsync(mx, ctr, 16, hipMemcpyDeviceToHost, c->stream));
         c->sync();
         if (mx[1] <= 16384 && n < (1ull << 31)) {
+            // three tiers by hit count: one wave per read (<= 512), a 256-thread workgroup
+            // (<= 2048), a 1024-thread workgroup (<= 16384); the last two over listed reads
+            uint32_t* mid = nullptr;
             uint32_t* big = nullptr;
-            unsigned long long nbig = 0;
-            if (mx[1] > 2048) {   // the few long reads: list them, one 1024-thread workgroup each
-                big = static_cast<uint32_t*>(L.big_list.ensure(n * 4 + 64));
+            unsigned long long nl[2] = {0, 0};
+            if (mx[1] > 64u * WIPT) {
+                mid = static_cast<uint32_t*>(L.big_list.ensure(2 * n * 4 + 64));
+                big = mid + n;
                 auto* bc = reinterpret_cast<unsigned long long*>(ctr + 2);
-                hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, hptr, n, 2048ull,
-                                   big, bc);
-                HGA_HIP(hipMemcpyAsync(&nbig, bc, 8, hipMemcpyDeviceToHost, c->stream));
+                HGA_HIP(hipMemsetAsync(bc, 0, 16, c->stream));
+                hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, hptr, n,
+                                   (unsigned long long)(64 * WIPT), mid, bc);
+                if (mx[1] > 2048)
+                    hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, hptr, n,
+                                       2048ull, big, bc + 1);
+                HGA_HIP(hipMemcpyAsync(nl, bc, 16, hipMemcpyDeviceToHost, c->stream));
                 c->sync();
+                HGA_HIP(hipMemsetAsync(bc, 0, 16, c->stream));   // ctr[2..3] are read back below
             }
             c->launch("lk_sort", [&] {
-                hipLaunchKernelGGL((lk_segsort<256, 2048>), dim3((unsigned)n), dim3(256), 0, c->stream, hptr, n, kbits,
-                                   sk, sv, 1u, (const uint32_t*)nullptr);
-                if (nbig)
-                    hipLaunchKernelGGL((lk_segsort<1024, 16384>), dim3((unsigned)nbig), dim3(1024), 0, c->stream,
+                hipLaunchKernelGGL(lk_wsort, dim3((unsigned)n), dim3(64), 0, c->stream, hptr, n, kbits, sk, sv);
+                if (nl[0])
+                    hipLaunchKernelGGL((lk_segsort<256, 8>), dim3((unsigned)nl[0]), dim3(256), 0, c->stream, hptr, n,
+                                       kbits, sk, sv, (uint32_t)(64 * WIPT), (const uint32_t*)mid);
+                if (nl[1])
+                    hipLaunchKernelGGL((lk_segsort<1024, 16>), dim3((unsigned)nl[1]), dim3(1024), 0, c->stream,
                                        hptr, n, kbits, sk, sv, 2048u, (const uint32_t*)big);
             });
             c->check_launch("lk_segsort");
