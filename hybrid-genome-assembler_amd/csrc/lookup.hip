@@ -659,27 +659,63 @@ __global__ void lk_compose(const uint32_t* __restrict__ rd, const uint32_t* __re
     val[i] = pos[i];
 }
 
-__global__ void lk_first_flags(const uint64_t* __restrict__ key, uint64_t H, uint64_t* __restrict__ flag,
-                               uint32_t* __restrict__ sorted_kid, uint64_t kmask) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= H) return;
-    flag[i] = (i == 0 || key[i] != key[i - 1]) ? 1ull : 0ull;
-    sorted_kid[i] = (uint32_t)(key[i] & kmask);
+// First occurrences per (read, KmerID) from the per-read sorted hits, one wave per read (no
+// H-sized flag array or scan): pass A writes the sorted KmerIDs and counts each read's distinct
+// ids into cnt[r]; after an exclusive scan over the reads (= the first-occurrence CSR pointers)
+// pass B writes each read's heads at its offset, in sorted order (ReadClusteringEngine.cpp:267).
+__global__ void __launch_bounds__(256) lk_first_count(const uint64_t* __restrict__ hptr, uint64_t n,
+                                                      const uint64_t* __restrict__ key, uint64_t kmask,
+                                                      uint32_t* __restrict__ sorted_kid, uint64_t* __restrict__ cnt) {
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= n) return;
+    const uint64_t b = hptr[r], e = hptr[r + 1];
+    uint64_t prev = ~0ull;   // last key of the previous chunk
+    uint32_t u = 0;
+    for (uint64_t i0 = b; i0 < e; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const bool ok = i < e;
+        const uint64_t k = ok ? key[i] : 0ull;
+        uint64_t kp = __shfl_up(k, 1, 64);
+        if (lane == 0) kp = prev;
+        const bool head = ok && k != kp;
+        if (ok) sorted_kid[i] = (uint32_t)(k & kmask);
+        u += (uint32_t)__popcll(__ballot(head));
+        prev = __shfl(k, 63, 64);
+    }
+    if (lane == 0) cnt[r] = u;
 }
-
-__global__ void lk_first_scatter(const uint64_t* __restrict__ key, const uint32_t* __restrict__ pos,
-                                 const uint64_t* __restrict__ off, uint64_t H, int kbits,
-                                 uint64_t kmask, uint32_t* __restrict__ fk, uint32_t* __restrict__ fp,
-                                 uint32_t* __restrict__ fr) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= H) return;
-    if (i == 0 || key[i] != key[i - 1]) {
-        const uint64_t o = off[i];
-        fk[o] = (uint32_t)(key[i] & kmask);
-        fp[o] = pos[i];
-        fr[o] = (uint32_t)(key[i] >> kbits);
+__global__ void __launch_bounds__(256) lk_first_write(const uint64_t* __restrict__ hptr, uint64_t n,
+                                                      const uint64_t* __restrict__ key,
+                                                      const uint32_t* __restrict__ pos,
+                                                      const uint64_t* __restrict__ foff, uint64_t kmask,
+                                                      uint32_t* __restrict__ fk, uint32_t* __restrict__ fp,
+                                                      uint32_t* __restrict__ fr) {
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= n) return;
+    const uint64_t b = hptr[r], e = hptr[r + 1];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t prev = ~0ull, o = foff[r];
+    for (uint64_t i0 = b; i0 < e; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const bool ok = i < e;
+        const uint64_t k = ok ? key[i] : 0ull;
+        uint64_t kp = __shfl_up(k, 1, 64);
+        if (lane == 0) kp = prev;
+        const bool head = ok && k != kp;
+        const uint64_t m = __ballot(head);
+        if (head) {
+            const uint64_t at = o + (uint64_t)__popcll(m & lt);
+            fk[at] = (uint32_t)(k & kmask);
+            fp[at] = pos[i];
+            fr[at] = (uint32_t)r;
+        }
+        o += (uint64_t)__popcll(m);
+        prev = __shfl(k, 63, 64);
     }
 }
+
 
 inline unsigned blocks_for(uint64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 inline int bits_for(uint64_t n) {   // bits to hold values in [0, n)
@@ -877,23 +913,25 @@ void lookup_run(hga_ctx* c) {
         } else {
             radix_sort_u64(c, sk, sv, H, kbits + rbits, L.scratch2);   // a read with > 16384 hits
         }
-        uint64_t* flag = static_cast<uint64_t*>(L.s_key2.ensure((H + 1) * 8));
         uint32_t* skid = static_cast<uint32_t*>(L.s_val2.ensure(H * 4));
+        uint64_t* fptr0 = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
         c->launch("lk_post", [&] {
-            hipLaunchKernelGGL(lk_first_flags, dim3(blocks_for(H, 256)), dim3(256), 0, c->stream, sk, H, flag,
-                               skid, kmask);
+            hipLaunchKernelGGL(lk_first_count, dim3(blocks_for(n, 4)), dim3(256), 0, c->stream, hptr, n, sk, kmask,
+                               skid, fptr0);
         });
-        HGA_HIP(hipMemsetAsync(flag + H, 0, 8, c->stream));
-        exclusive_scan_u64(c, flag, H + 1, L.scratch3);
-        HGA_HIP(hipMemcpyAsync(&U, flag + H, 8, hipMemcpyDeviceToHost, c->stream));
+        c->check_launch("lk_first_count");
+        HGA_HIP(hipMemsetAsync(fptr0 + n, 0, 8, c->stream));
+        exclusive_scan_u64(c, fptr0, n + 1, L.scratch3);
+        HGA_HIP(hipMemcpyAsync(&U, fptr0 + n, 8, hipMemcpyDeviceToHost, c->stream));
         c->sync();
-        uint32_t* fk = static_cast<uint32_t*>(L.first_kid.ensure(U * 4));
-        uint32_t* fp = static_cast<uint32_t*>(L.first_pos.ensure(U * 4));
-        uint32_t* fr = static_cast<uint32_t*>(L.first_read.ensure(U * 4));
+        uint32_t* fk = static_cast<uint32_t*>(L.first_kid.ensure(std::max<uint64_t>(U, 1) * 4));
+        uint32_t* fp = static_cast<uint32_t*>(L.first_pos.ensure(std::max<uint64_t>(U, 1) * 4));
+        uint32_t* fr = static_cast<uint32_t*>(L.first_read.ensure(std::max<uint64_t>(U, 1) * 4));
         c->launch("lk_post", [&] {
-            hipLaunchKernelGGL(lk_first_scatter, dim3(blocks_for(H, 256)), dim3(256), 0, c->stream, sk, sv, flag,
-                               H, kbits, kmask, fk, fp, fr);
+            hipLaunchKernelGGL(lk_first_write, dim3(blocks_for(n, 4)), dim3(256), 0, c->stream, hptr, n, sk, sv,
+                               fptr0, kmask, fk, fp, fr);
         });
+        c->check_launch("lk_first_write");
         // kmer_component_index: stable sort of the read-ordered hits by KmerID
         uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
         uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(H * 4));
@@ -905,8 +943,9 @@ void lookup_run(hga_ctx* c) {
     uint64_t* fptr = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
     uint64_t* kptr = static_cast<uint64_t*>(L.kci_ptr.ensure(((uint64_t)L.n_sdk + 1) * 8));
     c->launch("lk_post", [&] {
-        hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(U + 1, 256)), dim3(256), 0, c->stream,
-                           U ? L.first_read.as<uint32_t>() : (const uint32_t*)nullptr, U, n, fptr);
+        if (!H)   // with hits the first-occurrence scan above already left the CSR pointers in fptr
+            hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(U + 1, 256)), dim3(256), 0, c->stream,
+                               (const uint32_t*)nullptr, U, n, fptr);
         hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(H + 1, 256)), dim3(256), 0, c->stream,
                            H ? L.kci_key.as<uint32_t>() : (const uint32_t*)nullptr, H, (uint64_t)L.n_sdk, kptr);
     });
