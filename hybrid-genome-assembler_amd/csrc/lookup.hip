@@ -390,17 +390,15 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
         return;
     }
+    // independent loads first (hit mask, tile offset, the read containing p0 — p0 is 32-aligned,
+    // so it is precomputed per word), so their latencies overlap instead of chaining
     uint32_t hits = p0 < nbases ? hmask[gt] : 0u;
+    const uint64_t tb = tile_cnt[blockIdx.x];
+    uint64_t r = p0 < nbases ? word_read[p0 / 32] : 0u, re = 0;
     uint32_t tot;
     const uint32_t ex = block_excl_scan<LK_T>((uint32_t)__popc(hits), ws, &tot);
     if (tot == 0) return;   // uniform
-    const uint64_t tb = tile_cnt[blockIdx.x];
-    // read containing p0 (p0 is 32-aligned): precomputed per word, no search
-    uint64_t r = 0, re = 0;
-    if (hits) {
-        r = word_read[p0 / 32];
-        re = offs[r + 1];
-    }
+    if (hits) re = offs[r + 1];
     const uint32_t* __restrict__ wk = win_kid + gt * LK_P;
     if (tot <= (uint32_t)LK_ST) {
         // the tile's hits staged in LDS at their tile offsets, then written as three coalesced runs
