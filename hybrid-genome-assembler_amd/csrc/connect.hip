@@ -21,7 +21,9 @@
 //   cn_global   the same walk over a per-pivot table in HBM for the overflow list;
 //   cn_keys / radix sort / cn_decode
 //               composite sort key (CAP-free): (max - score, pivot, candidate).
+#include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
@@ -83,12 +85,20 @@ struct CnOut {
     uint64_t rcap;                 // entries per region
     unsigned long long* ctr;       // [1] max score, [2] / [3] tier-2 / tier-3 pivots, [5] work
     unsigned long long* rcur;      // region cursors, stride CN_RSTRIDE
+    uint64_t *pst, *pcnt;          // per pivot read: first output slot and pair count (null: unused)
 };
 
 // Reserves n entries in region r; returns the region-local offset (entries past rcap are
 // counted but not written, and the host retries with the exact size).
 __device__ __forceinline__ uint64_t cn_reserve(const CnOut& out, uint32_t r, uint32_t n) {
     return atomicAdd(&out.rcur[(uint64_t)r * CN_RSTRIDE], (unsigned long long)n);
+}
+// Records pivot p's output run (one reservation per pivot in every tier).
+__device__ __forceinline__ void cn_note(const CnOut& out, uint32_t p, uint32_t r, uint64_t base, uint32_t n) {
+    if (out.pcnt) {
+        out.pst[p] = (uint64_t)r * out.rcap + base;
+        out.pcnt[p] = n;
+    }
 }
 __device__ __forceinline__ void cn_put(const CnOut& out, uint32_t r, uint64_t w, uint32_t x, uint32_t y, uint32_t sc) {
     if (w < out.rcap) {
@@ -157,7 +167,10 @@ __device__ void cn_emit(const CnIn& in, const CnOut& out, uint32_t p, const uint
     if (total == 0) return;
     __shared__ unsigned long long base_s;
     const uint32_t reg = p % CN_R;
-    if (threadIdx.x == 0) base_s = cn_reserve(out, reg, total);
+    if (threadIdx.x == 0) {
+        base_s = cn_reserve(out, reg, total);
+        cn_note(out, p, reg, base_s, total);
+    }
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(&out.ctr[1], (unsigned long long)mx);
     __syncthreads();
     uint64_t w = base_s + pre;
@@ -329,7 +342,10 @@ __global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint3
     if (total == 0) return;
     __shared__ unsigned long long base_s;
     const uint32_t reg = p % CN_R;
-    if (t == 0) base_s = cn_reserve(out, reg, total);
+    if (t == 0) {
+        base_s = cn_reserve(out, reg, total);
+        cn_note(out, p, reg, base_s, total);
+    }
     if ((t & 63) == 0 && mx) atomicMax(&out.ctr[1], (unsigned long long)mx);
     __syncthreads();
     uint64_t w = base_s + pre;
@@ -483,7 +499,10 @@ __global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, co
         wmax = max(wmax, mx);
         unsigned long long base = 0;
         const uint32_t reg = p % CN_R;
-        if (lane == 0) base = cn_reserve(out, reg, tot);
+        if (lane == 0) {
+            base = cn_reserve(out, reg, tot);
+            cn_note(out, p, reg, base, tot);
+        }
         base = __shfl(base, 0, 64);
         uint64_t w = base + inc - cnt;
 #pragma unroll
@@ -605,6 +624,43 @@ __global__ void cn_decode2(const uint64_t* __restrict__ pkey, const uint32_t* __
     og[j] = cat ? (uint8_t)(cat[x] == cat[y]) : (uint8_t)0;
 }
 
+// Pivot-ordered pairs: pivot p's run (candidate, score) copied to its scanned offset, one wave
+// per pivot; the per-pivot sort by candidate then the stable score pass give the final order.
+__global__ void __launch_bounds__(256) cn_gather(const uint64_t* __restrict__ pst, const uint64_t* __restrict__ poff,
+                                                 uint64_t nr, int ib, const uint32_t* __restrict__ y,
+                                                 const uint32_t* __restrict__ s, uint64_t* __restrict__ sk,
+                                                 uint32_t* __restrict__ sv) {
+    const uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= nr) return;
+    const uint64_t o = poff[p], m = poff[p + 1] - o;
+    if (!m) return;
+    const uint64_t g = pst[p];
+    for (uint64_t i = threadIdx.x & 63; i < m; i += 64) {
+        sk[o + i] = (p << ib) | y[g + i];   // composed: runs of one pair are left as they are
+        sv[o + i] = s[g + i];
+    }
+}
+// key = (pivot << ib | candidate) << sb | (max - score): a stable sort by the low sb bits of keys
+// already in (pivot, candidate) order gives (score desc, pivot, candidate)
+__global__ void cn_keys3(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint64_t n, uint32_t mxs,
+                         int sb, uint64_t* __restrict__ key) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) key[i] = (sk[i] << sb) | (uint64_t)(mxs - sv[i]);
+}
+__global__ void cn_decode3(const uint64_t* __restrict__ key, uint64_t n, uint32_t mxs, int ib, int sb,
+                           const int32_t* __restrict__ cat, uint32_t first_id, uint32_t* __restrict__ ox,
+                           uint32_t* __restrict__ oy, uint64_t* __restrict__ os, uint8_t* __restrict__ og) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = key[i];
+    const uint64_t m = (1ull << ib) - 1, sm = sb ? (1ull << sb) - 1 : 0ull;
+    const uint32_t y = (uint32_t)((k >> sb) & m), x = (uint32_t)((k >> (sb + ib)) & m);
+    ox[i] = x + first_id;
+    oy[i] = y + first_id;
+    os[i] = mxs - (uint32_t)(k & sm);
+    og[i] = cat ? (uint8_t)(cat[x] == cat[y]) : (uint8_t)0;
+}
+
 int bits_for(uint64_t v) {
     int b = 0;
     while (b < 64 && (v >> b)) ++b;
@@ -632,6 +688,7 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     // pivots: ReadIDs -> read indices
     const uint32_t* d_piv = nullptr;
     uint64_t P = nr;
+    bool dup_piv = false;   // a pivot listed twice: its runs cannot be keyed by the pivot read
     if (pivots) {
         std::vector<uint32_t> idx(n_piv);
         for (uint64_t i = 0; i < n_piv; ++i) {
@@ -639,6 +696,9 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
                         HGA_ERR_INVALID, "pivot ReadID outside the lookup's reads");
             idx[i] = pivots[i] - L.first_read_id;
         }
+        std::vector<uint32_t> srt(idx);
+        std::sort(srt.begin(), srt.end());
+        dup_piv = std::adjacent_find(srt.begin(), srt.end()) != srt.end();
         P = n_piv;
         if (!P) {
             S.ready = true;
@@ -666,6 +726,10 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     const bool force_global = std::getenv("HGA_CN_FORCE_GLOBAL") != nullptr;
     const bool force_block = force_global || std::getenv("HGA_CN_FORCE_BLOCK") != nullptr;
     const bool force_two = std::getenv("HGA_CN_TWO_STAGE") != nullptr;
+    const bool force_full = std::getenv("HGA_CN_FULL_SORT") != nullptr;   // test hook: the one-pass key sort
+    const bool runs = !dup_piv && !force_two && !force_full;
+    uint64_t* pst = runs ? static_cast<uint64_t*>(S.pst.ensure(nr * 8)) : nullptr;
+    uint64_t* pcnt = runs ? static_cast<uint64_t*>(S.pcnt.ensure((nr + 1) * 8)) : nullptr;
     if (const char* rc = std::getenv("HGA_CN_RCAP")) rcap = std::max<uint64_t>(1, std::strtoull(rc, nullptr, 10));
     unsigned long long h[4];
     std::vector<unsigned long long> hc(ctr_bytes / 8);
@@ -673,8 +737,9 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     for (int attempt = 0; attempt < 2; ++attempt) {
         const uint64_t cap = rcap * CN_R;
         CnOut out{static_cast<uint32_t*>(S.x.ensure(cap * 4)), static_cast<uint32_t*>(S.y.ensure(cap * 4)),
-                  static_cast<uint32_t*>(S.s.ensure(cap * 4)), rcap, ctr, rcur};
+                  static_cast<uint32_t*>(S.s.ensure(cap * 4)), rcap, ctr, rcur, pst, pcnt};
         HGA_HIP(hipMemsetAsync(ctr, 0, ctr_bytes, c->stream));
+        if (pcnt) HGA_HIP(hipMemsetAsync(pcnt, 0, (nr + 1) * 8, c->stream));
         const uint64_t wblk = std::min<uint64_t>((P + CNW_WAVES - 1) / CNW_WAVES, (uint64_t)c->num_cu * 7);
         c->launch("cn_wave", [&] {
             hipLaunchKernelGGL(cn_wave, dim3((unsigned)wblk), dim3(64 * CNW_WAVES), 0, c->stream, in, out, d_piv, P,
@@ -745,7 +810,34 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     uint32_t* oy = static_cast<uint32_t*>(S.oy.ensure(std::max<uint64_t>(n, 1) * 4));
     uint64_t* os = static_cast<uint64_t*>(S.os.ensure(std::max<uint64_t>(n, 1) * 8));
     uint8_t* og = static_cast<uint8_t*>(S.og.ensure(std::max<uint64_t>(n, 1)));
-    if (n) {
+    bool done = false;
+    if (n && runs && sb + 2 * ib <= 64) {
+        // pivot-ordered runs, each sorted by candidate, then one stable pass over the score bits
+        exclusive_scan_u64(c, pcnt, nr + 1, L.scratch);
+        uint64_t* sk = static_cast<uint64_t*>(S.sk2.ensure(n * 8));
+        uint32_t* sv = static_cast<uint32_t*>(S.sv2.ensure(n * 4));
+        c->launch("cn_sort", [&] {
+            hipLaunchKernelGGL(cn_gather, dim3(cn_blocks(nr, 4)), dim3(256), 0, c->stream, pst, pcnt, nr, ib,
+                               S.y.as<uint32_t>(), S.s.as<uint32_t>(), sk, sv);
+        });
+        c->check_launch("cn_gather");
+        if (segment_sort(c, pcnt, nr, ~0ull, ib, sk, sv, S.lst, ctr + 6, "cn_sort")) {
+            uint64_t* key = static_cast<uint64_t*>(S.key.ensure(n * 8));
+            c->launch("cn_sort", [&] {
+                hipLaunchKernelGGL(cn_keys3, dim3(cn_blocks(n, 256)), dim3(256), 0, c->stream, sk, sv, n, mxs, sb,
+                                   key);
+            });
+            c->check_launch("cn_keys3");
+            radix_sort_u64(c, key, nullptr, n, sb, L.scratch);
+            c->launch("cn_sort", [&] {
+                hipLaunchKernelGGL(cn_decode3, dim3(cn_blocks(n, 256)), dim3(256), 0, c->stream, key, n, mxs, ib, sb,
+                                   d_cat, L.first_read_id, ox, oy, os, og);
+            });
+            c->check_launch("cn_decode3");
+            done = true;
+        }
+    }
+    if (n && !done) {
         uint64_t* key = static_cast<uint64_t*>(S.key.ensure(n * 8));
         if (sb + 2 * ib <= 64 && !force_two) {
             c->launch("cn_sort", [&] {

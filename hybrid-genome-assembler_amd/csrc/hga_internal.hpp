@@ -160,7 +160,8 @@ struct LookupState {
 struct ConnState {
     bool ready = false;
     uint64_t n = 0, cap_hint = 0;
-    DevBuf piv, cat, ctr, rpre, ovf, ovf2, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og;
+    DevBuf piv, cat, ctr, rpre, ovf, ovf2, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og, pst, pcnt, sk2, sv2,
+        lst;
 };
 
 }  // namespace hga
@@ -236,6 +237,9 @@ void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int 
 // exclusive scan of u64 in place (sort.hip)
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
 void count_settle(hga_ctx* c, const unsigned long long* h = nullptr);
+// stable per-segment sort by the low kbits of sk (lookup.hip); false when a segment passes 16384
+bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxlen, int kbits, uint64_t* sk,
+                  uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label);
 void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t dbase, const uint32_t* d_hist,
                      const uint32_t* h_hist, DevBuf& scratch);
 }  // namespace hga

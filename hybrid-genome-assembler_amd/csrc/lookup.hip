@@ -724,6 +724,51 @@ inline int bits_for(uint64_t n) {   // bits to hold values in [0, n)
 
 }  // namespace
 
+// Stable per-segment sort of (sk low kbits, sv) by the key, segments hptr[s]..hptr[s+1] of at
+// most maxlen <= 16384 entries (returns false, doing nothing, above that): one wave per segment
+// up to 512 entries, listed segments on 256- and 1024-thread workgroups above.  Leaves
+// sk = s << kbits | key (segments of one entry are not touched: sk must arrive composed).  maxlen ~0: measured here.  `ctr2`: two device counters of scratch.
+bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxlen, int kbits, uint64_t* sk,
+                  uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label) {
+    if (maxlen == ~0ull) {   // unknown: the longest segment first
+        unsigned long long h2[2] = {0, 0};
+        HGA_HIP(hipMemsetAsync(ctr2, 0, 16, c->stream));
+        if (nseg)
+            hipLaunchKernelGGL(lk_nonempty, dim3(blocks_for(nseg, 1024)), dim3(1024), 0, c->stream, hptr, nseg, ctr2);
+        HGA_HIP(hipMemcpyAsync(h2, ctr2, 16, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        maxlen = h2[1];
+    }
+    if (maxlen > 16384 || nseg >= (1ull << 31)) return false;
+    uint32_t* mid = nullptr;
+    uint32_t* big = nullptr;
+    unsigned long long nl[2] = {0, 0};
+    if (maxlen > 64u * WIPT) {
+        mid = static_cast<uint32_t*>(list_buf.ensure(2 * nseg * 4 + 64));
+        big = mid + nseg;
+        HGA_HIP(hipMemsetAsync(ctr2, 0, 16, c->stream));
+        hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(nseg, 256)), dim3(256), 0, c->stream, hptr, nseg,
+                           (unsigned long long)(64 * WIPT), mid, ctr2);
+        if (maxlen > 2048)
+            hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(nseg, 256)), dim3(256), 0, c->stream, hptr, nseg,
+                               2048ull, big, ctr2 + 1);
+        HGA_HIP(hipMemcpyAsync(nl, ctr2, 16, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        HGA_HIP(hipMemsetAsync(ctr2, 0, 16, c->stream));
+    }
+    c->launch(label, [&] {
+        hipLaunchKernelGGL(lk_wsort, dim3((unsigned)nseg), dim3(64), 0, c->stream, hptr, nseg, kbits, sk, sv);
+        if (nl[0])
+            hipLaunchKernelGGL((lk_segsort<256, 8>), dim3((unsigned)nl[0]), dim3(256), 0, c->stream, hptr, nseg,
+                               kbits, sk, sv, (uint32_t)(64 * WIPT), (const uint32_t*)mid);
+        if (nl[1])
+            hipLaunchKernelGGL((lk_segsort<1024, 16>), dim3((unsigned)nl[1]), dim3(1024), 0, c->stream, hptr, nseg,
+                               kbits, sk, sv, 2048u, (const uint32_t*)big);
+    });
+    c->check_launch("segment_sort");
+    return true;
+}
+
 void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n) {
     HGA_REQUIRE(k >= 1 && k <= 32, HGA_ERR_INVALID, "k must be in [1,32]");
     auto& L = c->lookup;
@@ -878,39 +923,8 @@ void lookup_run(hga_ctx* c) {
         unsigned long long mx[2];
         HGA_HIP(hipMemcpyAsync(mx, ctr, 16, hipMemcpyDeviceToHost, c->stream));
         c->sync();
-        if (mx[1] <= 16384 && n < (1ull << 31)) {
-            // three tiers by hit count: one wave per read (<= 512), a 256-thread workgroup
-            // (<= 2048), a 1024-thread workgroup (<= 16384); the last two over listed reads
-            uint32_t* mid = nullptr;
-            uint32_t* big = nullptr;
-            unsigned long long nl[2] = {0, 0};
-            if (mx[1] > 64u * WIPT) {
-                mid = static_cast<uint32_t*>(L.big_list.ensure(2 * n * 4 + 64));
-                big = mid + n;
-                auto* bc = reinterpret_cast<unsigned long long*>(ctr + 2);
-                HGA_HIP(hipMemsetAsync(bc, 0, 16, c->stream));
-                hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, hptr, n,
-                                   (unsigned long long)(64 * WIPT), mid, bc);
-                if (mx[1] > 2048)
-                    hipLaunchKernelGGL(lk_big_reads, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, hptr, n,
-                                       2048ull, big, bc + 1);
-                HGA_HIP(hipMemcpyAsync(nl, bc, 16, hipMemcpyDeviceToHost, c->stream));
-                c->sync();
-                HGA_HIP(hipMemsetAsync(bc, 0, 16, c->stream));   // ctr[2..3] are read back below
-            }
-            c->launch("lk_sort", [&] {
-                hipLaunchKernelGGL(lk_wsort, dim3((unsigned)n), dim3(64), 0, c->stream, hptr, n, kbits, sk, sv);
-                if (nl[0])
-                    hipLaunchKernelGGL((lk_segsort<256, 8>), dim3((unsigned)nl[0]), dim3(256), 0, c->stream, hptr, n,
-                                       kbits, sk, sv, (uint32_t)(64 * WIPT), (const uint32_t*)mid);
-                if (nl[1])
-                    hipLaunchKernelGGL((lk_segsort<1024, 16>), dim3((unsigned)nl[1]), dim3(1024), 0, c->stream,
-                                       hptr, n, kbits, sk, sv, 2048u, (const uint32_t*)big);
-            });
-            c->check_launch("lk_segsort");
-        } else {
+        if (!segment_sort(c, hptr, n, mx[1], kbits, sk, sv, L.big_list, ctr + 2, "lk_sort"))
             radix_sort_u64(c, sk, sv, H, kbits + rbits, L.scratch2);   // a read with > 16384 hits
-        }
         uint32_t* skid = static_cast<uint32_t*>(L.s_val2.ensure(H * 4));
         uint64_t* fptr0 = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
         c->launch("lk_post", [&] {

@@ -54,9 +54,13 @@ def test_connections_filters_and_pivots(gpu_ctx, golden_case):
     piv = np.arange(1, n + 1, 3, dtype=np.uint32)[::-1]
     same(gpu_ctx.connections(pivots=piv), oracle.connections(idx, pivots=piv))
     assert gpu_ctx.connections(pivots=np.zeros(0, np.uint32))[0].size == 0
+    # a pivot listed twice (its runs cannot be keyed by the pivot read: the one-pass key sort)
+    dup = np.concatenate([piv[:5], piv[:3]]).astype(np.uint32)
+    same(gpu_ctx.connections(pivots=dup), oracle.connections(idx, pivots=dup))
 
 
-@pytest.mark.parametrize("env", [None, "HGA_CN_FORCE_BLOCK", "HGA_CN_FORCE_GLOBAL", "HGA_CN_TWO_STAGE", "HGA_CN_RCAP"])
+@pytest.mark.parametrize("env", [None, "HGA_CN_FORCE_BLOCK", "HGA_CN_FORCE_GLOBAL", "HGA_CN_TWO_STAGE", "HGA_CN_RCAP",
+                                 "HGA_CN_FULL_SORT"])
 def test_connections_random_first_id(gpu_ctx, hga_mod, monkeypatch, env):
     if env:
         monkeypatch.setenv(env, "1")
