@@ -188,11 +188,14 @@ def _mix_inv(h, k):
     return (h * np.uint64(c1i)) & mask
 
 
-@pytest.mark.parametrize("skew", [False, True])
-def test_merge_packed_many_pieces(skew):
+@pytest.mark.parametrize("skew,one_pass", [(False, False), (True, False), (True, True)])
+def test_merge_packed_many_pieces(skew, one_pass, monkeypatch):
     """Owner merge at scale against a numpy group-by: 3 M pieces (many buckets, repeated keys,
     split rows); with skew, a twelfth of them in ONE bucket of the merge's mix binning, so that
-    bucket is summed in several passes over its LDS table."""
+    bucket is summed in several passes over its LDS table; one_pass forces a first attempt in one
+    pass per bucket, whose table overflow must be detected and retried."""
+    if one_pass:
+        monkeypatch.setenv("HGA_MB_ONE_PASS", "1")
     k, F, min_c = 19, 2, 2
     rng = np.random.default_rng(7)
     n = 3_000_000
