@@ -234,6 +234,9 @@ void radix_sort_u64(hga_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n, int 
                     DevBuf& scratch);
 void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int bits,
                     DevBuf& scratch);
+// the same with the input read from src_k / src_v (left intact), the result in keys / vals
+void radix_sort_u32_from(hga_ctx* c, const uint32_t* src_k, const uint32_t* src_v, uint32_t* keys, uint32_t* vals,
+                         uint64_t n, int bits, DevBuf& scratch);
 // exclusive scan of u64 in place (sort.hip)
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
 void count_settle(hga_ctx* c, const unsigned long long* h = nullptr);

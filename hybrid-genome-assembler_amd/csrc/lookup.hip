@@ -947,9 +947,7 @@ void lookup_run(hga_ctx* c) {
         // kmer_component_index: stable sort of the read-ordered hits by KmerID
         uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
         uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(H * 4));
-        HGA_HIP(hipMemcpyAsync(kk, hk, H * 4, hipMemcpyDeviceToDevice, c->stream));
-        HGA_HIP(hipMemcpyAsync(kv, hr, H * 4, hipMemcpyDeviceToDevice, c->stream));
-        radix_sort_u32(c, kk, kv, H, kbits, L.scratch2);
+        radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
     }
     L.firsts = U;
     uint64_t* fptr = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));

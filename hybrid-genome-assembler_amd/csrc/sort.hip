@@ -484,8 +484,18 @@ inline uint64_t hga_onesweep_max() {
     return v;
 }
 
+// src_k / src_v (optional): read the first pass from these instead of keys / vals (saves the copy
+// of an input that must stay intact); the result always ends in keys / vals.
 template <class K>
-void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, DevBuf& scratch) {
+void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, DevBuf& scratch,
+                     const K* src_k = nullptr, const uint32_t* src_v = nullptr) {
+    if (src_k && (n <= 1 || bits <= 0)) {
+        if (n) {
+            HGA_HIP(hipMemcpyAsync(keys, src_k, n * sizeof(K), hipMemcpyDeviceToDevice, c->stream));
+            if (vals) HGA_HIP(hipMemcpyAsync(vals, src_v, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        }
+        return;
+    }
     if (n <= 1 || bits <= 0) return;
     HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "radix sort: n >= 2^32");
     const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
@@ -515,13 +525,21 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
         HGA_HIP(hipMemsetAsync(hist, 0, hb + stb + tcb, c->stream));
         const unsigned hgrid = (unsigned)std::min<uint64_t>(n_tiles, (uint64_t)c->num_cu * 2);
         c->launch("radix_upsweep", [&] {
-            hipLaunchKernelGGL(rs_hist_all<K>, dim3(hgrid), dim3(RS_T), 0, c->stream, keys, n, npass, bits, hist);
+            hipLaunchKernelGGL(rs_hist_all<K>, dim3(hgrid), dim3(RS_T), 0, c->stream, src_k ? src_k : keys, n, npass,
+                               bits, hist);
         });
         c->check_launch("rs_hist_all");
+        // buffers by pass: [src,] then alternating so that the last pass writes keys when possible
         K* ka2 = keys;
         K* kb2 = k2o;
         uint32_t* va2 = vals;
         uint32_t* vb2 = v2o;
+        if (src_k) {
+            ka2 = const_cast<K*>(src_k);
+            va2 = const_cast<uint32_t*>(src_v);
+            kb2 = (npass & 1) ? keys : k2o;
+            vb2 = (npass & 1) ? vals : v2o;
+        }
         for (int p = 0; p < npass; ++p) {
             const uint32_t dm = bits - 8 * p >= 8 ? 255u : ((1u << (bits - 8 * p)) - 1u);
             c->launch("radix_downsweep", [&] {
@@ -534,17 +552,29 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
                                        status + (size_t)p * n_tiles * 256, tctr + p);
             });
             c->check_launch("rs_onesweep");
+            if (src_k && p == 0) {   // the source is never written: continue between keys and k2o
+                ka2 = kb2;
+                va2 = vb2;
+                kb2 = ka2 == keys ? k2o : keys;
+                vb2 = va2 == vals ? v2o : vals;
+                continue;
+            }
             std::swap(ka2, kb2);
             std::swap(va2, vb2);
         }
-        if (npass & 1) {
+        if (ka2 != keys) {
             HGA_HIP(hipMemcpyAsync(keys, ka2, n * sizeof(K), hipMemcpyDeviceToDevice, c->stream));
             if (vals) HGA_HIP(hipMemcpyAsync(vals, va2, n * 4, hipMemcpyDeviceToDevice, c->stream));
         }
         return;
     }
-    int passes = 0;
-    for (int shift = 0; shift < bits; shift += 8, ++passes) {
+    if (src_k) {
+        ka = const_cast<K*>(src_k);
+        va = const_cast<uint32_t*>(src_v);
+        kbuf = (npass & 1) ? keys : k2;
+        vbuf = (npass & 1) ? vals : v2;
+    }
+    for (int shift = 0; shift < bits; shift += 8) {
         const uint32_t dm = bits - shift >= 8 ? 255u : ((1u << (bits - shift)) - 1u);
         c->launch("radix_upsweep", [&] {
             hipLaunchKernelGGL(rs_upsweep<K>, dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n,
@@ -565,10 +595,17 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
             });
         }
         c->check_launch("rs_downsweep");
+        if (src_k && shift == 0) {   // the source is never written: continue between keys and k2
+            ka = kbuf;
+            va = vbuf;
+            kbuf = ka == keys ? k2 : keys;
+            vbuf = va == vals ? v2 : vals;
+            continue;
+        }
         std::swap(ka, kbuf);
         std::swap(va, vbuf);
     }
-    if (passes & 1) {
+    if (ka != keys) {
         HGA_HIP(hipMemcpyAsync(keys, ka, n * sizeof(K), hipMemcpyDeviceToDevice, c->stream));
         if (vals) HGA_HIP(hipMemcpyAsync(vals, va, n * 4, hipMemcpyDeviceToDevice, c->stream));
     }
@@ -628,6 +665,10 @@ void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t
 void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int bits,
                     DevBuf& scratch) {
     radix_sort_impl<uint32_t>(c, keys, vals, n, bits > 32 ? 32 : bits, scratch);
+}
+void radix_sort_u32_from(hga_ctx* c, const uint32_t* src_k, const uint32_t* src_v, uint32_t* keys, uint32_t* vals,
+                         uint64_t n, int bits, DevBuf& scratch) {
+    radix_sort_impl<uint32_t>(c, keys, vals, n, bits > 32 ? 32 : bits, scratch, src_k, src_v);
 }
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch) {
     scratch.ensure(scan_scratch_bytes(n));
