@@ -240,7 +240,8 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
                                                 uint32_t* __restrict__ win_kid,
                                                 unsigned long long* __restrict__ tile_cnt,
                                                 uint32_t* __restrict__ h_read, uint32_t* __restrict__ h_kid,
-                                                uint32_t* __restrict__ h_pos) {
+                                                uint32_t* __restrict__ h_pos, uint64_t* __restrict__ h_skey = nullptr,
+                                                uint32_t* __restrict__ h_sval = nullptr, int kbits = 0) {
     __shared__ uint32_t ws[LK_T / 64 + 1];
     const int k = K ? K : k_rt;
     const uint64_t gt = (uint64_t)blockIdx.x * LK_T + threadIdx.x;
@@ -417,9 +418,12 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < tot; i += LK_T) {
-            h_read[tb + i] = s_r[i];
-            h_kid[tb + i] = s_k[i];
-            h_pos[tb + i] = s_p[i];
+            const uint32_t rr = s_r[i], kk = s_k[i], pp = s_p[i];
+            h_read[tb + i] = rr;
+            h_kid[tb + i] = kk;
+            h_pos[tb + i] = pp;
+            h_skey[tb + i] = ((uint64_t)rr << kbits) | kk;   // the per-read sort's input, composed here
+            h_sval[tb + i] = pp;
         }
         return;
     }
@@ -429,9 +433,12 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         hits &= hits - 1u;
         const uint64_t e = p0 + j;
         while (re <= e) re = offs[++r + 1];
+        const uint32_t kk = wk[j], pp = (uint32_t)(e + 1 - offs[r]);
         h_read[o] = (uint32_t)r;
-        h_kid[o] = wk[j];
-        h_pos[o] = (uint32_t)(e + 1 - offs[r]);
+        h_kid[o] = kk;
+        h_pos[o] = pp;
+        h_skey[o] = (r << kbits) | kk;
+        h_sval[o] = pp;
         ++o;
     }
 }
@@ -648,14 +655,6 @@ __global__ void __launch_bounds__(64) lk_wsort(const uint64_t* __restrict__ hptr
     }
 }
 
-__global__ void lk_compose(const uint32_t* __restrict__ rd, const uint32_t* __restrict__ kid,
-                           const uint32_t* __restrict__ pos, uint64_t H, int kbits,
-                           uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= H) return;
-    key[i] = ((uint64_t)rd[i] << kbits) | kid[i];
-    val[i] = pos[i];
-}
 
 // First occurrences per (read, KmerID) from the per-read sorted hits, one wave per read (no
 // H-sized flag array or scan): pass A writes the sorted KmerIDs and counts each read's distinct
@@ -891,10 +890,14 @@ void lookup_run(hga_ctx* c) {
     uint32_t* hr = static_cast<uint32_t*>(L.hit_read.ensure(std::max<uint64_t>(H, 1) * 4));
     uint32_t* hk = static_cast<uint32_t*>(L.hit_kid.ensure(std::max<uint64_t>(H, 1) * 4));
     uint32_t* hp = static_cast<uint32_t*>(L.hit_pos.ensure(std::max<uint64_t>(H, 1) * 4));
+    const int kbits = bits_for(std::max<uint32_t>(L.n_sdk, 1));
+    uint64_t* sk = static_cast<uint64_t*>(L.s_key.ensure(std::max<uint64_t>(H, 1) * 8));
+    uint32_t* sv = static_cast<uint32_t*>(L.s_val.ensure(std::max<uint64_t>(H, 1) * 4));
     if (H) {
         c->launch("lk_emit", [&] {
             hipLaunchKernelGGL((lk_scan<true, 0>), dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, nb,
-                               offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, hr, hk, hp);
+                               offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, hr, hk, hp, sk, sv,
+                               kbits);
         });
         c->check_launch("lk_emit");
     }
@@ -908,18 +911,11 @@ void lookup_run(hga_ctx* c) {
             hipLaunchKernelGGL(lk_nonempty, dim3(blocks_for(n, 1024)), dim3(1024), 0, c->stream, hptr, n, ctr);
     });
     c->check_launch("lk_ptr");
-    const int kbits = bits_for(std::max<uint32_t>(L.n_sdk, 1));
     const int rbits = bits_for(std::max<uint64_t>(n, 1));
     const uint64_t kmask = (1ull << kbits) - 1;
     uint64_t U = 0;
     if (H) {
-        // per-read (read, KmerID) sort, positions as payload (stable: window order kept)
-        uint64_t* sk = static_cast<uint64_t*>(L.s_key.ensure(H * 8));
-        uint32_t* sv = static_cast<uint32_t*>(L.s_val.ensure(H * 4));
-        c->launch("lk_post", [&] {
-            hipLaunchKernelGGL(lk_compose, dim3(blocks_for(H, 256)), dim3(256), 0, c->stream, hr, hk, hp, H,
-                               kbits, sk, sv);
-        });
+        // per-read (read, KmerID) sort of the emitted (read << kbits | KmerID, position) pairs
         unsigned long long mx[2];
         HGA_HIP(hipMemcpyAsync(mx, ctr, 16, hipMemcpyDeviceToHost, c->stream));
         c->sync();
