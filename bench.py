@@ -311,6 +311,51 @@ def ingest_leg(ga, gb, threads):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def scale_leg(dev, reps=2):
+    """SURVEY.md C4 at one rank of eight: reads of a 2 x 500 Mbp diploid (d = 0.005) at 30x / 8 =
+    3.75x, ART-like 150 bp, 2 files (3.77 Gbases, 3.3 G 19-mer instances) counted on this GPU in one
+    pass (the third split level); the same step as the headline."""
+    L4, cov = 500_000_000, 3.75
+    t_gen = time.perf_counter()
+    g4a = hga.gen_genome(L4, 41)
+    g4b = hga.gen_haplotype(g4a, 0.005, 0, 42)
+    n4 = int(cov * L4 / READ_LEN)
+    r4a = hga.gen_art(g4a, n4, READ_LEN, 43)
+    r4b = hga.gen_art(g4b, n4, READ_LEN, 44)
+    del g4a, g4b
+    log(f"C4 rank shard generated in {time.perf_counter() - t_gen:.1f}s: {2 * n4} reads")
+    c4 = hga.Ctx(dev)
+    try:
+        c4.count_begin(K, 2)
+        c4.count_add(0, r4a.seq)
+        c4.count_add(1, r4b.seq)
+        bases = len(r4a.seq) + len(r4b.seq)
+        del r4a, r4b
+        count_step(c4)   # warm-up (allocations)
+        c4.profile(True)
+        c4.profile_reset()
+        count_step(c4)
+        names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
+                 "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
+        ker = {nm: round(c4.profile_get(nm)[0], 3) for nm in names if c4.profile_get(nm)[1]}
+        c4.profile(False)
+        c4.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            n_sel, n_disc = count_step(c4)
+        c4.sync()
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        st = c4.count_stats()
+        return {"workload": "C4 rank shard: 1/8 of ART-like 30x reads of a 2 x 500 Mbp diploid (d=0.005), k=19, "
+                            "2 files; step = count_run + spec_hist + select[10,25]",
+                "bases": int(bases), "instances": int(st.instances), "distinct_rows": int(st.distinct_rows),
+                "buckets": int(st.buckets), "max_split": int(st.max_split), "selected": int(n_sel),
+                "discriminative": int(n_disc), "ms_per_step": round(ms, 2),
+                "k_mers_per_s": round(st.instances / (ms * 1e-3), 1), "kernels_ms": ker}
+    finally:
+        c4.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -319,6 +364,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lookup", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host FASTQ ingest leg")
+    ap.add_argument("--no-scale", action="store_true", help="skip the C4 rank-shard count leg (N=1 only)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("HGA_CPU_THREADS", "16")))
     args = ap.parse_args()
     D = Dist(args.gpus)
@@ -456,6 +502,8 @@ def main():
         result["cpu_baseline"] = cpu_baseline(ra, rb, args.cpu_threads)
     if not args.no_ingest and D.rank == 0 and D.world == 1:
         result["ingest"] = ingest_leg(ga, gb, args.cpu_threads)
+    if not args.no_scale and D.world == 1:
+        result["scale_c4_shard"] = scale_leg(dev)
     ctx.close()
     D.close()
     if D.rank == 0:

@@ -9,7 +9,7 @@ TAG=$1; shift
 R=$PWD; mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/stats_$TAG -o run -- \
-    python3 $R/bench.py --steps 10 --warmup 2 --no-cpu "$@" > $R/gpurun_out/stats_$TAG.json 2> $R/gpurun_out/stats_$TAG.err \
+    python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-scale "$@" > $R/gpurun_out/stats_$TAG.json 2> $R/gpurun_out/stats_$TAG.err \
     || { echo "stats run failed"; tail -5 $R/gpurun_out/stats_$TAG.err; exit 1; }
 for p in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $p --output-format csv -d $R/gpurun_out/hbm_${TAG}_$p -o run -- \
