@@ -406,15 +406,27 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         // (each lane's hits are consecutive in the output: direct stores would be 4-B scatters)
         __shared__ uint32_t s_r[LK_ST], s_k[LK_ST], s_p[LK_ST];
         uint32_t o = ex;
-        while (hits) {
-            const int j = __builtin_ctz(hits);
+        uint64_t rs = hits ? offs[r] : 0;   // start of read r: positions without a load per hit
+        while (hits) {   // two hits per round: both KmerID loads in flight before either is used
+            const int j0 = __builtin_ctz(hits);
             hits &= hits - 1u;
-            const uint64_t e = p0 + j;
-            while (re <= e) re = offs[++r + 1];
-            s_r[o] = (uint32_t)r;
-            s_k[o] = wk[j];
-            s_p[o] = (uint32_t)(e + 1 - offs[r]);
-            ++o;
+            const bool two = hits != 0u;
+            const int j1 = two ? __builtin_ctz(hits) : j0;
+            if (two) hits &= hits - 1u;
+            const uint32_t k0 = wk[j0], k1 = wk[j1];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                if (t == 1 && !two) break;
+                const uint64_t e = p0 + (t ? j1 : j0);
+                while (re <= e) {
+                    rs = re;
+                    re = offs[++r + 1];
+                }
+                s_r[o] = (uint32_t)r;
+                s_k[o] = t ? k1 : k0;
+                s_p[o] = (uint32_t)(e + 1 - rs);
+                ++o;
+            }
         }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < tot; i += LK_T) {
