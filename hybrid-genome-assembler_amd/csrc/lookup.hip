@@ -407,23 +407,29 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         __shared__ uint32_t s_r[LK_ST], s_k[LK_ST], s_p[LK_ST];
         uint32_t o = ex;
         uint64_t rs = hits ? offs[r] : 0;   // start of read r: positions without a load per hit
-        while (hits) {   // two hits per round: both KmerID loads in flight before either is used
-            const int j0 = __builtin_ctz(hits);
-            hits &= hits - 1u;
-            const bool two = hits != 0u;
-            const int j1 = two ? __builtin_ctz(hits) : j0;
-            if (two) hits &= hits - 1u;
-            const uint32_t k0 = wk[j0], k1 = wk[j1];
+        while (hits) {   // up to four hits per round: their KmerID loads in flight before any is used
+            constexpr int U = 4;
+            int jj[U];
+            uint32_t kk[U];
+            int cnt = 0;
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                if (t == 1 && !two) break;
-                const uint64_t e = p0 + (t ? j1 : j0);
+            for (int t = 0; t < U; ++t) {
+                jj[t] = hits ? __builtin_ctz(hits) : jj[t > 0 ? t - 1 : 0];
+                cnt += hits ? 1 : 0;
+                hits &= hits ? hits - 1u : 0u;
+            }
+#pragma unroll
+            for (int t = 0; t < U; ++t) kk[t] = wk[jj[t]];
+#pragma unroll
+            for (int t = 0; t < U; ++t) {
+                if (t >= cnt) break;
+                const uint64_t e = p0 + jj[t];
                 while (re <= e) {
                     rs = re;
                     re = offs[++r + 1];
                 }
                 s_r[o] = (uint32_t)r;
-                s_k[o] = t ? k1 : k0;
+                s_k[o] = kk[t];
                 s_p[o] = (uint32_t)(e + 1 - rs);
                 ++o;
             }
