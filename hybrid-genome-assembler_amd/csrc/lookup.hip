@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         uint32_t o = ex;
         uint64_t rs = hits ? offs[r] : 0;   // start of read r: positions without a load per hit
         while (hits) {   // up to four hits per round: their KmerID loads in flight before any is used
-            constexpr int U = 4;
+            constexpr int U = 8;
             int jj[U];
             uint32_t kk[U];
             int cnt = 0;
