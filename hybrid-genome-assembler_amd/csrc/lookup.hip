@@ -674,6 +674,7 @@ __global__ void __launch_bounds__(64) lk_wsort(const uint64_t* __restrict__ hptr
 }
 
 
+constexpr int FC = 4;   // chunks of 64 hits per round in the first-occurrence passes
 // First occurrences per (read, KmerID) from the per-read sorted hits, one wave per read (no
 // H-sized flag array or scan): pass A writes the sorted KmerIDs and counts each read's distinct
 // ids into cnt[r]; after an exclusive scan over the reads (= the first-occurrence CSR pointers)
@@ -687,16 +688,26 @@ __global__ void __launch_bounds__(256) lk_first_count(const uint64_t* __restrict
     const uint64_t b = hptr[r], e = hptr[r + 1];
     uint64_t prev = ~0ull;   // last key of the previous chunk
     uint32_t u = 0;
-    for (uint64_t i0 = b; i0 < e; i0 += 64) {
-        const uint64_t i = i0 + lane;
-        const bool ok = i < e;
-        const uint64_t k = ok ? key[i] : 0ull;
-        uint64_t kp = __shfl_up(k, 1, 64);
-        if (lane == 0) kp = prev;
-        const bool head = ok && k != kp;
-        if (ok) sorted_kid[i] = (uint32_t)(k & kmask);
-        u += (uint32_t)__popcll(__ballot(head));
-        prev = __shfl(k, 63, 64);
+    for (uint64_t i00 = b; i00 < e; i00 += 64 * FC) {   // FC chunks' loads in flight together
+        uint64_t kk[FC];
+#pragma unroll
+        for (int t = 0; t < FC; ++t) {
+            const uint64_t i = i00 + 64 * t + lane;
+            kk[t] = i < e ? key[i] : 0ull;
+        }
+#pragma unroll
+        for (int t = 0; t < FC; ++t) {
+            const uint64_t i = i00 + 64 * t + lane;
+            if (i00 + 64 * t >= e) break;   // wave-uniform
+            const bool ok = i < e;
+            const uint64_t k = kk[t];
+            uint64_t kp = __shfl_up(k, 1, 64);
+            if (lane == 0) kp = prev;
+            const bool head = ok && k != kp;
+            if (ok) sorted_kid[i] = (uint32_t)(k & kmask);
+            u += (uint32_t)__popcll(__ballot(head));
+            prev = __shfl(k, 63, 64);
+        }
     }
     if (lane == 0) cnt[r] = u;
 }
@@ -712,22 +723,35 @@ __global__ void __launch_bounds__(256) lk_first_write(const uint64_t* __restrict
     const uint64_t b = hptr[r], e = hptr[r + 1];
     const uint64_t lt = (1ull << lane) - 1ull;
     uint64_t prev = ~0ull, o = foff[r];
-    for (uint64_t i0 = b; i0 < e; i0 += 64) {
-        const uint64_t i = i0 + lane;
-        const bool ok = i < e;
-        const uint64_t k = ok ? key[i] : 0ull;
-        uint64_t kp = __shfl_up(k, 1, 64);
-        if (lane == 0) kp = prev;
-        const bool head = ok && k != kp;
-        const uint64_t m = __ballot(head);
-        if (head) {
-            const uint64_t at = o + (uint64_t)__popcll(m & lt);
-            fk[at] = (uint32_t)(k & kmask);
-            fp[at] = pos[i];
-            fr[at] = (uint32_t)r;
+    for (uint64_t i00 = b; i00 < e; i00 += 64 * FC) {   // FC chunks' loads in flight together
+        uint64_t kk[FC];
+        uint32_t pp[FC];
+#pragma unroll
+        for (int t = 0; t < FC; ++t) {
+            const uint64_t i = i00 + 64 * t + lane;
+            kk[t] = i < e ? key[i] : 0ull;
+            pp[t] = i < e ? pos[i] : 0u;   // with the key: no dependent load per head
         }
-        o += (uint64_t)__popcll(m);
-        prev = __shfl(k, 63, 64);
+#pragma unroll
+        for (int t = 0; t < FC; ++t) {
+            if (i00 + 64 * t >= e) break;   // wave-uniform
+            const uint64_t i = i00 + 64 * t + lane;
+            const bool ok = i < e;
+            const uint64_t k = kk[t];
+            const uint32_t ps = pp[t];
+            uint64_t kp = __shfl_up(k, 1, 64);
+            if (lane == 0) kp = prev;
+            const bool head = ok && k != kp;
+            const uint64_t m = __ballot(head);
+            if (head) {
+                const uint64_t at = o + (uint64_t)__popcll(m & lt);
+                fk[at] = (uint32_t)(k & kmask);
+                fp[at] = ps;
+                fr[at] = (uint32_t)r;
+            }
+            o += (uint64_t)__popcll(m);
+            prev = __shfl(k, 63, 64);
+        }
     }
 }
 
