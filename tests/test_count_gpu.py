@@ -251,3 +251,26 @@ def test_count_split3_c1_scale(gpu_ctx, hga_mod, monkeypatch):
     r = run_gpu(gpu_ctx, streams, 19, 10, 25)
     assert_same(r, o)
     assert r["stats"].buckets == 64 * r["stats"].buckets // 64 and r["stats"].buckets >= 64
+
+
+def test_count_split3_auto_large(gpu_ctx, hga_mod):
+    # 4x C2 (1.06 G instances): fine buckets far past one LDS table, so count_run adds the third
+    # split level by itself; size-independent checks (every window counted once at min 1, rows
+    # strictly ascending after rows())
+    g = hga_mod.gen_genome(20_000_000, 31)
+    h = hga_mod.gen_haplotype(g, 0.005, 0, 32)
+    ra = hga_mod.gen_art(g, 4_000_000, 150, 33)
+    rb = hga_mod.gen_art(h, 4_000_000, 150, 34)
+    gpu_ctx.count_begin(19, 2)
+    gpu_ctx.count_add(0, ra.seq)
+    gpu_ctx.count_add(1, rb.seq)
+    del ra, rb
+    gpu_ctx.count_run(1)
+    st = gpu_ctx.count_stats()
+    assert st.instances == 8_000_000 * 132
+    assert st.buckets > 4096 and st.max_split == 1
+    keys, counts = gpu_ctx.rows()
+    assert int(counts.astype(np.uint64).sum()) == st.instances
+    assert np.all(np.diff(keys.astype(np.int64)) > 0)
+    hist = gpu_ctx.spec_hist(oracle.THRESHOLDS)
+    assert int(hist[:, 2].sum()) == len(keys)
