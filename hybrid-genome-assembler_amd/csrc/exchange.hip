@@ -384,14 +384,15 @@ __global__ void __launch_bounds__(KX_T) kx_pack_scatter(const uint64_t* __restri
 }
 
 // ---------------------------------------------------------------- owner merge by hash buckets
-// The owner's pieces (any order, one key split over up to one piece per sender and count
-// overflow) are grouped by the top mb bits of the counting mix (kmer_dev.hpp Mix: the senders'
-// rows come out of kc_count_s in runs of one fine bucket, so with mb = their fb the scatter
-// moves whole runs) — kx_mb_hist counts them per
-// (bucket, tile), one exclusive scan gives every (bucket, tile) its output run, kx_mb_scatter
-// writes them — and each bucket (about T/2 pieces) is summed in an LDS hash table by one
-// workgroup (kx_mb_merge), which applies the per-file drop and writes the kept rows.  No sort:
-// spec_hist is order-free and the export sort (kc_select + sort_export_u64) orders the keys.
+// The owner's pieces (any order; a key has up to one piece per sender, more when a count passes
+// the piece width) are binned by the top mb bits of the counting mix (kmer_dev.hpp Mix: the
+// senders' rows come out of kc_count_s in runs of one fine bucket, so the bins arrive in runs):
+// kx_mb_hist adds every tile's per-bin counts to the bin totals (one device atomic per nonzero
+// bin), a scan of the totals gives the bin starts, kx_mb_scatter reserves each tile's run per bin
+// with one device atomic and writes it; kx_mb_merge sums each bin (about T/2 pieces) in an LDS
+// hash table, applies the per-file drop and writes the kept rows into the bin's own range, and
+// kx_mb_compact packs them after a scan of the per-bin row counts.  No sort: spec_hist is
+// order-free and the export sort (kc_select + sort_export_u64) orders the keys.
 constexpr int MB_NT = 1024;
 constexpr int MB_R = 16;                       // pieces per thread per tile
 constexpr uint64_t MB_TILE = (uint64_t)MB_NT * MB_R;
