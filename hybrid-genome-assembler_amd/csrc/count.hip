@@ -2,7 +2,7 @@
 // + `dump` + `sort` (src/occurrences/run_jellyfish.sh:3-6) and for the two string
 // k-way merge passes of JellyfishOccurrenceReader (JellyfishOccurrenceReader.cpp:63-135).
 //
-// Pipeline (all HBM-bound integer work, no MFMA):
+// Pipeline (integer / byte work, no MFMA; DESIGN.md §4 has each kernel's bound):
 //   P  kc_pack   ASCII -> 2-bit codes (u32 per 16 bases) + base-valid bits (u16 per 16).
 //   B1 kc_bin1   per tile of 8K window ends: closed-form canonical k-mer of every valid
 //                window from packed frames, bijective 2k-bit mix; the top fb1 (<= 6) bits
@@ -13,12 +13,15 @@
 //                chunk table of the level-1 regions.
 //   B2 kc_rebin  per 8K-element chunk of a level-1 region: the next fb2 bits pick the fine
 //                bucket (again <= 64-way, coalesced); writes the remainder (u32 when <= 31 bits).
+//   B3 kc_split3 (inputs far above C2 only) per fine bucket: the next fb3 bits pick one of
+//                2^fb3 sub-buckets, staged in LDS and written in runs; the count kernels then
+//                run on the sub-buckets.
 //   C  kc_count  one workgroup per fine bucket: LDS open-addressing table keyed by the
 //                remainder with one u32 counter per file; adaptive sub-range splitting
 //                if a bucket holds more distinct k-mers than the table; per-file drop
 //                of counts < min (jellyfish --bc); emit merged rows (key, counts[F]).
 //   H  kc_spec_hist   specificity x total histogram (get_specificity, :88-108).
-//   X  kc_select      rows with lower <= total <= upper, + radix sort ascending
+//   X  kc_select      rows with lower <= total <= upper, + the export sort ascending
 //                     (export_kmers, :110-135; numeric order == LC_ALL=C order).
 #include <algorithm>
 #include <cstdlib>
