@@ -306,6 +306,23 @@ def ingest_leg(ga, gb, threads):
                           "bases": int(n), "records": int(len(rec["offsets"]) - 1)}
         hga.set_host_threads(0)
         out["note"] = "wall time through the ctypes mirror (includes the copy into Python bytes)"
+        # the drop-in CLI end to end on the same files (src/jellyfish_occurrences.cpp's argv and
+        # stdin; no dump caches yet, so it counts on the GPU and writes them, as run_jellyfish.sh would)
+        cli = os.path.join(ROOT, "hybrid-genome-assembler_amd", "bin", "jf_occurrences")
+        if os.path.exists(cli):
+            import subprocess
+            env = dict(os.environ, HGA_PLOT_CMD="cat > /dev/null")
+            t0 = time.perf_counter()
+            r = subprocess.run([cli, *paths, "-k", str(K)], input=f"{LOWER} {UPPER} 1\n", text=True,
+                               capture_output=True, cwd=d, env=env, timeout=300)
+            dt = time.perf_counter() - t0
+            exp = os.path.join(d, f"{K}-mers_{LOWER}_{UPPER}_100%.txt")
+            out["cli_jf_occurrences"] = {
+                "argv": f"jf_occurrences mg1655.fq uti89.fq -k {K}  (stdin: {LOWER} {UPPER} 1)",
+                "rc": r.returncode, "wall_s": round(dt, 3),
+                "exported_lines": sum(1 for _ in open(exp)) if r.returncode == 0 and os.path.exists(exp) else None,
+                "note": "one process: HIP init, FASTQ ingest, upload, count, the two per-file sorted dump "
+                        "caches written as text, histogram wire string, export file"}
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
