@@ -1790,20 +1790,21 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
     for (uint64_t ch = blockIdx.x; ch < chunks; ch += gridDim.x) {
         const uint64_t base = ch * NT_H * SEL_R;
         uint64_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
+        // the first two files' counts of all SEL_R rows loaded together (rows < cap are allocated)
+        uint32_t c0[SEL_R], c1[SEL_R];
+#pragma unroll
+        for (int q = 0; q < SEL_R; ++q) {
+            const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
+            c0[q] = r < cap ? cnt[r] : 0u;
+            c1[q] = (F > 1 && r < cap) ? cnt[cap + r] : 0u;
+        }
 #pragma unroll
         for (int q = 0; q < SEL_R; ++q) {
             const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
             if (r >= rows) continue;
-            int64_t total = 0;
-            uint32_t nz = 0;
-#pragma unroll
-            for (uint32_t f = 0; f < 4; ++f)   // the common file counts unrolled: loads issued together
-                if (f < F) {
-                    const uint32_t c = cnt[(size_t)f * cap + r];
-                    total += c;
-                    nz += c > 0;
-                }
-            for (uint32_t f = 4; f < F; ++f) {
+            int64_t total = (int64_t)c0[q] + c1[q];
+            uint32_t nz = (c0[q] > 0) + (c1[q] > 0);
+            for (uint32_t f = 2; f < F; ++f) {
                 const uint32_t c = cnt[(size_t)f * cap + r];
                 total += c;
                 nz += c > 0;
@@ -1813,6 +1814,11 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
                 if (nz == 1) disc |= 1ull << q;
             }
         }
+        // the kept rows' keys requested now: their latency overlaps the scans and the cursor atomic
+        uint64_t kv[SEL_R];
+#pragma unroll
+        for (int q = 0; q < SEL_R; ++q)
+            kv[q] = ((take >> q) & 1ull) ? keys[base + (uint64_t)q * NT_H + threadIdx.x] : 0ull;
         uint32_t tot;
         const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popcll(take), ws, &tot);
         // same-address device atomics serialise (≈88/µs chip-wide): one pair per chunk
@@ -1827,11 +1833,9 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
 #pragma unroll
         for (int q = 0; q < SEL_R; ++q)
             if ((take >> q) & 1ull) {
-                const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
-                const uint64_t kv = keys[r];
-                stage[o++] = kv | (flag_bit ? (((disc >> q) & 1ull) << 63) : 0ull);
+                stage[o++] = kv[q] | (flag_bit ? (((disc >> q) & 1ull) << 63) : 0ull);
                 if (!flag_bit) sflag[o - 1] = (uint8_t)((disc >> q) & 1ull);
-                if (dhist_rows) atomicAdd(&dh[(uint32_t)(kv >> hshift) & (SEL_HB - 1)], 1u);
+                if (dhist_rows) atomicAdd(&dh[(uint32_t)(kv[q] >> hshift) & (SEL_HB - 1)], 1u);
             }
         __syncthreads();
         const uint64_t ob = s_base;
