@@ -57,6 +57,9 @@
 #ifndef HGA_EXP_B1_COMPUTEONLY
 #define HGA_EXP_B1_COMPUTEONLY 0
 #endif
+#ifndef HGA_EXP_B1_DIRECT
+#define HGA_EXP_B1_DIRECT 0
+#endif
 #ifndef HGA_EXP_B1_NOFHIST
 #define HGA_EXP_B1_NOFHIST 0
 #endif
@@ -317,6 +320,18 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
             if (tid == 63) off1[nb1] = inc;
         }
         lds_barrier();
+#if HGA_EXP_B1_DIRECT
+        // timing experiment: every element straight to its block slot (no LDS stage / flush)
+#pragma unroll
+        for (int j = 0; j < P_B; ++j)
+            if ((wm >> j) & 1u) {
+                const uint32_t d = dd[j], ta = take_a[d];
+                const unsigned long long g = rk[j] < ta ? base_a[d] + rk[j] : base_b[d] + (rk[j] - ta);
+                if (g < pool_cap) out1[g] = ee[j];
+            }
+        lds_barrier();
+        continue;
+#endif
 #pragma unroll
         for (int j = 0; j < P_B; ++j)
             if ((wm >> j) & 1u) stage[off1[dd[j]] + rk[j]] = ee[j];
