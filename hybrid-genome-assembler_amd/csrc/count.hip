@@ -113,8 +113,12 @@ constexpr int MAX_FB1 = HGA_MAX_FB1;    // level-1 fan-out <= 64
 constexpr int NB1_MAX = 1 << MAX_FB1;
 constexpr int NB2_MAX = 1 << (MAX_FB - MAX_FB1 > 6 ? MAX_FB - MAX_FB1 : 6);   // level-2 fan-out
 static_assert(NB1_MAX <= 64 && NB2_MAX <= 128, "bin1 scans <= 64 regions with one wave, rebin <= 128 digits with two");
-constexpr int NT_R = 512;     // re-bin workgroup
-constexpr int CH_R = NT_R * 16;        // 8192 elements per re-bin chunk
+#ifndef HGA_NT_R
+#define HGA_NT_R 512
+#endif
+constexpr int NT_R = HGA_NT_R;   // re-bin workgroup
+constexpr int CH_R = 8192;       // elements per re-bin chunk (one level-1 block)
+static_assert(NT_R >= 128 && CH_R % NT_R == 0, "rebin scans 128 digits with two waves");
 constexpr int NT_C = HGA_NT_C;   // threads of the per-bucket count workgroup
 #ifndef HGA_PF_C
 #define HGA_PF_C 8
