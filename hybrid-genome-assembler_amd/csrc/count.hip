@@ -114,11 +114,19 @@ constexpr int NB1_MAX = 1 << MAX_FB1;
 constexpr int NB2_MAX = 1 << (MAX_FB - MAX_FB1 > 6 ? MAX_FB - MAX_FB1 : 6);   // level-2 fan-out
 static_assert(NB1_MAX <= 64 && NB2_MAX <= 128, "bin1 scans <= 64 regions with one wave, rebin <= 128 digits with two");
 #ifndef HGA_NT_R
-#define HGA_NT_R 512
+#define HGA_NT_R 256
 #endif
-constexpr int NT_R = HGA_NT_R;   // re-bin workgroup
+#ifndef HGA_NT_R64
+#define HGA_NT_R64 512
+#endif
 constexpr int CH_R = 8192;       // elements per re-bin chunk (one level-1 block)
-static_assert(NT_R >= 128 && CH_R % NT_R == 0, "rebin scans 128 digits with two waves");
+// re-bin workgroup: 256 threads for u32 remainders (4 workgroups per CU on 33 KB of stage:
+// 0.456 vs 0.472 ms at C2 with 512), 512 for u64 ones (two per CU on 66 KB)
+template <class E>
+constexpr int rebin_nt() { return sizeof(E) == 4 ? HGA_NT_R : HGA_NT_R64; }
+constexpr int NT_R_MAX = HGA_NT_R > HGA_NT_R64 ? HGA_NT_R : HGA_NT_R64;
+static_assert(HGA_NT_R >= 128 && HGA_NT_R64 >= 128 && CH_R % HGA_NT_R == 0 && CH_R % HGA_NT_R64 == 0,
+              "rebin scans 128 digits with two waves");
 constexpr int NT_C = HGA_NT_C;   // threads of the per-bucket count workgroup
 #ifndef HGA_PF_C
 #define HGA_PF_C 8
@@ -556,11 +564,12 @@ __global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, cons
 // One workgroup per level-1 block: the next fb2 bits pick the fine bucket (<= 64-way,
 // ranked through LDS so each bucket's run is one coalesced segment).
 template <class E1, class E>
-__global__ void __launch_bounds__(NT_R) kc_rebin(const E1* __restrict__ in1, const Blk* __restrict__ table,
+__global__ void __launch_bounds__(NT_R_MAX) kc_rebin(const E1* __restrict__ in1, const Blk* __restrict__ table,
                                                  const unsigned long long* __restrict__ gstat, uint32_t W,
                                                  KP kp, const uint32_t* __restrict__ nblk,
                                                  unsigned long long* __restrict__ off,
                                                  E* __restrict__ out) {
+    constexpr int NT_R = rebin_nt<E>();
     constexpr int IT = CH_R / NT_R;
     static_assert(CH_R >= (int)BLK, "a block must fit one re-bin pass");
     __shared__ uint32_t cnt2[NB2_MAX];
@@ -2088,7 +2097,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const unsigned rebin_grid = (unsigned)std::max<uint64_t>(1, table_cap);   // exits past gstat[3]
     c->launch("kc_rebin", [&] {
 #define HGA_REBIN(E1T, ET)                                                                                 \
-    hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3(rebin_grid), dim3(NT_R), 0, c->stream,                    \
+    hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3(rebin_grid), dim3(rebin_nt<ET>()), 0, c->stream,                    \
                        static_cast<const E1T*>(binned1), table, gstat, W, kp, nblk, off, static_cast<ET*>(binned))
         if (e1_32 && e32) HGA_REBIN(uint32_t, uint32_t);
         else if (e32) HGA_REBIN(uint64_t, uint32_t);
