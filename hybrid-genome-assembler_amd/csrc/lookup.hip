@@ -28,7 +28,10 @@ namespace {
 #ifndef HGA_FBITS2
 #define HGA_FBITS2 22
 #endif
-constexpr int LK_T = 256;
+#ifndef HGA_LK_T
+#define HGA_LK_T 256
+#endif
+constexpr int LK_T = HGA_LK_T;   // lookup scan workgroup
 constexpr int LK_P = 32;                  // window ends per thread (frame of 4 words)
 constexpr int LK_QN = 256;                // filter-pass queue entries per wave
 constexpr int LK_ST = 2048;               // emit pass: hits per tile staged in LDS (more: direct stores)
