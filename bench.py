@@ -152,38 +152,87 @@ KERNEL_BYTES = {
 }
 
 
-def cpu_baseline(ra, rb, threads):
-    """The oracle (C++ restatement, multi-threaded) over a bounded sample of the same workload."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(ra, rb, threads, parse_s=None):
+    """The oracle (C++ restatement of the count stage) timed on this box's host cores
+    (BASELINE.md §3): per-file exact counts + --bc drop + merge + specificity + select.
+      value          the whole C2 workload, `threads` threads (the box's CPU share), no parsing;
+      with_parsing   the same plus the FASTQ parse of the C2 pair at the same thread count (ingest leg);
+      one_core       1/16 of each file, 1 thread;
+      reference_like 1/64 of file A, 1 thread, the reference's map-based KmerIterator loop
+                     (KmerIterator.cpp:7-19,54-63) into a std::unordered_map (SURVEY.md §8(d)(2))."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    frac = 4   # a quarter of each file's reads
-    sa = ra.seq[: ra.seq.find(b"\n", len(ra.seq) // frac)]
-    sb = rb.seq[: rb.seq.find(b"\n", len(rb.seq) // frac)]
-    inst = oracle.count_instances(sa, K) + oracle.count_instances(sb, K)
+    streams = [ra.seq, rb.seq]
+    inst = sum(oracle.count_instances(s, K) for s in streams)
+
+    def stage(ss, th):
+        t0 = time.perf_counter()
+        keys, counts = oracle.count_files_mt(ss, K, 2, th)
+        oracle.specificity(counts, THRESHOLDS)
+        oracle.select(keys, counts, LOWER, UPPER)
+        return time.perf_counter() - t0
+
+    dt = stage(streams, threads)
+    sub16 = [s[: s.find(b"\n", len(s) // 16)] for s in streams]
+    inst16 = sum(oracle.count_instances(s, K) for s in sub16)
+    dt1 = stage(sub16, 1)
+    sub64 = ra.seq[: ra.seq.find(b"\n", len(ra.seq) // 64)]
+    inst64 = oracle.count_instances(sub64, K)
     t0 = time.perf_counter()
-    dumps = [oracle.count_stream(s, K, 2, threads=threads) for s in (sa, sb)]
-    keys, counts = oracle.merge(dumps)
-    oracle.specificity(counts, THRESHOLDS)
-    oracle.select(keys, counts, LOWER, UPPER)
-    dt = time.perf_counter() - t0
-    return {"value": inst / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
-            "sample": f"first 1/{frac} of each C2 read file ({inst} 19-mer windows); oracle count "
-                      f"(std::unordered_map, {threads} threads) + merge + specificity + select",
-            "seconds": round(dt, 3)}
+    oracle.count_reference_like(sub64, K, 2)
+    dtr = time.perf_counter() - t0
+    out = {"value": inst / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+           "sample": f"the whole C2 workload ({inst} 19-mer windows, 2 files), resident in host memory: oracle "
+                     f"count stage (range-partitioned exact counts, sort + run-length, --bc drop, merge; "
+                     f"{threads} threads) + specificity + select[10,25]",
+           "seconds": round(dt, 3), "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "threads_note": "threads = the GPU box's CPU share for one GPU (16), not nproc, which counts the whole host",
+           "one_core": {"value": round(inst16 / dt1, 1), "unit": "k-mers/s", "cores": 1,
+                        "sample": f"first 1/16 of each C2 file ({inst16} windows), same stage", "seconds": round(dt1, 3)},
+           "reference_like": {"value": round(inst64 / dtr, 1), "unit": "k-mers/s", "cores": 1,
+                              "sample": f"first 1/64 of the MG1655-sized file ({inst64} windows): per read the "
+                                        "reference's KmerIterator loop with its unordered_map<char,Kmer> base maps, "
+                                        "counted in a std::unordered_map, --bc drop, sorted dump",
+                              "seconds": round(dtr, 3)}}
+    if parse_s:
+        out["with_parsing"] = {"value": round(inst / (dt + parse_s), 1), "unit": "k-mers/s", "cores": threads,
+                               "parse_seconds": round(parse_s, 3),
+                               "sample": "FASTQ parse of the C2 pair (host reader, same threads) + the count stage"}
+    return out
 
 
 def cpu_lookup_baseline(bases, offsets, sdk, threads):
+    """construct_indices (ReadClusteringEngine.cpp:234-299) restated (oracle, all 9 outputs) on a
+    bounded sample of the C3 reads: `threads` threads and 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    n = min(len(offsets) - 1, 6000)
-    sub_off = offsets[: n + 1]
-    sub = bases[: int(sub_off[-1])]
-    t0 = time.perf_counter()
-    oracle.lookup_hits_mt(sub, sub_off, K, sdk, threads)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "reads/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} C3 reads, std::unordered_set lookup of every window, {threads} threads",
-            "seconds": round(dt, 3)}
+    out = {"unit": "reads/s", "kind": "port", "nproc": os.cpu_count(), "cpu_model": cpu_model()}
+    for label, n_r, th in (("all", 24000, threads), ("one_core", 2000, 1)):
+        n = min(len(offsets) - 1, n_r)
+        sub_off = offsets[: n + 1]
+        sub = bases[: int(sub_off[-1])]
+        w = int(sum(max(int(l) - K + 1, 0) for l in np.diff(sub_off)))
+        t0 = time.perf_counter()
+        oracle.construct_indices(sub, sub_off, K, sdk, 1, threads=th)
+        dt = time.perf_counter() - t0
+        rec = {"value": round(n / dt, 1), "windows_per_s": round(w / dt, 1), "cores": th,
+               "sample": f"first {n} C3 reads ({w} windows), oracle construct_indices (9 CSR outputs), {th} threads",
+               "seconds": round(dt, 3)}
+        if label == "all":
+            out.update(rec)
+        else:
+            out["one_core"] = rec
+    return out
 
 
 def connections_leg(ctx2, D, reps, args):
@@ -500,14 +549,20 @@ def main():
         dtl = D.max((time.perf_counter() - t0) / reps)
         s = ctx2.lookup_sizes()
         lk_ms = lk.get("lk_count", 0) + lk.get("lk_emit", 0)
-        lk_bytes = s.windows * 2 * 12.25 + 12 * s.hits    # two walks: 0.25 B input + 12 B slot read per window
+        # 0.25 B packed input + 12 B slot read per window, 12 B out per hit (once)
+        lk_bytes = s.windows * 12.25 + 12 * s.hits
         result["categorize"] = {
             "workload": "C3: Nanosim-H-like 75x long reads of the C2 pair vs the C2 [10,25] export (k=19)",
             "reads": int(s.n_reads), "bases": int(len(bases)), "windows": int(s.windows), "hits": int(s.hits),
             "sdk": int(s.n_sdk), "ms": round(dtl * 1e3, 3), "reads_per_s": round(D.sum(s.n_reads) / dtl, 1),
             "windows_per_s": round(D.sum(s.windows) / dtl, 1), "kernels_ms": lk,
-            "lookup_roofline": {"model": "12.25 B per window per walk + 12 B per hit (SURVEY.md §8(d))",
-                                "achieved": round(lk_bytes / (lk_ms * 1e-3) / 1e9, 1) if lk_ms else None},
+            "lookup_roofline": {"model": "12.25 B per window + 12 B per hit (SURVEY.md §8(d)), counted once",
+                                "kernel": "lk_scan<0> + lk_scan<1> (lk_count + lk_emit)", "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s",
+                                "achieved": round(lk_bytes / (lk_ms * 1e-3) / 1e9, 1) if lk_ms else None,
+                                "frac": round(lk_bytes / (lk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if lk_ms else None,
+                                "whole_lookup_achieved": round(lk_bytes / dtl / 1e9, 1),
+                                "whole_lookup_frac": round(lk_bytes / dtl / 1e9 / HBM_PEAK_GBS, 4)},
         }
         result["categorize"]["connections"] = connections_leg(ctx2, D, reps, args)
         result["categorize"]["hll_auto_k"] = hll_leg(ctx2, D, len(bases), bases, offsets, args)
@@ -515,10 +570,11 @@ def main():
         if not args.no_cpu and D.rank == 0:
             result["categorize"]["cpu_baseline"] = cpu_lookup_baseline(bases, offsets, sdk, args.cpu_threads)
 
-    if not args.no_cpu and D.rank == 0:
-        result["cpu_baseline"] = cpu_baseline(ra, rb, args.cpu_threads)
     if not args.no_ingest and D.rank == 0 and D.world == 1:
         result["ingest"] = ingest_leg(ga, gb, args.cpu_threads)
+    if not args.no_cpu and D.rank == 0:
+        parse_s = result.get("ingest", {}).get("parallel", {}).get("jf_stream_s")
+        result["cpu_baseline"] = cpu_baseline(ra, rb, args.cpu_threads, parse_s)
     if not args.no_scale and D.world == 1:
         result["scale_c4_shard"] = scale_leg(dev)
     ctx.close()

@@ -33,60 +33,6 @@
 
 // Timing experiments (tools/build_variants.sh): each disables one part of a kernel; results are
 // wrong with any of them set, the default build has all 0.
-#ifndef HGA_S_NEXT
-#define HGA_S_NEXT 0
-#endif
-#ifndef HGA_EXP_S_HITSTORE
-#define HGA_EXP_S_HITSTORE 0
-#endif
-#ifndef HGA_EXP_S_NOHIT
-#define HGA_EXP_S_NOHIT 0
-#endif
-#ifndef HGA_EXP_LOADONLY
-#define HGA_EXP_LOADONLY 0
-#endif
-#ifndef HGA_EXP_NOADD
-#define HGA_EXP_NOADD 0
-#endif
-#ifndef HGA_EXP_NOMISS
-#define HGA_EXP_NOMISS 0
-#endif
-#ifndef HGA_EXP_NOCLAIM
-#define HGA_EXP_NOCLAIM 0
-#endif
-#ifndef HGA_EXP_B1_COMPUTEONLY
-#define HGA_EXP_B1_COMPUTEONLY 0
-#endif
-#ifndef HGA_EXP_B1_DIRECT
-#define HGA_EXP_B1_DIRECT 0
-#endif
-#ifndef HGA_EXP_B1_NOFHIST
-#define HGA_EXP_B1_NOFHIST 0
-#endif
-#ifndef HGA_EXP_B1_NOFLUSH
-#define HGA_EXP_B1_NOFLUSH 0
-#endif
-#ifndef HGA_EXP_SH_LOADONLY
-#define HGA_EXP_SH_LOADONLY 0
-#endif
-#ifndef HGA_EXP_SH_NOROWS
-#define HGA_EXP_SH_NOROWS 0
-#endif
-#ifndef HGA_EXP_SH_NODIV
-#define HGA_EXP_SH_NODIV 0
-#endif
-#ifndef HGA_EXP_SH_NOLDS
-#define HGA_EXP_SH_NOLDS 0
-#endif
-#ifndef HGA_EXP_SH_NOFLUSH
-#define HGA_EXP_SH_NOFLUSH 0
-#endif
-#ifndef HGA_EXP_PK_NOVD
-#define HGA_EXP_PK_NOVD 0
-#endif
-#ifndef HGA_EXP_NOEMIT
-#define HGA_EXP_NOEMIT 0
-#endif
 
 namespace hga {
 namespace {
@@ -203,14 +149,11 @@ struct BinFile {
     uint64_t woff;   // first word of the file's region in the packed buffers
     uint64_t n;      // bases
     uint32_t w0, pad;
-    const uint8_t* seq;   // the file's ASCII bases (HGA_B1_ASCII: bin1 packs its own frames)
+    const uint8_t* seq;   // the file's ASCII bases
 };
 
 #ifndef HGA_B1_PER_CU
 #define HGA_B1_PER_CU 2   // bin1 super-tiles per CU
-#endif
-#ifndef HGA_B1_ASCII
-#define HGA_B1_ASCII 0    // 1: bin1 packs its frames from the ASCII bases itself (no kc_pack; measured slower)
 #endif
 #ifndef HGA_B1_WAVES
 #define HGA_B1_WAVES 1
@@ -260,22 +203,10 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
     const uint64_t start = (uint64_t)(w - files[file].w0) * st_pos;
     const uint64_t end = start + st_pos < n ? start + st_pos : n;
     uint32_t inst = 0;
-#if HGA_B1_ASCII
-    const uint8_t* __restrict__ seq = files[file].seq;
-#endif
     for (uint64_t t0 = start; t0 < end; t0 += TP_B) {
         const uint64_t p0 = t0 + (uint64_t)tid * P_B;
         Frame<P_B> f;
-#if HGA_B1_ASCII
-        // bases [p0-32, p0+16) straight from the ASCII stream (bytes outside the file are no base)
-        FrameRaw<P_B> raw;
-#pragma unroll
-        for (int i = 0; i < FrameRaw<P_B>::NW; ++i)
-            pack_bytes<false>(load16(seq, (int64_t)p0 - 32 + 16 * i, n), raw.x[i], raw.v[i]);
-        const uint64_t v64 = build_frame<P_B, false>(raw, kp.k, f);
-#else
         const uint64_t v64 = load_frame<P_B, false>(pk, vd, PAD_WORDS + p0 / 16 - 2, kp.k, f);
-#endif
         const uint32_t wm = (uint32_t)(runs_of(v64, kp.k) >> 32);   // bit j: window at p0+j valid
         uint32_t dd[P_B], rk[P_B];
         E1 ee[P_B];
@@ -285,27 +216,12 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
             dd[j] = region_of(h, kp);
             ee[j] = (E1)(h & kp.r1mask);
             rk[j] = 0;
-#if HGA_EXP_B1_COMPUTEONLY
-            rk[j] = (uint32_t)ee[j] ^ dd[j];
-#else
             if ((wm >> j) & 1u) {
                 rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
-#if !HGA_EXP_B1_NOFHIST
                 atomicAdd(&fhist[bucket_of(h, kp)], 1u);
-#endif
             }
-#endif
         }
         inst += __popc(wm);
-#if HGA_EXP_B1_COMPUTEONLY
-        {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int j = 0; j < P_B; ++j) acc += rk[j];
-            if (acc == 0x12345678u) out1[0] = 0;
-            continue;
-        }
-#endif
         lds_barrier();
         if (tid < 64) {   // one wave: scan the <= 64 region counts, place them in the blocks
             const uint32_t c = tid < (int)nb1 ? cnt1[tid] : 0u;
@@ -332,18 +248,6 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
             if (tid == 63) off1[nb1] = inc;
         }
         lds_barrier();
-#if HGA_EXP_B1_DIRECT
-        // timing experiment: every element straight to its block slot (no LDS stage / flush)
-#pragma unroll
-        for (int j = 0; j < P_B; ++j)
-            if ((wm >> j) & 1u) {
-                const uint32_t d = dd[j], ta = take_a[d];
-                const unsigned long long g = rk[j] < ta ? base_a[d] + rk[j] : base_b[d] + (rk[j] - ta);
-                if (g < pool_cap) out1[g] = ee[j];
-            }
-        lds_barrier();
-        continue;
-#endif
 #pragma unroll
         for (int j = 0; j < P_B; ++j)
             if ((wm >> j) & 1u) stage[off1[dd[j]] + rk[j]] = ee[j];
@@ -354,11 +258,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
             const unsigned long long ba = base_a[d], bb = base_b[d];
             for (uint32_t jj = (uint32_t)(tid & 63); jj < len; jj += 64) {
                 const unsigned long long g = jj < ta ? ba + jj : bb + (jj - ta);
-#if HGA_EXP_B1_NOFLUSH
-                if (g < pool_cap && stage[o + jj] == (E1)0x12345677u) out1[g] = 0;
-#else
                 if (g < pool_cap) out1[g] = stage[o + jj];
-#endif
             }
         }
         lds_barrier();
@@ -412,18 +312,11 @@ __global__ void kc_pack_files(const PackFile* __restrict__ files, uint32_t F, ui
         uint32_t code = 0, valid = 0;
         if (in[u]) pack_bytes<false>(raw[u], code, valid);
         pk[g] = code;
-#if HGA_EXP_PK_NOVD
-        if (valid == 0x12345u)
-#endif
         vd[g] = (uint16_t)valid;
     }
 }
 
 // Pipeline counters when there is no pack pass: gstat[3] = the first spill block, the rest 0.
-__global__ void kc_init_stat(unsigned long long* __restrict__ gstat, uint64_t n_first) {
-    if (threadIdx.x < 8) gstat[threadIdx.x] = threadIdx.x == 3 ? (unsigned long long)n_first : 0ull;
-}
-
 // ---------------------------------------------------------------- layout
 // off[b * W + w] = wcnt[w * nb + b] (64 x 64 LDS tiles), off[nb * W] = 0.  One exclusive scan
 // of off then gives every (fine bucket, workgroup) its first output slot: buckets in order,
@@ -722,9 +615,6 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 constexpr uint32_t QN_C = 128;   // miss-queue entries per wave
-#ifndef HGA_CNT_BRANCHLESS
-#define HGA_CNT_BRANCHLESS 0
-#endif
 #ifndef HGA_EMIT_STAGE
 #define HGA_EMIT_STAGE 1
 #endif
@@ -758,7 +648,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
     const uint32_t full_hi = 1u << SUBB;
     const uint32_t mc = min_count ? min_count : 1u;
     const uint32_t G = T / GRP;
-    // every bucket (blist null), or the buckets listed by kc_count_p (count in gstat[5])
+    // every bucket (blist null), or the buckets listed by kc_count_s (count in gstat[5])
     const uint32_t n_b = blist ? (uint32_t)gstat[5] : gridDim.x;
     for (uint32_t it = blockIdx.x; it < n_b; it += gridDim.x) {
     const uint32_t b = blist ? blist[it] : it;
@@ -825,15 +715,6 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                 // 1) every home group read before any counter is touched (the counters share
                 //    the LDS array, so an atomic in between would serialise the reads): one LDS
                 //    round trip settles every element whose key already sits in its home group
-#if HGA_EXP_LOADONLY
-                {
-                    uint32_t acc = 0;
-#pragma unroll
-                    for (int q = 0; q < PF_C; ++q) acc += (uint32_t)rv[q];
-                    if (acc == 0x12345678u) atomicAdd(&cf[0], 1u);
-                    continue;
-                }
-#endif
                 E kg[PF_C][GRP];
 #pragma unroll
                 for (int q = 0; q < PF_C; ++q) read_group(keys, (uint32_t)rv[q] & (G - 1), kg[q]);
@@ -845,24 +726,9 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 #pragma unroll
                     for (int t = GRP - 1; t >= 0; --t) w = kg[q][t] == rv[q] ? t : w;
                     const bool live = rv[q] != EMPTY;   // EMPTY would match an empty slot
-#if HGA_CNT_BRANCHLESS
-                    // every lane issues the add (+0 into its home group's first slot when it
-                    // misses): no per-element exec-mask branch around the LDS atomic
-                    const bool hit = live && w >= 0;
-                    atomicAdd(&cf[GRP * g + (hit ? (uint32_t)w : 0u)], hit ? 1u : 0u);
-                    miss |= (live && !hit ? 1u : 0u) << q;
-#else
-#if HGA_EXP_NOADD
-                    if (live && w < 0) miss |= 1u << q;
-#else
                     if (live && w >= 0) atomicAdd(&cf[GRP * g + w], 1u);
                     else if (live) miss |= 1u << q;
-#endif
-#endif
                 }
-#if HGA_EXP_NOMISS
-                miss = 0;
-#endif
                 // the misses (new keys, keys displaced from home) are compacted into this
                 // wave's queue once per batch
                 const uint32_t nm = (uint32_t)__popc(miss);
@@ -1017,338 +883,21 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
     }
 }
 
-// ---------------------------------------------------------------- pass C (packed entries)
-// F <= 2 files, u32 remainders, every per-file run of the bucket < 65536 instances (so no
-// count can pass 16 bits): one u64 LDS entry per slot, key in the low 32 bits, the counts in
-// the high 32 (F = 1: one 32-bit count; F = 2: file 0 in bits 32-47, file 1 in bits 48-63).
-// A hit is one ds_add_u64 into the entry it matched; a new key claims the first empty slot of
-// its home group with one ds_cmpst_b64 that also sets its count — inline, no loop — so only
-// keys whose home group is full (or that lost a claim race) go through the per-wave queue.
-// 64 KB per workgroup: two workgroups per CU, one's prologue / emit overlaps the other's stream.
-// Buckets this kernel cannot take (a per-file run >= 65536) are listed for kc_count.
-#ifndef HGA_COUNT_SOA
-#define HGA_COUNT_SOA 1   // kc_count_s (SoA keys/counts) rather than kc_count_p (u64 entries)
-#endif
-#ifndef HGA_S_BRANCHLESS
-#define HGA_S_BRANCHLESS 1   // kc_count_s: hits added by every lane (non-hits into per-lane dummy words)
-#endif
 #ifndef HGA_NT_P
 #define HGA_NT_P 512
 #endif
 #ifndef HGA_PF_P
 #define HGA_PF_P 8
 #endif
-#ifndef HGA_GP_P
-#define HGA_GP_P 2
-#endif
 constexpr int NT_P = HGA_NT_P;
 constexpr int PF_P = HGA_PF_P;          // binned elements per thread per batch
 static_assert(PF_P <= 15, "miss counts are scanned as 4-bit values");
-constexpr int GP_P = HGA_GP_P;          // entries per probe group (2: one ds_read_b128)
-constexpr uint32_t T_P = 8192;          // entries (64 KB)
-constexpr uint32_t G_P = T_P / GP_P;
 constexpr uint32_t QN_P = 128;          // per-wave queue of unsettled keys
 constexpr uint32_t MAXPROBE_P = 64;     // groups probed before the table counts as over-full
-constexpr uint64_t EMPTY_P = 0xFFFFFFFFull;
-static_assert(T_P % NT_P == 0, "emit: whole slots per thread");
 
-__device__ __forceinline__ void read_group_p(const uint64_t* tab, uint32_t g, uint64_t (&e)[GP_P]) {
-#pragma unroll
-    for (int t = 0; t < GP_P / 2; ++t) {
-        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(tab)[g * (GP_P / 2) + t];
-        e[2 * t] = v.x;
-        e[2 * t + 1] = v.y;
-    }
-}
-
-// Settle key r (count +inc) by probing from its home group; false if MAXPROBE_P groups were full.
-__device__ __forceinline__ bool probe_p(uint64_t* tab, uint32_t r, uint64_t inc) {
-    uint32_t g = r & (G_P - 1);
-    for (uint32_t steps = 0; steps < MAXPROBE_P;) {
-        uint64_t e[GP_P];
-        read_group_p(tab, g, e);
-        int w = -1, e0 = -1;
-#pragma unroll
-        for (int t = GP_P - 1; t >= 0; --t) {
-            w = (uint32_t)e[t] == r ? t : w;
-            e0 = e[t] == EMPTY_P ? t : e0;
-        }
-        if (w >= 0) {
-            atomicAdd((unsigned long long*)&tab[g * GP_P + w], (unsigned long long)inc);
-            return true;
-        }
-        if (e0 >= 0) {
-            const uint32_t sl = g * GP_P + (uint32_t)e0;
-            const uint64_t old = atomicCAS((unsigned long long*)&tab[sl], (unsigned long long)EMPTY_P,
-                                           (unsigned long long)(inc | r));
-            if (old == EMPTY_P) return true;
-            if ((uint32_t)old == r) {
-                atomicAdd((unsigned long long*)&tab[sl], (unsigned long long)inc);
-                return true;
-            }
-            continue;   // lost the slot to another key: re-read the same group
-        }
-        g = (g + 1) & (G_P - 1);
-        ++steps;
-    }
-    return false;
-}
-
-__global__ void __launch_bounds__(NT_P, 4) kc_count_p(const uint32_t* __restrict__ binned,
-                                                   const uint64_t* __restrict__ fs, uint32_t F,
-                                                   uint32_t min_count, KP kp, uint64_t* __restrict__ out_key,
-                                                   uint32_t* __restrict__ out_cnt, uint64_t cap,
-                                                   unsigned long long* __restrict__ gstat,
-                                                   uint32_t* __restrict__ blist) {
-    __shared__ __attribute__((aligned(16))) uint64_t tab[T_P];
-    __shared__ uint32_t qbuf[NT_P / 64][QN_P];
-    __shared__ uint32_t s_ovf, s_sp, s_ranges;
-    __shared__ uint32_t stk_lo[40], stk_hi[40];
-    __shared__ uint32_t ws[NT_P / 64 + 1];
-    __shared__ unsigned long long s_base;
-    const int tid = threadIdx.x;
-    const uint32_t lane = tid & 63;
-    uint32_t* myq = qbuf[tid >> 6];
-    const uint32_t b = blockIdx.x;
-    const uint64_t* f = fs + (uint64_t)b * (F + 1);
-    for (uint32_t ff = 0; ff < F; ++ff)
-        if (f[ff + 1] - f[ff] >= 65536u && F > 1) {   // a count could pass 16 bits: kc_count takes it
-            if (tid == 0) blist[atomicAdd(&gstat[5], 1ull)] = b;
-            return;
-        }
-    const uint32_t rbits = kp.rbits;
-    const uint32_t SUBB = rbits < 16 ? rbits : 16;
-    const uint32_t full_hi = 1u << SUBB;
-    const uint32_t mc = min_count ? min_count : 1u;
-    if (tid == 0) {
-        stk_lo[0] = 0;
-        stk_hi[0] = full_hi;
-        s_sp = 1;
-        s_ranges = 0;
-    }
-    __syncthreads();
-    while (true) {
-        const uint32_t sp = s_sp;
-        if (sp == 0) break;
-        const uint32_t lo = stk_lo[sp - 1], hi = stk_hi[sp - 1];
-        __syncthreads();
-        if (tid == 0) {
-            s_sp = sp - 1;
-            s_ovf = 0;
-        }
-        for (uint32_t i = tid; i < T_P; i += NT_P) tab[i] = EMPTY_P;
-        __syncthreads();
-        const bool filt = !(lo == 0 && hi == full_hi);
-        uint32_t qn = 0;   // this wave's queued keys (uniform)
-        for (uint32_t ff = 0; ff < F; ++ff) {
-            const uint64_t a = f[ff], e = f[ff + 1];
-            const uint64_t inc = F == 1 ? (1ull << 32) : (1ull << (32 + 16 * ff));
-            constexpr uint64_t STEP = (uint64_t)NT_P * PF_P;
-            if (a == e) continue;
-            const uint64_t nfull = (e - a) / STEP;
-            uint32_t nx[PF_P];
-            auto load = [&](uint64_t i0, uint64_t bi) {
-                if (bi < nfull) {
-                    const uint32_t* __restrict__ bp = binned + i0;
-#pragma unroll
-                    for (int q = 0; q < PF_P; ++q) nx[q] = bp[q * NT_P + tid];
-                } else {
-#pragma unroll
-                    for (int q = 0; q < PF_P; ++q) {
-                        const uint64_t i = i0 + (uint64_t)q * NT_P + tid;
-                        nx[q] = i < e ? binned[i] : 0xFFFFFFFFu;
-                    }
-                }
-            };
-            // settle the queue 64 keys at a time (all lanes busy); leftovers stay queued
-            auto drain = [&](uint32_t min_take) {   // while at least min_take (>= 1) are queued
-                while (qn >= min_take && qn > 0) {
-                    const uint32_t take = qn < 64 ? qn : 64;
-                    const uint32_t q0 = qn - take;
-                    bool ok = true;
-                    if (lane < take) ok = probe_p(tab, myq[q0 + lane], inc);
-                    if (!ok) s_ovf = 1u;
-                    qn = q0;
-                    wave_lds_sync();
-                }
-            };
-            load(a, 0);
-            uint64_t bi = 0;
-            for (uint64_t i0 = a; i0 < e; i0 += STEP, ++bi) {
-                uint32_t rv[PF_P];
-#pragma unroll
-                for (int q = 0; q < PF_P; ++q) rv[q] = nx[q];
-                if (i0 + STEP < e) load(i0 + STEP, bi + 1);
-                if (filt) {
-#pragma unroll
-                    for (int q = 0; q < PF_P; ++q) {
-                        const uint32_t sk = SUBB ? rv[q] >> (rbits - SUBB) : 0u;
-                        rv[q] = (sk >= lo && sk < hi) ? rv[q] : 0xFFFFFFFFu;
-                    }
-                }
-#if HGA_EXP_LOADONLY
-                {
-                    uint32_t acc = 0;
-#pragma unroll
-                    for (int q = 0; q < PF_P; ++q) acc += rv[q];
-                    if (acc == 0x12345678u) s_ovf = 2u;
-                    continue;
-                }
-#endif
-                // 1) home groups of the whole batch read before any entry is touched
-                uint64_t eg[PF_P][GP_P];
-#pragma unroll
-                for (int q = 0; q < PF_P; ++q) read_group_p(tab, rv[q] & (G_P - 1), eg[q]);
-                uint32_t claim = 0, slot[PF_P];
-                uint32_t miss = 0;
-#pragma unroll
-                for (int q = 0; q < PF_P; ++q) {
-                    const uint32_t g = rv[q] & (G_P - 1);
-                    int w = -1, e0 = -1;
-#pragma unroll
-                    for (int t = GP_P - 1; t >= 0; --t) {
-                        w = (uint32_t)eg[q][t] == rv[q] ? t : w;
-                        e0 = eg[q][t] == EMPTY_P ? t : e0;
-                    }
-                    const bool live = rv[q] != 0xFFFFFFFFu;
-                    slot[q] = g * GP_P + (uint32_t)(w >= 0 ? w : e0);
-                    if (live && w >= 0) atomicAdd((unsigned long long*)&tab[slot[q]], (unsigned long long)inc);
-                    else if (live && e0 >= 0) claim |= 1u << q;
-                    else if (live) miss |= 1u << q;
-                }
-#if HGA_EXP_NOCLAIM
-                claim = 0; miss = 0;
-#endif
-                // 2) new keys: claim the first empty slot of the home group (count included)
-#pragma unroll
-                for (int q = 0; q < PF_P; ++q)
-                    if ((claim >> q) & 1u) {
-                        const uint64_t old = atomicCAS((unsigned long long*)&tab[slot[q]],
-                                                       (unsigned long long)EMPTY_P,
-                                                       (unsigned long long)(inc | rv[q]));
-                        if (old != EMPTY_P) {
-                            if ((uint32_t)old == rv[q]) atomicAdd((unsigned long long*)&tab[slot[q]], (unsigned long long)inc);
-                            else miss |= 1u << q;
-                        }
-                    }
-                // 3) the rest (home group full, or a lost claim) into this wave's queue
-                const uint32_t nm = (uint32_t)__popc(miss);
-                const uint64_t any = __ballot(nm != 0u);
-                if (any) {
-                    uint32_t tot;
-                    const uint32_t incl = wave_excl_scan_small<4>(nm, &tot) + nm;   // nm <= PF_P = 8
-                    if (qn + tot > QN_P) {   // no room: settle the queue first, then these in place
-                        drain(1);
-                        bool ok = true;
-                        while (__any(miss != 0u)) {
-                            if (miss) {
-                                const int q = __builtin_ctz(miss);
-                                miss &= miss - 1u;
-                                uint32_t pick = rv[0];
-#pragma unroll
-                                for (int t = 1; t < PF_P; ++t) pick = q == t ? rv[t] : pick;
-                                ok = probe_p(tab, pick, inc) && ok;
-                            }
-                        }
-                        if (!ok) s_ovf = 1u;
-                    } else {
-                        uint32_t pos = qn + incl - nm;
-                        while (miss) {
-                            const int q = __builtin_ctz(miss);
-                            miss &= miss - 1u;
-                            uint32_t pick = rv[0];
-#pragma unroll
-                            for (int t = 1; t < PF_P; ++t) pick = q == t ? rv[t] : pick;
-                            myq[pos++] = pick;
-                        }
-                        qn += tot;
-                        wave_lds_sync();
-                        drain(64);
-                    }
-                }
-                if ((i0 - a) % (4 * STEP) == 0 && __atomic_load_n(&s_ovf, __ATOMIC_RELAXED)) break;
-            }
-            drain(1);
-        }
-        __syncthreads();
-        if (s_ovf) {
-            __syncthreads();
-            if (tid == 0) {
-                if (hi - lo <= 1 || s_sp + 2 > 40) {
-                    atomicOr(&gstat[2], 1ull);
-                    s_sp = 0;
-                } else {
-                    const uint32_t mid = lo + (hi - lo) / 2;
-                    stk_lo[s_sp] = mid; stk_hi[s_sp] = hi;
-                    stk_lo[s_sp + 1] = lo; stk_hi[s_sp + 1] = mid;
-                    s_sp += 2;
-                }
-            }
-            __syncthreads();
-            continue;
-        }
-#if HGA_EXP_NOEMIT
-        if (tab[tid] == 0x1234567ull) s_ranges = 9;
-        __syncthreads();
-        continue;
-#endif
-        // emit: each thread owns ES consecutive entries; kept rows are compacted in place
-        constexpr int ES = T_P / NT_P;
-        uint64_t ent[ES];
-#pragma unroll
-        for (int j = 0; j < ES; j += 2) {
-            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(tab)[(tid * ES + j) / 2];
-            ent[j] = v.x;
-            ent[j + 1] = v.y;
-        }
-        uint32_t keep = 0;
-#pragma unroll
-        for (int j = 0; j < ES; ++j) {
-            uint64_t c = ent[j] >> 32;
-            if (F == 1) {
-                c = c >= mc ? c : 0u;
-            } else {
-                const uint32_t c0 = (uint32_t)c & 0xFFFFu, c1 = (uint32_t)(c >> 16);
-                c = (uint64_t)(c0 >= mc ? c0 : 0u) | ((uint64_t)(c1 >= mc ? c1 : 0u) << 16);
-            }
-            ent[j] = (c << 32) | (ent[j] & 0xFFFFFFFFull);
-            if (ent[j] != EMPTY_P && c) keep |= 1u << j;
-        }
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan<NT_P>((uint32_t)__popc(keep), ws, &tot);
-        if (tid == 0) {
-            s_base = tot ? atomicAdd(&gstat[0], (unsigned long long)tot) : 0ull;
-            ++s_ranges;
-        }
-        __syncthreads();   // every entry read: the table becomes the staging area
-        uint32_t o = ex;
-#pragma unroll
-        for (int j = 0; j < ES; ++j)
-            if ((keep >> j) & 1u) tab[o++] = ent[j];
-        __syncthreads();
-        const uint64_t base = s_base;
-        if (base + tot > cap) {
-            if (tid == 0 && tot) atomicOr(&gstat[2], 2ull);
-        } else {
-            const uint64_t hb = kp.fb ? ((uint64_t)b << rbits) : 0ull;
-            for (uint32_t j = tid; j < tot; j += NT_P) {
-                const uint64_t v = tab[j];
-                out_key[base + j] = mix_inv(hb | (v & 0xFFFFFFFFull), kp.mix);
-                if (F == 1) {
-                    out_cnt[base + j] = (uint32_t)(v >> 32);
-                } else {
-                    out_cnt[base + j] = (uint32_t)(v >> 32) & 0xFFFFu;
-                    out_cnt[cap + base + j] = (uint32_t)(v >> 48);
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if (tid == 0) atomicMax(&gstat[1], (unsigned long long)s_ranges);
-}
-
-// ---------------------------------------------------------------- pass C (packed, SoA)
-// Same contract as kc_count_p, with the keys and the packed counts in two u32 arrays: a probe
+// ---------------------------------------------------------------- pass C (packed counts, SoA)
+// F <= 2 files, u32 remainders, every per-file run of the bucket < 65536 instances (so no
+// count can pass 16 bits).  Keys and the packed counts (16 bits per file) in two u32 arrays: a probe
 // reads 4 keys with one ds_read_b128, a hit is one ds_add_u32 on the count word (32 banks
 // for the count array instead of the odd half of 64), a claim is ds_cmpst_b32 on the key then
 // the add.
@@ -1500,50 +1049,13 @@ __global__ void __launch_bounds__(NT_P, 4) kc_count_s(const uint32_t* __restrict
                     match_s(kg[q], rv[q], w, e0);
                     const bool live = rv[q] != 0xFFFFFFFFu;
                     slot[q] = (rv[q] & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
-#if HGA_S_BRANCHLESS
                     {   // every lane adds: a hit to its slot, anything else to its own dummy word
                         const bool hit = live && w >= 0;
                         atomicAdd(&tcnt[hit ? slot[q] : T_S + lane], inc);
                         claim |= (live && !hit && e0 >= 0) ? 1u << q : 0u;
                         miss |= (live && !hit && e0 < 0) ? 1u << q : 0u;
                     }
-#elif HGA_EXP_S_HITSTORE
-                    if (live && w >= 0) tcnt[slot[q]] = inc;
-                    else if (live && e0 >= 0) claim |= 1u << q;
-                    else if (live) miss |= 1u << q;
-#elif HGA_EXP_S_NOHIT
-                    if (live && w >= 0 && rv[q] == 0x1234567u) tcnt[slot[q]] = inc;
-                    else if (live && e0 >= 0) claim |= 1u << q;
-                    else if (live) miss |= 1u << q;
-#else
-                    if (live && w >= 0) atomicAdd(&tcnt[slot[q]], inc);
-                    else if (live && e0 >= 0) claim |= 1u << q;
-                    else if (live) miss |= 1u << q;
-#endif
                 }
-#if HGA_S_NEXT
-                // home group full without the key: the next group, inline (one displacement
-                // step covers most displaced keys, which would otherwise queue on every occurrence)
-                if (__ballot(miss != 0u)) {
-#pragma unroll
-                    for (int q = 0; q < PF_P; ++q)
-                        if ((miss >> q) & 1u) kg[q] = read_keys_s(tkey, (rv[q] + 1) & (G_S - 1));
-#pragma unroll
-                    for (int q = 0; q < PF_P; ++q)
-                        if ((miss >> q) & 1u) {
-                            int w, e0;
-                            match_s(kg[q], rv[q], w, e0);
-                            slot[q] = ((rv[q] + 1) & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
-                            if (w >= 0) {
-                                atomicAdd(&tcnt[slot[q]], inc);
-                                miss &= ~(1u << q);
-                            } else if (e0 >= 0) {
-                                claim |= 1u << q;
-                                miss &= ~(1u << q);
-                            }
-                        }
-                }
-#endif
 #pragma unroll
                 for (int q = 0; q < PF_P; ++q)
                     if ((claim >> q) & 1u) {
@@ -1959,7 +1471,9 @@ void count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n) {
 void count_run(hga_ctx* c, uint32_t min_per_file) {
     auto& s = c->count;
     HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
-    count_settle(c);   // a previous run nobody consumed still reports its errors
+    // A previous run nobody consumed is discarded, errors included: this run replaces its rows
+    // (the stream is in order, and kc_pack re-initialises the counters it would have read).
+    s.pending = false;
     const uint32_t F = s.n_files;
     s.min_per_file = min_per_file;
     uint64_t total_bytes = 0;
@@ -1972,8 +1486,8 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     kp.mix = make_mix(s.k);
     const uint32_t nbits = 2u * (uint32_t)s.k;
     // fan-out: ~16K windows per fine bucket, at most 8192 buckets, never more bits than the key
-    // packed-entry counting (kc_count_p): F <= 2 and u32 remainders; ~32K windows per bucket
-    static const bool legacy = std::getenv("HGA_COUNT_LEGACY") != nullptr;
+    // packed-count counting (kc_count_s): F <= 2 and u32 remainders; ~64K windows per bucket
+    const bool legacy = std::getenv("HGA_COUNT_LEGACY") != nullptr;   // test hook: generic kc_count for F <= 2
     const bool packed = F <= 2 && nbits - std::min<uint32_t>(MAX_FB, nbits) <= 31 && !legacy;
     const uint64_t per_bucket = packed ? 65536 : 16384;
     uint32_t fb = 0, fb_max = MAX_FB;
@@ -2019,8 +1533,8 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const uint64_t tail_words = ST_ALIGN / 16 + 8;
     std::vector<uint64_t> woff(F + 1, 0);
     for (uint32_t f = 0; f < F; ++f) woff[f + 1] = woff[f] + PAD_WORDS + (s.seq_len[f] + 15) / 16 + tail_words;
-    uint32_t* pk_all = static_cast<uint32_t*>(s.pk_all.ensure(HGA_B1_ASCII ? 64 : woff[F] * 4));
-    uint16_t* vd_all = static_cast<uint16_t*>(s.vd_all.ensure(HGA_B1_ASCII ? 64 : woff[F] * 2));
+    uint32_t* pk_all = static_cast<uint32_t*>(s.pk_all.ensure(woff[F] * 4));
+    uint16_t* vd_all = static_cast<uint16_t*>(s.vd_all.ensure(woff[F] * 2));
     std::vector<PackFile> pf(F);
     for (uint32_t f = 0; f < F; ++f) {
         pf[f] = PackFile{s.seq[f]->as<uint8_t>(), s.seq_len[f], woff[f], (s.seq_len[f] + 15) / 16};
@@ -2041,7 +1555,8 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const PackFile* d_pf = reinterpret_cast<const PackFile*>(d_tab + sizeof(BinFile) * F);
 
     const size_t esz1 = e1_32 ? 4 : 8, esz = e32 ? 4 : 8;
-    const uint64_t cap = (total_bytes / std::max<uint32_t>(1, min_per_file) + 4) & ~3ull;   // x4: 16-B row groups
+    uint64_t cap = (total_bytes / std::max<uint32_t>(1, min_per_file) + 4) & ~3ull;   // x4: 16-B row groups
+    if (const char* e = std::getenv("HGA_ROW_CAP")) cap = std::max<uint64_t>(4, std::strtoull(e, nullptr, 10) & ~3ull);   // test hook
     s.rows_key.ensure(cap * 8);
     s.rows_cnt.ensure(cap * 4 * F);
     const uint32_t slot_b = (uint32_t)esz + 4u * F;
@@ -2058,16 +1573,11 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     void* binned1 = s.binned1.ensure(pool_cap * esz1);
     Blk* table = static_cast<Blk*>(s.regions.ensure(table_cap * sizeof(Blk)));
     // P: pack all files + counter init, one launch
-    if (HGA_B1_ASCII) {
-        hipLaunchKernelGGL(kc_init_stat, dim3(1), dim3(64), 0, c->stream, gstat, n_first);
-        c->check_launch("kc_init_stat");
-    } else {
-        c->launch("kc_pack", [&] {
-            hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256 * PK_W)), dim3(256),
-                               0, c->stream, d_pf, F, woff[F], pk_all, vd_all, gstat, n_first);
-        });
-        c->check_launch("kc_pack");
-    }
+    c->launch("kc_pack", [&] {
+        hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256 * PK_W)), dim3(256),
+                           0, c->stream, d_pf, F, woff[F], pk_all, vd_all, gstat, n_first);
+    });
+    c->check_launch("kc_pack");
 
     // B1: level-1 binning of every file into pool blocks + per-workgroup fine histograms
     if (W) {
@@ -2149,7 +1659,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     if (packed && e32) {
         uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nbc * 4));
         c->launch("kc_count", [&] {
-            hipLaunchKernelGGL(HGA_COUNT_SOA ? kc_count_s : kc_count_p, dim3(nbc), dim3(NT_P), 0, c->stream,
+            hipLaunchKernelGGL(kc_count_s, dim3(nbc), dim3(NT_P), 0, c->stream,
                                static_cast<const uint32_t*>(binned), fs, F, min_per_file, kp, s.rows_key.as<uint64_t>(),
                                s.rows_cnt.as<uint32_t>(), cap, gstat, blist);
             // buckets with a per-file run >= 65536 (listed in blist, count in gstat[5])
@@ -2208,7 +1718,7 @@ void count_settle(hga_ctx* c, const unsigned long long* h) {
 // (JellyfishOccurrenceReader.cpp:19-24 skips jellyfish for it and reads the dump verbatim).
 void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts, uint64_t n) {
     auto& s = c->count;
-    count_settle(c);
+    s.pending = false;   // an unconsumed run is discarded: its rows are out of date from here on
     HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
     HGA_REQUIRE(file < s.n_files, HGA_ERR_INVALID, "file index out of range");
     HGA_REQUIRE(n == 0 || (keys && counts), HGA_ERR_INVALID, "null rows pointer");

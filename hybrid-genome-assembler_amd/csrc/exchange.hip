@@ -514,6 +514,7 @@ __global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict_
     static_assert(T % MG_NT == 0 && T / MG_NT <= 32, "each thread owns T / MG_NT <= 32 slots");
     __shared__ unsigned long long tkey[T];
     __shared__ uint32_t tcnt[FMAX * T];
+    __shared__ uint32_t tsat[(FMAX * T + 31) / 32];   // bit f * T + slot: that sum passed 2^32 - 1
     __shared__ uint32_t ws[MG_NT / 64 + 1];
     __shared__ uint32_t s_ovf;
     const int tid = threadIdx.x;
@@ -528,6 +529,7 @@ __global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict_
     for (uint32_t p = 0; p < P; ++p) {
         for (uint32_t j = tid; j < T; j += MG_NT) tkey[j] = MG_EMPTY;
         for (uint32_t j = tid; j < F * T; j += MG_NT) tcnt[j] = 0;
+        for (uint32_t j = tid; j < (FMAX * T + 31) / 32; j += MG_NT) tsat[j] = 0;
         __syncthreads();
         for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)MG_NT * MG_R) {
             uint64_t v[MG_R];
@@ -554,7 +556,10 @@ __global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict_
                 }
                 for (uint32_t f = 0; f < F; ++f) {
                     const uint32_t c = (uint32_t)((v[q] >> (pf.kb + (int)f * pf.cb)) & pf.cmax);
-                    if (c) atomicAdd(&tcnt[f * T + slot], c);
+                    if (c) {   // counts saturate at 2^32 - 1 like count_merge's (a wrapping add is flagged)
+                        const uint32_t old = atomicAdd(&tcnt[f * T + slot], c);
+                        if (old + c < old) atomicOr(&tsat[(f * T + slot) >> 5], 1u << ((f * T + slot) & 31));
+                    }
                 }
             }
         }
@@ -574,6 +579,7 @@ __global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict_
             bool any = false;
             for (uint32_t f = 0; f < F; ++f) {
                 uint32_t c = tcnt[f * T + s];
+                if ((tsat[(f * T + s) >> 5] >> ((f * T + s) & 31)) & 1u) c = 0xFFFFFFFFu;
                 c = c >= min_c ? c : 0u;
                 tcnt[f * T + s] = c;
                 any |= c != 0u;

@@ -24,12 +24,6 @@ constexpr int RS_T = 256;              // threads per tile
 constexpr int RS_I = HGA_RS_I;         // items per thread
 constexpr int RS_TILE = RS_T * RS_I;   // 4096 keys per tile
 constexpr int SC_T = 1024, SC_I = 4, SC_TILE = SC_T * SC_I;
-#ifndef HGA_EXP_RS_NOLB
-#define HGA_EXP_RS_NOLB 0
-#endif
-#ifndef HGA_EXP_RS_NORANK
-#define HGA_EXP_RS_NORANK 0
-#endif
 #ifndef HGA_LBW
 #define HGA_LBW 8   // predecessor tiles read per look-back step (independent loads per digit thread)
 #endif
@@ -201,11 +195,6 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
     }
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
-#if HGA_EXP_RS_NORANK
-        rank[j] = j * 64 + lane;
-        if (lane == 0) wcnt[wave][dig[j] & 255] += 64;
-        continue;
-#endif
         const uint32_t d = dig[j];
         const bool ok = d < 256u;
         uint64_t m = __ballot(ok);
@@ -234,7 +223,7 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
         wcnt[3][d] = ex + c0 + c1 + c2;
         uint32_t* st = status + (uint64_t)tile * 256 + d;
         uint32_t excl = 0;
-        if (tile == 0 || HGA_EXP_RS_NOLB) {
+        if (tile == 0) {
             __hip_atomic_store(st, LB_P | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             __hip_atomic_store(st, LB_A | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -475,13 +464,10 @@ size_t scan_scratch_bytes(uint64_t n) {
     return b + 256;
 }
 
-// n below which the onesweep path is used (env HGA_ONESWEEP_MAX overrides; 0 disables).
+// n below which the onesweep path is used (env HGA_ONESWEEP_MAX overrides per call; 0 disables).
 inline uint64_t hga_onesweep_max() {
-    static const uint64_t v = [] {
-        const char* e = std::getenv("HGA_ONESWEEP_MAX");
-        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)(4ull << 20);
-    }();
-    return v;
+    const char* e = std::getenv("HGA_ONESWEEP_MAX");
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)(4ull << 20);
 }
 
 // src_k / src_v (optional): read the first pass from these instead of keys / vals (saves the copy

@@ -79,7 +79,8 @@ hga_status hga_count_add_rows(hga_ctx* ctx, uint32_t file, const uint64_t* keys,
  * queued and the call returns; the run's own failures (level-1 pool, unsplittable bucket,
  * row capacity) are reported by the next count call that consumes its rows
  * (hga_count_spec_hist, _select*, _rows, _dump, _get_stats, the exchange calls), which
- * then fails with that status. */
+ * then fails with that status.  A run nobody consumed is discarded, errors included, by the
+ * next hga_count_run or hga_count_add_rows (whose rows replace it). */
 hga_status hga_count_run(hga_ctx* ctx, uint32_t min_per_file);
 
 typedef struct hga_count_stats {

@@ -229,6 +229,154 @@ int64_t or_count_stream_mt(const char* s, uint64_t n, int k, uint32_t min_count,
     return (int64_t)ks.size();
 }
 
+// --- A3 + A4, multi-threaded over all files: merged rows of the whole count stage ----------
+// The same result as or_count_stream per file followed by or_merge, computed by range
+// partitioning (so no heap merge is needed): threads extract every canonical k-mer of their
+// slice of a file (cut at separator bytes) into P code-range partitions; then, one partition at
+// a time (threads take partitions from a shared counter), each file's codes are sorted and
+// run-length counted (count < min_count dropped: `--bc`, run_jellyfish.sh:3-6) and the F sorted
+// per-file lists are merged into rows (counts[f] = 0 where file f lacks the k-mer,
+// JellyfishOccurrenceReader.cpp:63-86).  Partitions are ascending code ranges, so their rows
+// concatenate in ascending order.  Output: keys[rows], counts[rows * F] row-major.
+int64_t or_count_files_mt(int F, const char* const* s, const uint64_t* n, int k, uint32_t min_count,
+                          int threads, uint64_t** keys, uint32_t** counts) {
+    if (k > 32 || k < 1 || F < 1) return -1;
+    if (threads < 1) threads = 1;
+    const int nb = 2 * k;
+    const int tb = nb < 16 ? nb : 16;              // top bits that pick the partition
+    const int P = nb <= 8 ? 1 : 512;
+    // canonical = min(fwd, rc) of uniform codes has mass 1 - (1 - x)^2 below x: equal-mass
+    // ranges, aligned to the top tb bits (any ascending ranges give the same rows)
+    std::vector<uint16_t> part_of(1u << tb);
+    for (uint32_t t = 0; t < (1u << tb); ++t) {
+        const double x = (double)t / (double)(1u << tb);
+        const int p = (int)((1.0 - (1.0 - x) * (1.0 - x)) * P);
+        part_of[t] = (uint16_t)std::min(p, P - 1);
+    }
+    const int shift = nb - tb;
+    // bins[f][t][p]
+    std::vector<std::vector<std::vector<std::vector<uint64_t>>>> bins(
+        F, std::vector<std::vector<std::vector<uint64_t>>>(threads, std::vector<std::vector<uint64_t>>(P)));
+    for (int f = 0; f < F; ++f) {
+        std::vector<uint64_t> cut(threads + 1, 0);
+        cut[threads] = n[f];
+        for (int t = 1; t < threads; ++t) {
+            uint64_t c = n[f] * (uint64_t)t / threads;
+            if (c < cut[t - 1]) c = cut[t - 1];
+            while (c < n[f] && jf_code((unsigned char)s[f][c]) >= 0) ++c;
+            cut[t] = c;
+        }
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, f, t] {
+                auto& B = bins[f][t];
+                for_each_jf_kmer(s[f] + cut[t], cut[t + 1] - cut[t], k,
+                                 [&](uint64_t c, uint64_t) { B[part_of[c >> shift]].push_back(c); });
+            });
+        for (auto& x : th) x.join();
+    }
+    std::vector<std::vector<uint64_t>> pk(P);
+    std::vector<std::vector<uint32_t>> pc(P);
+    std::atomic<int> next{0};
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&] {
+                std::vector<uint64_t> v;
+                std::vector<std::vector<std::pair<uint64_t, uint32_t>>> runs(F);
+                for (int p; (p = next.fetch_add(1)) < P;) {
+                    for (int f = 0; f < F; ++f) {
+                        v.clear();
+                        for (int t2 = 0; t2 < threads; ++t2) {
+                            auto& b = bins[f][t2][p];
+                            v.insert(v.end(), b.begin(), b.end());
+                            std::vector<uint64_t>().swap(b);
+                        }
+                        std::sort(v.begin(), v.end());
+                        auto& r = runs[f];
+                        r.clear();
+                        for (size_t i = 0; i < v.size();) {
+                            size_t j = i + 1;
+                            while (j < v.size() && v[j] == v[i]) ++j;
+                            if (j - i >= min_count) r.push_back({v[i], (uint32_t)(j - i)});
+                            i = j;
+                        }
+                    }
+                    std::vector<size_t> idx(F, 0);
+                    auto& K = pk[p];
+                    auto& C = pc[p];
+                    while (true) {
+                        uint64_t m = ~0ull;
+                        bool any = false;
+                        for (int f = 0; f < F; ++f)
+                            if (idx[f] < runs[f].size()) {
+                                m = std::min(m, runs[f][idx[f]].first);
+                                any = true;
+                            }
+                        if (!any) break;
+                        K.push_back(m);
+                        for (int f = 0; f < F; ++f) {
+                            uint32_t c = 0;
+                            if (idx[f] < runs[f].size() && runs[f][idx[f]].first == m) c = runs[f][idx[f]++].second;
+                            C.push_back(c);
+                        }
+                    }
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    size_t total = 0;
+    for (auto& x : pk) total += x.size();
+    uint64_t* ok = (uint64_t*)std::malloc(std::max<size_t>(1, total * 8));
+    uint32_t* oc = (uint32_t*)std::malloc(std::max<size_t>(1, total * 4 * F));
+    size_t o = 0;
+    for (int p = 0; p < P; ++p) {
+        if (!pk[p].empty()) {
+            std::memcpy(ok + o, pk[p].data(), pk[p].size() * 8);
+            std::memcpy(oc + o * F, pc[p].data(), pc[p].size() * 4);
+        }
+        o += pk[p].size();
+    }
+    *keys = ok;
+    *counts = oc;
+    return (int64_t)total;
+}
+
+// Reference-like single-thread count (cpu_baseline "reference_like" figure):
+// per read (the stream split at '\n'), the reference's KmerIterator inner loop with its
+// std::unordered_map<char, Kmer> BASE_TO_NUM / COMPLEMENT lookups (KmerIterator.cpp:7-19, 54-63;
+// operator[] as in the reference), counted into a std::unordered_map, then the per-file drop and
+// the sort of the dump.  For ACGT-only reads (the synthetic ones) the rows equal
+// or_count_stream's; returns the number of rows.
+int64_t or_count_reference_like(const char* s, uint64_t n, int k, uint32_t min_count) {
+    if (k > 32 || k < 1) return -1;
+    static std::unordered_map<char, uint64_t> base_to_num = {{'A', 0}, {'C', 1}, {'G', 2}, {'T', 3}};
+    static std::unordered_map<char, uint64_t> complement = {{'A', 3}, {'C', 2}, {'G', 1}, {'T', 0}};
+    const uint64_t mask = kmask(k);
+    const int sh = 2 * (k - 1);
+    std::unordered_map<uint64_t, uint32_t> m;
+    uint64_t i = 0;
+    while (i < n) {
+        uint64_t j = i;
+        while (j < n && s[j] != '\n') ++j;
+        const std::string read(s + i, s + j);   // GenomeReadData::sequence
+        if (read.size() >= (uint64_t)k) {
+            uint64_t fwd = 0, rc = 0;
+            for (size_t p = 0; p < read.size(); ++p) {
+                fwd = ((fwd << 2) | base_to_num[read[p]]) & mask;
+                rc = (rc >> 2) | (complement[read[p]] << sh);
+                if (p + 1 >= (size_t)k) ++m[fwd < rc ? fwd : rc];
+            }
+        }
+        i = j + 1;
+    }
+    std::vector<std::pair<uint64_t, uint32_t>> v;
+    for (auto& kv : m)
+        if (kv.second >= min_count) v.push_back(kv);
+    std::sort(v.begin(), v.end());
+    return (int64_t)v.size();
+}
+
 // --- A4: k-way merge of the per-file sorted dumps -------------------------------------
 // JellyfishOccurrenceReader::get_next_kmer (JellyfishOccurrenceReader.cpp:63-86): one
 // merged row per distinct k-mer, counts[f] = 0 where file f's dump lacks it.
@@ -412,6 +560,121 @@ int64_t or_construct_indices(const char* bases, const uint64_t* offsets, uint64_
     *hit_pos = dup_vec(hpos);
     *sorted_kid = dup_vec(sk);
     *first_ptr = dup_vec(fp);
+    *first_kid = dup_vec(fk);
+    *first_pos = dup_vec(fpos);
+    *kci_ptr = dup_vec(kp);
+    *kci_read = dup_vec(kr);
+    *n_first = fk.size();
+    return (int64_t)hk.size();
+}
+
+// Multi-threaded construct_indices with exactly or_construct_indices' outputs: threads take
+// contiguous read ranges (so per-thread hit lists concatenate in read order), each with the
+// same per-read steps; kmer_component_index lists are concatenated in thread order and sorted
+// per KmerID (:282-284).  For the C3-size parity test and the lookup cpu_baseline leg.
+int64_t or_construct_indices_mt(const char* bases, const uint64_t* offsets, uint64_t n,
+                                const uint32_t* read_ids, int k, const uint64_t* sdk_keys,
+                                uint32_t n_sdk, int threads, uint64_t** hit_ptr, uint32_t** hit_kid,
+                                uint32_t** hit_pos, uint32_t** sorted_kid, uint64_t** first_ptr,
+                                uint32_t** first_kid, uint32_t** first_pos, uint64_t** kci_ptr,
+                                uint32_t** kci_read, uint64_t* n_first) {
+    if (k > 32 || k < 1) return -1;
+    if (threads < 1) threads = 1;
+    std::unordered_map<uint64_t, uint32_t> kmer_index;  // KmerIndex, :237-241
+    kmer_index.reserve(n_sdk * 2);
+    for (uint32_t i = 0; i < n_sdk; ++i) kmer_index[sdk_keys[i]] = i;
+    struct Part {
+        std::vector<uint32_t> hk, hpos, sk, fk, fpos;
+        std::vector<uint64_t> hcnt, fcnt;   // per read of the range
+        std::vector<std::pair<uint32_t, uint32_t>> kci;   // (KmerID, ReadID) in hit order
+    };
+    std::vector<Part> parts(threads);
+    std::vector<uint64_t> r0(threads + 1);
+    for (int t = 0; t <= threads; ++t) r0[t] = n * (uint64_t)t / threads;
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                Part& P = parts[t];
+                std::vector<uint64_t> wk;
+                std::vector<uint32_t> wp, ids;
+                std::vector<std::pair<uint32_t, uint32_t>> fp;
+                for (uint64_t r = r0[t]; r < r0[t + 1]; ++r) {
+                    const uint64_t len = offsets[r + 1] - offsets[r];
+                    wk.resize(len + 1);
+                    wp.resize(len + 1);
+                    const int64_t w = or_kmer_windows(bases + offsets[r], len, k, wk.data(), wp.data());
+                    ids.clear();
+                    fp.clear();
+                    for (int64_t i = 0; i < w; ++i) {
+                        auto it = kmer_index.find(wk[i]);
+                        if (it == kmer_index.end()) continue;
+                        P.hk.push_back(it->second);
+                        P.hpos.push_back(wp[i]);
+                        ids.push_back(it->second);
+                        P.kci.push_back({it->second, read_ids[r]});
+                        fp.push_back({it->second, wp[i]});
+                    }
+                    std::sort(ids.begin(), ids.end());
+                    P.sk.insert(P.sk.end(), ids.begin(), ids.end());
+                    // first occurrence per KmerID (positions ascend in window order: stable sort)
+                    std::stable_sort(fp.begin(), fp.end(),
+                                     [](const auto& a, const auto& b) { return a.first < b.first; });
+                    uint64_t nf = 0;
+                    for (size_t i = 0; i < fp.size(); ++i)
+                        if (i == 0 || fp[i].first != fp[i - 1].first) {
+                            P.fk.push_back(fp[i].first);
+                            P.fpos.push_back(fp[i].second);
+                            ++nf;
+                        }
+                    P.hcnt.push_back(ids.size());
+                    P.fcnt.push_back(nf);
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    std::vector<uint64_t> hp(n + 1, 0), fpp(n + 1, 0);
+    std::vector<uint32_t> hk, hpos, sk, fk, fpos;
+    for (int t = 0; t < threads; ++t) {
+        const Part& P = parts[t];
+        for (uint64_t i = 0; i < P.hcnt.size(); ++i) {
+            const uint64_t r = r0[t] + i;
+            hp[r + 1] = hp[r] + P.hcnt[i];
+            fpp[r + 1] = fpp[r] + P.fcnt[i];
+        }
+        hk.insert(hk.end(), P.hk.begin(), P.hk.end());
+        hpos.insert(hpos.end(), P.hpos.begin(), P.hpos.end());
+        sk.insert(sk.end(), P.sk.begin(), P.sk.end());
+        fk.insert(fk.end(), P.fk.begin(), P.fk.end());
+        fpos.insert(fpos.end(), P.fpos.begin(), P.fpos.end());
+    }
+    // kmer_component_index: counting sort by KmerID, then each list sorted
+    std::vector<uint64_t> kp(n_sdk + 1, 0);
+    for (auto& P : parts)
+        for (auto& e : P.kci) ++kp[e.first + 1];
+    for (uint32_t i = 0; i < n_sdk; ++i) kp[i + 1] += kp[i];
+    std::vector<uint32_t> kr(kp[n_sdk]);
+    {
+        std::vector<uint64_t> cur(kp.begin(), kp.end() - 1);
+        for (auto& P : parts)
+            for (auto& e : P.kci) kr[cur[e.first]++] = e.second;
+    }
+    {
+        std::atomic<uint32_t> next{0};
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&] {
+                for (uint32_t b; (b = next.fetch_add(4096)) < n_sdk;)
+                    for (uint32_t i = b; i < std::min<uint32_t>(n_sdk, b + 4096); ++i)
+                        std::sort(kr.begin() + kp[i], kr.begin() + kp[i + 1]);
+            });
+        for (auto& x : th) x.join();
+    }
+    *hit_ptr = dup_vec(hp);
+    *hit_kid = dup_vec(hk);
+    *hit_pos = dup_vec(hpos);
+    *sorted_kid = dup_vec(sk);
+    *first_ptr = dup_vec(fpp);
     *first_kid = dup_vec(fk);
     *first_pos = dup_vec(fpos);
     *kci_ptr = dup_vec(kp);

@@ -42,6 +42,16 @@ def lib():
         L.or_count_stream_mt.restype = C.c_int64
         L.or_count_stream_mt.argtypes = [C.c_char_p, C.c_uint64, C.c_int, C.c_uint32, C.c_int,
                                          C.POINTER(_u64p), C.POINTER(_u32p)]
+        L.or_count_files_mt.restype = C.c_int64
+        L.or_count_files_mt.argtypes = [C.c_int, C.POINTER(C.c_char_p), _u64p, C.c_int, C.c_uint32, C.c_int,
+                                        C.POINTER(_u64p), C.POINTER(_u32p)]
+        L.or_count_reference_like.restype = C.c_int64
+        L.or_count_reference_like.argtypes = [C.c_char_p, C.c_uint64, C.c_int, C.c_uint32]
+        L.or_construct_indices_mt.restype = C.c_int64
+        L.or_construct_indices_mt.argtypes = [C.c_char_p, _u64p, C.c_uint64, _u32p, C.c_int, _u64p, C.c_uint32,
+                                              C.c_int] + \
+            [C.POINTER(_u64p), C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u64p),
+             C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u64p), C.POINTER(_u32p), _u64p]
         L.or_count_instances.restype = C.c_uint64
         L.or_count_instances.argtypes = [C.c_char_p, C.c_uint64, C.c_int]
         L.or_merge.restype = C.c_int64
@@ -112,6 +122,29 @@ def count_stream(seq: bytes, k: int, min_count: int = 2, threads: int = 0):
     return _take(kp, n, np.uint64), _take(cp, n, np.uint32)
 
 
+def count_files_mt(streams, k: int, min_count: int = 2, threads: int = 8):
+    """Merged rows of the whole count stage (per-file exact counts, drop, merge), multi-threaded:
+    (keys ascending, counts[rows, F])."""
+    F = len(streams)
+    arr = (C.c_char_p * F)(*streams)
+    lens = np.array([len(x) for x in streams], np.uint64)
+    kp, cp = _u64p(), _u32p()
+    n = lib().or_count_files_mt(F, arr, _p(lens, C.c_uint64), k, min_count, threads, C.byref(kp), C.byref(cp))
+    if n < 0:
+        raise ValueError("k out of range")
+    return _take(kp, n, np.uint64), _take(cp, n * F, np.uint32).reshape(-1, F)
+
+
+def count_reference_like(seq: bytes, k: int, min_count: int = 2) -> int:
+    """Single-thread count with the reference's map-based KmerIterator loop; returns rows (timing leg)."""
+    return int(lib().or_count_reference_like(seq, len(seq), k, min_count))
+
+
+def dumps_of(keys, counts):
+    """Per-file dumps (rows with a nonzero count in that file) of merged rows."""
+    return [(keys[counts[:, f] > 0], counts[counts[:, f] > 0, f]) for f in range(counts.shape[1])]
+
+
 def count_instances(seq: bytes, k: int) -> int:
     return int(lib().or_count_instances(seq, len(seq), k))
 
@@ -160,15 +193,20 @@ def load_sdk_text(text: bytes):
     return _take(p, n, np.uint64), k.value
 
 
-def construct_indices(bases: bytes, offsets, k: int, sdk_keys, first_read_id: int = 1):
+def construct_indices(bases: bytes, offsets, k: int, sdk_keys, first_read_id: int = 1, threads: int = 0):
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = len(offsets) - 1
     ids = np.arange(first_read_id, first_read_id + n, dtype=np.uint32)
     sdk = np.ascontiguousarray(sdk_keys, np.uint64)
     ptrs = [_u64p(), _u32p(), _u32p(), _u32p(), _u64p(), _u32p(), _u32p(), _u64p(), _u32p()]
     nf = C.c_uint64()
-    H = lib().or_construct_indices(bases, _p(offsets, C.c_uint64), n, _p(ids, C.c_uint32), k,
-                                   _p(sdk, C.c_uint64), len(sdk), *[C.byref(x) for x in ptrs], C.byref(nf))
+    if threads:
+        H = lib().or_construct_indices_mt(bases, _p(offsets, C.c_uint64), n, _p(ids, C.c_uint32), k,
+                                          _p(sdk, C.c_uint64), len(sdk), threads, *[C.byref(x) for x in ptrs],
+                                          C.byref(nf))
+    else:
+        H = lib().or_construct_indices(bases, _p(offsets, C.c_uint64), n, _p(ids, C.c_uint32), k,
+                                       _p(sdk, C.c_uint64), len(sdk), *[C.byref(x) for x in ptrs], C.byref(nf))
     if H < 0:
         raise ValueError("k out of range")
     U = nf.value

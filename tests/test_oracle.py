@@ -124,3 +124,50 @@ def test_oracle_connections_vs_python(min_kmers, min_score, use_piv):
     exp = py_connections(idx, piv, min_kmers, min_score, cat, 5)
     assert len(exp) > 10
     assert list(zip(x.tolist(), y.tolist(), s.tolist(), g.tolist())) == exp
+
+
+@pytest.mark.parametrize("k,F,min_count", [(1, 2, 1), (4, 1, 2), (11, 3, 2), (19, 2, 2), (19, 2, 1), (27, 2, 3),
+                                           (32, 2, 2)])
+def test_count_files_mt_matches_plain(k, F, min_count):
+    """The partitioned multi-threaded count stage equals per-file count_stream + merge."""
+    rng = random.Random(1000 + k * 10 + F)
+    streams = []
+    for f in range(F):
+        reads = [rand_seq(rng, rng.randint(0, 160), "ACGTACGTACGTACGTNa") for _ in range(1500)]
+        streams.append("\n".join(reads + reads[: 400 + 100 * f]).encode())
+    dumps = [oracle.count_stream(s, k, min_count) for s in streams]
+    keys, counts = oracle.merge(dumps)
+    for t in (1, 5):
+        k2, c2 = oracle.count_files_mt(streams, k, min_count, threads=t)
+        assert np.array_equal(keys, k2) and np.array_equal(counts, c2)
+    for (dk, dc), (ek, ec) in zip(oracle.dumps_of(keys, counts), dumps):
+        assert np.array_equal(dk, ek) and np.array_equal(dc, ec)
+
+
+def test_count_reference_like_rows():
+    rng = random.Random(5)
+    reads = [rand_seq(rng, 150) for _ in range(2000)]
+    stream = "\n".join(reads + reads[:700]).encode()
+    assert oracle.count_reference_like(stream, 19, 2) == len(oracle.count_stream(stream, 19, 2)[0])
+
+
+@pytest.mark.parametrize("threads", [1, 2, 7])
+def test_construct_indices_mt_matches_plain(threads):
+    rng = np.random.default_rng(21)
+    gnm = bytes(rng.choice(list(b"ACGT"), 6000).tolist())
+    reads = []
+    for i in range(400):
+        s = int(rng.integers(0, 5800))
+        r = bytearray(gnm[s:s + int(rng.integers(0, 400))])
+        if i % 7 == 0 and len(r) > 10:
+            r[5] = ord("N")
+        reads.append(bytes(r))
+    bases = b"".join(reads)
+    offs = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    c, _ = oracle.kmer_windows(gnm, 15)
+    sdk = np.concatenate([np.unique(c)[::3], np.array([0, 7], np.uint64)])
+    a = oracle.construct_indices(bases, offs, 15, sdk, 3)
+    b = oracle.construct_indices(bases, offs, 15, sdk, 3, threads=threads)
+    assert int(a["hit_ptr"][-1]) > 1000
+    for name in a:
+        assert np.array_equal(a[name], b[name]), name
