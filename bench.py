@@ -11,7 +11,8 @@ selection at [10,25] (hga_count_select_device) — everything jf_occurrences doe
 Inputs are resident in HBM before the timed region.  N > 1 (torchrun, one rank per GPU, RCCL):
 every rank holds its own C2-sized shard of reads (weak scaling) and a step is the distributed
 count of DESIGN.md §6 — local count, owner partition, all-to-all of the rows over xGMI, owner
-merge + `--bc` drop, histogram reduction, per-owner export selection (hga_dist.OwnerExchange);
+merge + `--bc` drop, histogram reduction, per-owner export selection (hga_count_exchange in the
+C ABI over the library's RCCL communicator, set up by hga_dist.OwnerExchange);
 barrier + max-over-ranks timing.  Rank 0 prints one JSON line.
 """
 import argparse
@@ -446,15 +447,18 @@ def main():
     ex = None
     if D.world > 1:
         import hga_dist
-        ex = hga_dist.OwnerExchange(hga_dist.HgaEngine(ctx, K, 2, f"cuda:{dev}"))
+        ex = hga_dist.OwnerExchange(ctx)   # the library's RCCL communicator (hga_comm_init)
     step = (lambda: dist_count_step(ex)) if ex else (lambda: count_step(ctx))
     for _ in range(args.warmup):
         step()
+    if ex:   # this rank's own count (what its counting kernels process in a step: min 1, no exchange)
+        ctx.count_run(1)
     st = ctx.count_stats()
     stats = {"bytes": st.bytes, "instances": st.instances, "rows": st.distinct_rows, "files": 2}
     # 1) untimed profiled pass: per-kernel breakdown (events around every launch)
     names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
-             "kx_partition", "kx_merge", "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
+             "kx_partition", "kx_piece_hist", "kx_pack_scatter", "kx_merge", "kx_mb_hist", "kx_mb_scatter",
+             "kx_mb_merge", "kx_mb_compact", "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
     ctx.profile(True)
     ctx.profile_reset()
     for _ in range(args.steps):
@@ -504,9 +508,9 @@ def main():
                    "k": K, "reads": ra.n + rb.n, "bases": st.bytes, "instances_per_gpu": st.instances,
                    "distinct_rows": st.distinct_rows, "selected": n_sel, "discriminative": n_disc,
                    "buckets": st.buckets, "max_split": st.max_split, "parallelism": f"dp{D.world}",
-                   "exchange": (f"owner all-to-all over {os.environ.get('HGA_BENCH_BACKEND', 'nccl (RCCL)')} of "
-                                f"{'packed u64 row pieces' if ctx.count_pack_bits() else '(key, counts[F]) rows'}: "
-                                f"{ex.local_rows} local rows -> {ex.received_rows} owned pieces on rank 0")
+                   "exchange": (f"hga_count_exchange: owner all-to-all-v over "
+                                f"{'RCCL (hga_comm_init)' if os.environ.get('HGA_BENCH_BACKEND', 'nccl') == 'nccl' else 'the host transport hook (gloo)'} "
+                                f"of {'packed u64 row pieces' if ctx.count_pack_bits() else '(key, counts[F]) rows'}")
                    if ex else None},
         "roofline": roofline,
         "pipeline_roofline": {"model": "16.25 B per k-mer instance (SURVEY.md §8(d))",
@@ -521,7 +525,7 @@ def main():
         ctx2 = hga.Ctx(dev)
         if ex:
             ex.count(2)
-            sdk = ex.select_all(LOWER, UPPER)
+            sdk, _ = ex.select(LOWER, UPPER)   # the whole export on every rank
         else:
             ctx.count_run(2)
             sdk, _, _ = ctx.select(LOWER, UPPER)

@@ -145,6 +145,15 @@ hga_status hga_count_get_stats(hga_ctx* c, hga_count_stats* out) {
         uint64_t b = 0;
         for (auto l : s.seq_len) b += l;
         out->bytes = b;
+        if (s.dist) {   // after hga_count_exchange: the whole input over all ranks
+            uint64_t r = s.rows;
+            std::vector<uint64_t> g(c->comm->nranks);
+            hga::comm_allgather(c, &r, 8, g.data());
+            out->distinct_rows = 0;
+            for (auto v : g) out->distinct_rows += v;
+            out->instances = s.g_instances;
+            out->bytes = s.g_bytes;
+        }
         out->buckets = s.buckets;
         out->max_split = s.max_split;
     });
@@ -155,7 +164,8 @@ hga_status hga_count_spec_hist(hga_ctx* c, const double* thr, uint32_t n_thr, in
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(thr && triples && n, HGA_ERR_INVALID, "null pointer");
         std::vector<int64_t> v;
-        hga::count_spec_hist(c, thr, n_thr, v);
+        if (c->count.dist) hga::count_spec_hist_global(c, thr, n_thr, v);
+        else hga::count_spec_hist(c, thr, n_thr, v);
         *triples = host_dup(v.data(), v.size());
         *n = v.size() / 3;
     });
@@ -166,6 +176,16 @@ hga_status hga_count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t**
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(keys && n && n_discriminative, HGA_ERR_INVALID, "null pointer");
         uint64_t m = 0, d = 0;
+        if (c->count.dist) {
+            hga::count_select_global(c, lower, upper, &m, &d);
+            std::vector<uint64_t> k;
+            std::vector<uint8_t> f;
+            hga::count_fetch_selected_global(c, k, f);
+            *keys = host_dup(k.data(), k.size());
+            *n = m;
+            *n_discriminative = d;
+            return;
+        }
         hga::count_select(c, lower, upper, &m, &d);
         uint64_t* out = static_cast<uint64_t*>(std::malloc(m ? m * 8 : 8));
         if (!out) throw std::bad_alloc();
@@ -181,6 +201,17 @@ hga_status hga_count_select_ex(hga_ctx* c, int64_t lower, int64_t upper, uint64_
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(keys && disc && n && n_discriminative, HGA_ERR_INVALID, "null pointer");
         uint64_t m = 0, d = 0;
+        if (c->count.dist) {
+            hga::count_select_global(c, lower, upper, &m, &d);
+            std::vector<uint64_t> k;
+            std::vector<uint8_t> f;
+            hga::count_fetch_selected_global(c, k, f);
+            *keys = host_dup(k.data(), k.size());
+            *disc = host_dup(f.data(), f.size());
+            *n = m;
+            *n_discriminative = d;
+            return;
+        }
         hga::count_select(c, lower, upper, &m, &d);
         uint64_t* out = static_cast<uint64_t*>(std::malloc(m ? m * 8 : 8));
         uint8_t* fl = static_cast<uint8_t*>(std::malloc(m ? m : 1));
@@ -197,7 +228,8 @@ hga_status hga_count_select_device(hga_ctx* c, int64_t lower, int64_t upper, uin
                                    uint64_t* n_discriminative) {
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(n && n_discriminative, HGA_ERR_INVALID, "null pointer");
-        hga::count_select(c, lower, upper, n, n_discriminative);
+        if (c->count.dist) hga::count_select_global(c, lower, upper, n, n_discriminative);
+        else hga::count_select(c, lower, upper, n, n_discriminative);
     });
 }
 
@@ -240,7 +272,8 @@ hga_status hga_count_rows(hga_ctx* c, uint64_t** keys, uint32_t** counts, uint64
         HGA_REQUIRE(keys && counts && rows, HGA_ERR_INVALID, "null pointer");
         std::vector<uint64_t> k;
         std::vector<uint32_t> v;
-        hga::count_rows(c, -1, k, v);
+        if (c->count.dist) hga::count_rows_global(c, -1, k, v);
+        else hga::count_rows(c, -1, k, v);
         *keys = host_dup(k.data(), k.size());
         *counts = host_dup(v.data(), v.size());
         *rows = k.size();
@@ -253,7 +286,8 @@ hga_status hga_count_dump(hga_ctx* c, uint32_t file, uint64_t** keys, uint32_t**
         HGA_REQUIRE(file < c->count.n_files, HGA_ERR_INVALID, "file index out of range");
         std::vector<uint64_t> k;
         std::vector<uint32_t> v;
-        hga::count_rows(c, (int)file, k, v);
+        if (c->count.dist) hga::count_rows_global(c, (int)file, k, v);
+        else hga::count_rows(c, (int)file, k, v);
         *keys = host_dup(k.data(), k.size());
         *counts = host_dup(v.data(), v.size());
         *rows = k.size();
@@ -341,5 +375,42 @@ hga_status hga_profile_get(hga_ctx* c, const char* name, double* ms, uint64_t* l
 }
 
 hga_status hga_sync(hga_ctx* c) { HGA_CTX_GUARD(c, c->sync()); }
+
+hga_status hga_comm_init(hga_ctx* c, const void* unique_id, int rank, int nranks) {
+    HGA_CTX_GUARD(c, hga::comm_init_rccl(c, unique_id, rank, nranks));
+}
+
+hga_status hga_comm_init_host(hga_ctx* c, int rank, int nranks, const hga_transport* t) {
+    HGA_CTX_GUARD(c, hga::comm_init_host(c, rank, nranks, t));
+}
+
+hga_status hga_comm_info(hga_ctx* c, int* rank, int* nranks) {
+    HGA_CTX_GUARD(c, {
+        HGA_REQUIRE(rank && nranks, HGA_ERR_INVALID, "null pointer");
+        *rank = c->comm ? c->comm->rank : 0;
+        *nranks = c->comm ? c->comm->nranks : 1;
+    });
+}
+
+hga_status hga_comm_destroy(hga_ctx* c) {
+    HGA_CTX_GUARD(c, {
+        c->sync();
+        c->comm.reset();
+        c->count.dist = false;
+    });
+}
+
+hga_status hga_count_exchange(hga_ctx* c, uint32_t min_per_file) {
+    HGA_CTX_GUARD(c, hga::count_exchange(c, min_per_file));
+}
+
+hga_status hga_lookup_gather(hga_ctx* c) { HGA_CTX_GUARD(c, hga::lookup_gather(c)); }
+
+hga_status hga_connections_gather(hga_ctx* c, uint64_t* n) {
+    HGA_CTX_GUARD(c, {
+        HGA_REQUIRE(n, HGA_ERR_INVALID, "null out pointer");
+        hga::connections_gather(c, n);
+    });
+}
 
 }  // extern "C"

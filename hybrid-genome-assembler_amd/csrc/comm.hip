@@ -1,0 +1,409 @@
+// comm.hip — multi-GPU counting in the C ABI (SURVEY.md §8(b) hga_comm_init, §8(e)).
+//
+// One hga_ctx per rank: one process per GPU (torchrun, MPI, ...) or one thread per GPU in one
+// process (bin/jf_occurrences --gpus N).  A rank's transport is RCCL over xGMI (hga_comm_init,
+// ncclSend/ncclRecv of device buffers, enqueued on the ctx stream) or the caller's host-staged hook
+// (hga_comm_init_host: gloo, MPI, sockets, threads).  The protocol is the same either way:
+//   every rank: hga_count_run(ctx, 1) on its shard of every file (no per-file drop before the sum)
+//   hga_count_exchange(ctx, min):
+//     rows range-partitioned by canonical code on equal-mass splitters (owner o holds
+//     [spl[o-1], spl[o])), packed one u64 per row piece (exchange.hip kx_piece_hist/kx_pack_scatter),
+//     piece counts all-gathered, one all-to-all-v of the pieces, owner merge + `--bc` drop
+//     (kx_mb_*, run_jellyfish.sh:3-6).  Rows too wide to pack go as (key, counts[F]) rows.
+//   Afterwards the count queries of the ctx answer for the whole input, identically on every rank:
+//     spec_hist  owners' (threshold, total, count) triples gathered and summed per bin
+//                (JellyfishOccurrenceReader.cpp:88-108 over all k-mers);
+//     select*    owners' sorted exports concatenated in rank order = ascending (:110-135);
+//     select_device  keys stay on their owner, (n, n_discriminative) summed;
+//     rows/dump  owners' rows concatenated in rank order (:63-86; run_jellyfish.sh:5-6).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "exchange_protocol.hpp"
+#include "hga_internal.hpp"
+
+#define HGA_NCCL(call)                                                                               \
+    do {                                                                                             \
+        ncclResult_t r_ = (call);                                                                    \
+        if (r_ != ncclSuccess) throw ::hga::Error(HGA_ERR_COMM, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+namespace hga {
+
+namespace {
+
+struct RcclComm : Comm {
+    ncclComm_t comm = nullptr;
+    bool on_device() const override { return true; }
+    void alltoallv(hga_ctx* c, const void* const* send, const uint64_t* sb, void* const* recv,
+                   const uint64_t* rb) override {
+        if (sb[rank]) {
+            HGA_REQUIRE(rb[rank] == sb[rank], HGA_ERR_COMM, "alltoallv: self sizes disagree");
+            HGA_HIP(hipMemcpyAsync(recv[rank], send[rank], sb[rank], hipMemcpyDeviceToDevice, c->stream));
+        }
+        HGA_NCCL(ncclGroupStart());
+        for (int p = 0; p < nranks; ++p) {
+            if (p == rank) continue;
+            if (sb[p]) HGA_NCCL(ncclSend(send[p], sb[p], ncclUint8, p, comm, c->stream));
+            if (rb[p]) HGA_NCCL(ncclRecv(recv[p], rb[p], ncclUint8, p, comm, c->stream));
+        }
+        HGA_NCCL(ncclGroupEnd());
+    }
+    ~RcclComm() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+};
+
+struct HostComm : Comm {
+    hga_transport t{};
+    bool on_device() const override { return false; }
+    void alltoallv(hga_ctx*, const void* const* send, const uint64_t* sb, void* const* recv,
+                   const uint64_t* rb) override {
+        const int r = t.alltoallv(t.user, send, sb, recv, rb);
+        HGA_REQUIRE(r == 0, HGA_ERR_COMM, "host transport: alltoallv callback failed");
+    }
+};
+
+Comm& need_comm(hga_ctx* c) {
+    HGA_REQUIRE(c->comm, HGA_ERR_STATE, "no communicator: hga_comm_init / hga_comm_init_host first");
+    return *c->comm;
+}
+
+}  // namespace
+
+// Equal-size all-gather of host bytes: all[p * bytes ...] = rank p's `mine`.
+void comm_allgather(hga_ctx* c, const void* mine, uint64_t bytes, void* all) {
+    Comm& m = need_comm(c);
+    const int P = m.nranks;
+    std::vector<uint64_t> sz(P, bytes);
+    std::vector<const void*> sp(P);
+    std::vector<void*> rp(P);
+    if (!m.on_device()) {
+        for (int p = 0; p < P; ++p) {
+            sp[p] = mine;
+            rp[p] = static_cast<char*>(all) + (uint64_t)p * bytes;
+        }
+        m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+        return;
+    }
+    DevBuf d;
+    char* ds = static_cast<char*>(d.ensure(bytes * (P + 1) + 16));
+    HGA_HIP(hipMemcpyAsync(ds, mine, bytes, hipMemcpyHostToDevice, c->stream));
+    for (int p = 0; p < P; ++p) {
+        sp[p] = ds;
+        rp[p] = ds + bytes * (p + 1);
+    }
+    m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+    HGA_HIP(hipMemcpyAsync(all, ds + bytes, bytes * P, hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+}
+
+// Variable-size all-gather of host bytes, in rank order.
+std::vector<std::vector<char>> comm_allgatherv(hga_ctx* c, const void* mine, uint64_t bytes) {
+    Comm& m = need_comm(c);
+    const int P = m.nranks;
+    std::vector<uint64_t> sz(P);
+    comm_allgather(c, &bytes, 8, sz.data());
+    std::vector<std::vector<char>> out(P);
+    for (int p = 0; p < P; ++p) out[p].resize(sz[p]);
+    std::vector<uint64_t> sb(P, bytes);
+    std::vector<const void*> sp(P);
+    std::vector<void*> rp(P);
+    if (!m.on_device()) {
+        for (int p = 0; p < P; ++p) {
+            sp[p] = mine;
+            rp[p] = out[p].data();
+        }
+        m.alltoallv(c, sp.data(), sb.data(), rp.data(), sz.data());
+        return out;
+    }
+    uint64_t tot = 0;
+    for (auto v : sz) tot += v;
+    DevBuf d;
+    char* ds = static_cast<char*>(d.ensure(bytes + tot + 16));
+    if (bytes) HGA_HIP(hipMemcpyAsync(ds, mine, bytes, hipMemcpyHostToDevice, c->stream));
+    uint64_t o = bytes;
+    for (int p = 0; p < P; ++p) {
+        sp[p] = ds;
+        rp[p] = ds + o;
+        o += sz[p];
+    }
+    m.alltoallv(c, sp.data(), sb.data(), rp.data(), sz.data());
+    o = bytes;
+    for (int p = 0; p < P; ++p) {
+        if (sz[p]) HGA_HIP(hipMemcpyAsync(out[p].data(), ds + o, sz[p], hipMemcpyDeviceToHost, c->stream));
+        o += sz[p];
+    }
+    c->sync();
+    return out;
+}
+
+// All-to-all-v of DEVICE buffers whose per-peer slices are contiguous in rank order.
+void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) {
+    Comm& m = need_comm(c);
+    const int P = m.nranks;
+    std::vector<const void*> sp(P);
+    std::vector<void*> rp(P);
+    uint64_t so = 0, ro = 0, st = 0, rt = 0;
+    for (int p = 0; p < P; ++p) {
+        st += sb[p];
+        rt += rb[p];
+    }
+    if (m.on_device()) {
+        for (int p = 0; p < P; ++p) {
+            sp[p] = static_cast<const char*>(send) + so;
+            rp[p] = static_cast<char*>(recv) + ro;
+            so += sb[p];
+            ro += rb[p];
+        }
+        m.alltoallv(c, sp.data(), sb, rp.data(), rb);
+        return;
+    }
+    // host-staged: device -> host, the caller's transport, host -> device
+    std::vector<char> hs(st), hr(rt);
+    if (st) HGA_HIP(hipMemcpyAsync(hs.data(), send, st, hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+    for (int p = 0; p < P; ++p) {
+        sp[p] = hs.data() + so;
+        rp[p] = hr.data() + ro;
+        so += sb[p];
+        ro += rb[p];
+    }
+    m.alltoallv(c, sp.data(), sb, rp.data(), rb);
+    if (rt) HGA_HIP(hipMemcpyAsync(recv, hr.data(), rt, hipMemcpyHostToDevice, c->stream));
+    c->sync();
+}
+
+std::vector<uint64_t> owner_splitters(int k, int P) { return proto::owner_splitters(k, P); }
+
+namespace {
+
+// The protocol's view of a rank: the ctx's communicator ...
+struct CtxXport : proto::Xport {
+    hga_ctx* c;
+    explicit CtxXport(hga_ctx* cc) : c(cc) {
+        rank = cc->comm->rank;
+        nranks = cc->comm->nranks;
+    }
+    void allgather(const void* mine, uint64_t bytes, void* all) override { comm_allgather(c, mine, bytes, all); }
+    std::vector<std::vector<char>> allgatherv(const void* mine, uint64_t bytes) override {
+        return comm_allgatherv(c, mine, bytes);
+    }
+    void alltoallv_eng(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
+        comm_alltoallv_dev(c, send, sb, recv, rb);
+    }
+};
+
+// ... and its rows on the device (exchange.hip kernels).
+struct DevEngine {
+    hga_ctx* c;
+    int k() const { return c->count.k; }
+    uint32_t n_files() const { return c->count.n_files; }
+    uint64_t rows() const { return c->count.rows; }
+    int pack_bits() { return count_pack_bits(c); }
+    void* send_buf(uint64_t bytes) { return c->count.xsend.ensure(bytes + 64); }
+    void* recv_buf(uint64_t bytes) { return c->count.xrecv.ensure(bytes + 64); }
+    uint64_t partition_packed(const uint64_t* spl, uint32_t P, uint64_t* out, uint64_t cap, uint64_t* per) {
+        return count_partition_packed(c, spl, P, out, cap, per);
+    }
+    void merge_packed(const uint64_t* in, uint64_t n, uint32_t min) { count_merge_packed(c, in, n, min); }
+    void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per) {
+        count_partition(c, spl, P, keys, counts, per);
+    }
+    void merge(const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min) {
+        count_merge(c, keys, counts, n, min);
+    }
+    void sync() { c->sync(); }
+};
+
+}  // namespace
+
+void count_exchange(hga_ctx* c, uint32_t min_per_file) {
+    auto& s = c->count;
+    need_comm(c);
+    count_settle(c);
+    HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run(ctx, 1) first");
+    HGA_REQUIRE(s.min_per_file == 1, HGA_ERR_STATE, "the local count must keep singletons: hga_count_run(ctx, 1)");
+    HGA_REQUIRE(min_per_file >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
+    CtxXport x(c);
+    // instances / bytes this rank counted, summed for the global stats
+    std::vector<uint64_t> mine{s.instances, 0};
+    for (auto l : s.seq_len) mine[1] += l;
+    const std::vector<uint64_t> g = proto::sum_u64(x, mine);
+    DevEngine e{c};
+    proto::count_exchange(e, x, min_per_file);
+    s.g_instances = g[0];
+    s.g_bytes = g[1];
+    s.dist = true;
+}
+
+// ---- global answers of the count queries after hga_count_exchange ----------------------------
+
+void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out) {
+    std::vector<int64_t> local;
+    count_spec_hist(c, thr, n_thr, local);
+    CtxXport x(c);
+    out = proto::spec_hist_global(x, local);
+}
+
+void count_select_global(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* nd) {
+    std::vector<uint64_t> mine(2);
+    count_select(c, lower, upper, &mine[0], &mine[1]);
+    CtxXport x(c);
+    const std::vector<uint64_t> g = proto::sum_u64(x, mine);
+    *n = g[0];
+    *nd = g[1];
+}
+
+// The whole export on every rank (after count_select): keys ascending, flags.
+void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags) {
+    auto& s = c->count;
+    std::vector<uint64_t> k(s.n_sel);
+    std::vector<uint8_t> f(s.n_sel);
+    count_fetch_selected(c, k.data(), f.data());
+    CtxXport x(c);
+    keys = proto::concat(x, k);
+    flags = proto::concat(x, f);
+}
+
+void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
+    std::vector<uint64_t> k;
+    std::vector<uint32_t> v;
+    count_rows(c, file, k, v);
+    CtxXport x(c);
+    keys = proto::concat(x, k);
+    counts = proto::concat(x, v);
+}
+
+// ---- sharded categorization ------------------------------------------------------------------
+
+void lookup_gather(hga_ctx* c) {
+    auto& L = c->lookup;
+    need_comm(c);
+    HGA_REQUIRE(L.ran, HGA_ERR_STATE, "hga_lookup_run not called");
+    HGA_REQUIRE(!L.gathered, HGA_ERR_STATE, "index already gathered: hga_lookup_run first");
+    proto::CsrIndex in;
+    in.n = L.n_reads;
+    in.windows = L.windows;
+    in.reads_hit = L.reads_hit;
+    in.first_read_id = L.first_read_id;
+    in.n_sdk = L.n_sdk;
+    const uint64_t n = L.n_reads, H = L.hits, U = L.firsts, K = L.n_sdk;
+    in.hit_ptr.resize(n + 1);
+    in.first_ptr.resize(n + 1);
+    in.kci_ptr.resize(K + 1);
+    in.hit_kid.resize(H);
+    in.hit_pos.resize(H);
+    in.sorted_kid.resize(H);
+    in.first_kid.resize(U);
+    in.first_pos.resize(U);
+    in.kci_read.resize(H);
+    auto d2h = [&](void* dst, const DevBuf& src, size_t bytes) {
+        if (bytes) HGA_HIP(hipMemcpyAsync(dst, src.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    };
+    d2h(in.hit_ptr.data(), L.hit_ptr, (n + 1) * 8);
+    d2h(in.hit_kid.data(), L.hit_kid, H * 4);
+    d2h(in.hit_pos.data(), L.hit_pos, H * 4);
+    d2h(in.sorted_kid.data(), L.s_val2, H * 4);
+    d2h(in.first_ptr.data(), L.first_ptr, (n + 1) * 8);
+    d2h(in.first_kid.data(), L.first_kid, U * 4);
+    d2h(in.first_pos.data(), L.first_pos, U * 4);
+    d2h(in.kci_ptr.data(), L.kci_ptr, (K + 1) * 8);
+    d2h(in.kci_read.data(), L.kci_val, H * 4);
+    c->sync();
+    CtxXport x(c);
+    proto::CsrIndex g;
+    HGA_REQUIRE(proto::gather_index(x, in, g), HGA_ERR_INVALID,
+                "lookup shards must load the same SDK set and cover contiguous ReadID ranges in rank order");
+    HGA_REQUIRE(g.n < (1ull << 32), HGA_ERR_INVALID, "too many reads");
+    auto h2d = [&](DevBuf& dst, const void* src, size_t bytes) {
+        void* d = dst.ensure(bytes + 16);
+        if (bytes) HGA_HIP(hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, c->stream));
+    };
+    const uint64_t Hg = g.hit_kid.size(), Ug = g.first_kid.size();
+    h2d(L.hit_ptr, g.hit_ptr.data(), (g.n + 1) * 8);
+    h2d(L.hit_kid, g.hit_kid.data(), Hg * 4);
+    h2d(L.hit_pos, g.hit_pos.data(), Hg * 4);
+    h2d(L.s_val2, g.sorted_kid.data(), Hg * 4);
+    h2d(L.first_ptr, g.first_ptr.data(), (g.n + 1) * 8);
+    h2d(L.first_kid, g.first_kid.data(), Ug * 4);
+    h2d(L.first_pos, g.first_pos.data(), Ug * 4);
+    h2d(L.kci_ptr, g.kci_ptr.data(), (K + 1) * 8);
+    h2d(L.kci_val, g.kci_read.data(), Hg * 4);
+    c->sync();
+    L.loc_n_reads = L.n_reads;
+    L.loc_first_read_id = L.first_read_id;
+    L.n_reads = g.n;
+    L.first_read_id = g.first_read_id;
+    L.hits = Hg;
+    L.firsts = Ug;
+    L.windows = g.windows;
+    L.reads_hit = g.reads_hit;
+    L.gathered = true;
+    c->conn.ready = false;
+}
+
+void connections_gather(hga_ctx* c, uint64_t* n_out) {
+    auto& S = c->conn;
+    need_comm(c);
+    HGA_REQUIRE(S.ready, HGA_ERR_STATE, "hga_connections_run not called");
+    proto::ConnList in;
+    in.x.resize(S.n);
+    in.y.resize(S.n);
+    in.s.resize(S.n);
+    in.g.resize(S.n);
+    connections_fetch(c, in.x.data(), in.y.data(), in.s.data(), in.g.data());
+    CtxXport x(c);
+    const proto::ConnList g = proto::merge_connections(x, in);
+    const uint64_t N = g.x.size();
+    auto h2d = [&](DevBuf& dst, const void* src, size_t bytes) {
+        void* d = dst.ensure(bytes + 16);
+        if (bytes) HGA_HIP(hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, c->stream));
+    };
+    h2d(S.ox, g.x.data(), N * 4);
+    h2d(S.oy, g.y.data(), N * 4);
+    h2d(S.os, g.s.data(), N * 8);
+    h2d(S.og, g.g.data(), N);
+    c->sync();
+    S.n = N;
+    *n_out = N;
+}
+
+void comm_init_rccl(hga_ctx* c, const void* id, int rank, int nranks) {
+    HGA_REQUIRE(id, HGA_ERR_INVALID, "null unique id");
+    HGA_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, HGA_ERR_INVALID, "rank out of range");
+    auto cm = std::make_unique<RcclComm>();
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    HGA_NCCL(ncclCommInitRank(&cm->comm, nranks, uid, rank));
+    cm->rank = rank;
+    cm->nranks = nranks;
+    c->comm = std::move(cm);
+    c->count.dist = false;
+}
+
+void comm_init_host(hga_ctx* c, int rank, int nranks, const hga_transport* t) {
+    HGA_REQUIRE(t && t->alltoallv, HGA_ERR_INVALID, "transport with an alltoallv callback required");
+    HGA_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, HGA_ERR_INVALID, "rank out of range");
+    auto cm = std::make_unique<HostComm>();
+    cm->t = *t;
+    cm->rank = rank;
+    cm->nranks = nranks;
+    c->comm = std::move(cm);
+    c->count.dist = false;
+}
+
+}  // namespace hga
+
+extern "C" hga_status hga_comm_unique_id(void* id) {
+    if (!id) return HGA_ERR_INVALID;
+    ncclUniqueId uid;
+    const ncclResult_t r = ncclGetUniqueId(&uid);
+    if (r != ncclSuccess) return HGA_ERR_COMM;
+    std::memcpy(id, &uid, sizeof(uid));
+    return HGA_OK;
+}

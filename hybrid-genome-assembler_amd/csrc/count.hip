@@ -1438,6 +1438,7 @@ void count_begin(hga_ctx* c, int k, uint32_t n_files) {
     s.n_files = n_files;
     s.begun = true;
     s.ran = false;
+    s.dist = false;
     s.rows = s.instances = s.n_sel = 0;
     s.pending = false;
 }
@@ -1466,6 +1467,7 @@ void count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n) {
     c->sync();
     s.seq_len[file] = need;
     s.ran = false;
+    s.dist = false;
 }
 
 void count_run(hga_ctx* c, uint32_t min_per_file) {
@@ -1685,6 +1687,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     // them (count_settle), so the following spec_hist queues behind the count without a gap.
     s.rows_cap = cap;
     s.ran = true;
+    s.dist = false;
     s.n_sel = 0;
     s.pending = true;
     bool dumps = false;
@@ -1732,6 +1735,7 @@ void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint3
         dc.push_back(counts[i]);
     }
     s.ran = false;
+    s.dist = false;
 }
 
 // Folds the staged dump rows into the counted rows: one merge (sum per key, no drop: the

@@ -220,6 +220,7 @@ void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint6
     }
     s.min_per_file = min_c;
     s.ran = true;
+    s.dist = false;
     s.n_sel = 0;
 }
 
@@ -777,6 +778,7 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
     }
     s.min_per_file = min_c;
     s.ran = true;
+    s.dist = false;
     s.n_sel = 0;
 }
 

@@ -1,0 +1,274 @@
+// exchange_protocol.hpp — the multi-GPU counting protocol, written once over two
+// small interfaces so that the product (comm.hip: device engine, RCCL or host-staged transport) and
+// the CPU test harness (tests/native/xproto_host.cpp: host engine, the caller's transport hook)
+// run the same code.  Plain C++17, no HIP.
+//
+//   every rank has counted its shard with min 1 (no per-file drop before the global sum);
+//   owner o holds canonical codes [spl[o-1], spl[o]) on equal-mass splitters;
+//   rows go to their owner as packed u64 pieces (or wide (key, counts[F]) rows), sizes first;
+//   the owner sums equal keys and drops counts < min per file (jellyfish --bc, run_jellyfish.sh:3-6);
+//   histogram triples of all owners are summed per (threshold, total) bin in std::map order
+//   (JellyfishOccurrenceReader.cpp:88-108); exports and rows concatenate in rank order, which is
+//   ascending code order (:63-86, :110-135).
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+#include <map>
+#include <utility>
+#include <vector>
+
+namespace hga {
+namespace proto {
+
+// Collectives of one rank.  Host-memory forms take host pointers; `alltoallv_eng` moves engine
+// memory (device memory in the product) with per-peer slices contiguous in rank order.
+struct Xport {
+    int rank = 0, nranks = 1;
+    virtual ~Xport() = default;
+    virtual void allgather(const void* mine, uint64_t bytes, void* all) = 0;
+    virtual std::vector<std::vector<char>> allgatherv(const void* mine, uint64_t bytes) = 0;
+    virtual void alltoallv_eng(const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes) = 0;
+};
+
+// Owner ranges over canonical codes in [0, 4^k): canonical = min(fwd, rc) of uniform codes has mass
+// 1 - (1 - x/4^k)^2 below x, so owner o starts at 4^k (1 - sqrt(1 - o/P)).  Any ascending splitters
+// give the same global result; these balance the load.
+inline std::vector<uint64_t> owner_splitters(int k, int P) {
+    const long double m = std::ldexp(1.0L, 2 * k);
+    std::vector<uint64_t> out;
+    for (int o = 1; o < P; ++o) {
+        const long double x = m * (1.0L - std::sqrt(1.0L - (long double)o / P));
+        uint64_t v = x >= m ? (uint64_t)(m - 1) : (uint64_t)x;
+        if (!out.empty() && v < out.back()) v = out.back();
+        out.push_back(v);
+    }
+    return out;
+}
+
+// Engine E (the rank's rows after a local count with min 1):
+//   int k(); uint32_t n_files(); uint64_t rows(); int pack_bits();
+//   void* send_buf(uint64_t bytes); void* recv_buf(uint64_t bytes);     (engine memory, kept by E)
+//   uint64_t partition_packed(const uint64_t* spl, uint32_t P, uint64_t* out, uint64_t cap, uint64_t* per);
+//       (returns the piece total; writes nothing when it exceeds cap)
+//   void merge_packed(const uint64_t* pieces, uint64_t n, uint32_t min);
+//   void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per);
+//   void merge(const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min);
+//   void sync();
+// Returns the pieces / rows this owner received.
+template <class E>
+uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file) {
+    const int P = x.nranks;
+    const std::vector<uint64_t> spl = owner_splitters(e.k(), P);
+    std::vector<uint64_t> per(P), all((size_t)P * P), rn(P), sb(P), rb(P);
+    auto recv_counts = [&] {
+        x.allgather(per.data(), 8 * (uint64_t)P, all.data());
+        uint64_t n = 0;
+        for (int p = 0; p < P; ++p) n += (rn[p] = all[(size_t)p * P + x.rank]);
+        return n;
+    };
+    if (e.pack_bits() > 0) {   // one u64 piece per row (a count past the piece width: several pieces)
+        const uint64_t rows = e.rows();
+        uint64_t cap = rows + rows / 64 + 1024;
+        uint64_t* out = static_cast<uint64_t*>(e.send_buf(cap * 8));
+        uint64_t total = e.partition_packed(spl.data(), (uint32_t)P, out, cap, per.data());
+        if (total > cap) {
+            cap = total;
+            out = static_cast<uint64_t*>(e.send_buf(cap * 8));
+            total = e.partition_packed(spl.data(), (uint32_t)P, out, cap, per.data());
+        }
+        const uint64_t n = recv_counts();
+        uint64_t* in = static_cast<uint64_t*>(e.recv_buf((n ? n : 1) * 8));
+        for (int p = 0; p < P; ++p) {
+            sb[p] = per[p] * 8;
+            rb[p] = rn[p] * 8;
+        }
+        x.alltoallv_eng(out, sb.data(), in, rb.data());
+        e.merge_packed(in, n, min_per_file);
+        return n;
+    }
+    // wide rows: keys u64 then counts u32[F] row-major, one all-to-all each
+    const uint32_t F = e.n_files();
+    const uint64_t rows = e.rows(), rcap = rows ? rows : 1;
+    char* w = static_cast<char*>(e.send_buf(rcap * (8 + 4ull * F)));
+    uint64_t* keys = reinterpret_cast<uint64_t*>(w);
+    uint32_t* cnts = reinterpret_cast<uint32_t*>(w + rcap * 8);
+    e.partition(spl.data(), (uint32_t)P, keys, cnts, per.data());
+    const uint64_t n = recv_counts(), ncap = n ? n : 1;
+    char* r = static_cast<char*>(e.recv_buf(ncap * (8 + 4ull * F)));
+    uint64_t* rk = reinterpret_cast<uint64_t*>(r);
+    uint32_t* rc = reinterpret_cast<uint32_t*>(r + ncap * 8);
+    for (int p = 0; p < P; ++p) {
+        sb[p] = per[p] * 8;
+        rb[p] = rn[p] * 8;
+    }
+    x.alltoallv_eng(keys, sb.data(), rk, rb.data());
+    for (int p = 0; p < P; ++p) {
+        sb[p] = per[p] * 4 * F;
+        rb[p] = rn[p] * 4 * F;
+    }
+    x.alltoallv_eng(cnts, sb.data(), rc, rb.data());
+    e.sync();
+    e.merge(rk, rc, n, min_per_file);
+    return n;
+}
+
+// Owners' (threshold index, total, count) triples -> the global histogram, (threshold, total) order.
+inline std::vector<int64_t> spec_hist_global(Xport& x, const std::vector<int64_t>& local) {
+    const auto parts = x.allgatherv(local.data(), local.size() * 8);
+    std::map<std::pair<int64_t, int64_t>, int64_t> bins;
+    for (const auto& pt : parts) {
+        const int64_t* t = reinterpret_cast<const int64_t*>(pt.data());
+        for (size_t i = 0; i + 3 <= pt.size() / 8; i += 3) bins[{t[i], t[i + 1]}] += t[i + 2];
+    }
+    std::vector<int64_t> out;
+    out.reserve(bins.size() * 3);
+    for (const auto& b : bins) {
+        out.push_back(b.first.first);
+        out.push_back(b.first.second);
+        out.push_back(b.second);
+    }
+    return out;
+}
+
+// Element-wise sums of a small u64 vector over all ranks.
+inline std::vector<uint64_t> sum_u64(Xport& x, const std::vector<uint64_t>& mine) {
+    std::vector<uint64_t> all(mine.size() * x.nranks), out(mine.size(), 0);
+    x.allgather(mine.data(), mine.size() * 8, all.data());
+    for (int p = 0; p < x.nranks; ++p)
+        for (size_t i = 0; i < mine.size(); ++i) out[i] += all[p * mine.size() + i];
+    return out;
+}
+
+// Every rank's vector of T, concatenated in rank order (owner order = ascending codes).
+template <class T>
+std::vector<T> concat(Xport& x, const std::vector<T>& mine) {
+    const auto parts = x.allgatherv(mine.data(), mine.size() * sizeof(T));
+    std::vector<T> out;
+    for (const auto& pt : parts) {
+        const T* v = reinterpret_cast<const T*>(pt.data());
+        out.insert(out.end(), v, v + pt.size() / sizeof(T));
+    }
+    return out;
+}
+
+// ---- sharded categorization -------------------------------------------
+// construct_indices output of one rank (ReadClusteringEngine.cpp:234-299) over its contiguous ReadID
+// range: per-read CSRs (hit_ptr[n+1] with hit_kid/hit_pos/sorted_kid[H], first_ptr[n+1] with
+// first_kid/first_pos[U]) and kmer_component_index kci_ptr[K+1] / kci_read[H] holding read
+// indices relative to first_read_id.
+struct CsrIndex {
+    uint64_t n = 0, windows = 0, reads_hit = 0;
+    uint32_t first_read_id = 1, n_sdk = 0;
+    std::vector<uint64_t> hit_ptr, first_ptr, kci_ptr;
+    std::vector<uint32_t> hit_kid, hit_pos, sorted_kid, first_kid, first_pos, kci_read;
+};
+
+// The whole input's index from every rank's shard, identical on every rank: reads concatenated in
+// rank order (ReadIDs must be contiguous across ranks), kmer_component_index per KmerID the ranks'
+// lists concatenated in rank order — ascending ReadIDs, as the reference's sort leaves them
+// (:282-284).  Returns false when the shards are not contiguous or use different SDK sets.
+inline bool gather_index(Xport& x, const CsrIndex& in, CsrIndex& out) {
+    const int P = x.nranks;
+    const std::vector<uint64_t> mine{in.n, in.hit_kid.size(), in.first_kid.size(), in.first_read_id, in.n_sdk,
+                                     in.windows, in.reads_hit};
+    std::vector<uint64_t> all(mine.size() * P);
+    x.allgather(mine.data(), mine.size() * 8, all.data());
+    auto at = [&](int r, int i) { return all[(size_t)r * mine.size() + i]; };
+    std::vector<uint64_t> read_off(P + 1, 0), hit_off(P + 1, 0), first_off(P + 1, 0);
+    bool ok = true;
+    for (int r = 0; r < P; ++r) {
+        read_off[r + 1] = read_off[r] + at(r, 0);
+        hit_off[r + 1] = hit_off[r] + at(r, 1);
+        first_off[r + 1] = first_off[r] + at(r, 2);
+        ok = ok && at(r, 4) == at(0, 4) && at(r, 3) == at(0, 3) + read_off[r];
+    }
+    if (!ok) return false;
+    const int me = x.rank;
+    std::vector<uint64_t> hp(in.n), fp(in.n);
+    for (uint64_t i = 0; i < in.n; ++i) {
+        hp[i] = in.hit_ptr[i + 1] + hit_off[me];
+        fp[i] = in.first_ptr[i + 1] + first_off[me];
+    }
+    std::vector<uint32_t> kr(in.kci_read);
+    for (auto& v : kr) v += (uint32_t)read_off[me];
+    out = CsrIndex();
+    out.n = read_off[P];
+    out.first_read_id = (uint32_t)at(0, 3);
+    out.n_sdk = (uint32_t)at(0, 4);
+    for (int r = 0; r < P; ++r) {
+        out.windows += at(r, 5);
+        out.reads_hit += at(r, 6);
+    }
+    out.hit_ptr = concat(x, hp);
+    out.hit_ptr.insert(out.hit_ptr.begin(), 0);
+    out.first_ptr = concat(x, fp);
+    out.first_ptr.insert(out.first_ptr.begin(), 0);
+    out.hit_kid = concat(x, in.hit_kid);
+    out.hit_pos = concat(x, in.hit_pos);
+    out.sorted_kid = concat(x, in.sorted_kid);
+    out.first_kid = concat(x, in.first_kid);
+    out.first_pos = concat(x, in.first_pos);
+    const std::vector<uint64_t> kps = concat(x, in.kci_ptr);   // P blocks of K+1
+    const std::vector<uint32_t> krs = concat(x, kr);           // P blocks of H_r
+    const uint64_t K = out.n_sdk;
+    out.kci_ptr.assign(K + 1, 0);
+    for (int r = 0; r < P; ++r)
+        for (uint64_t i = 0; i < K; ++i) out.kci_ptr[i + 1] += kps[r * (K + 1) + i + 1] - kps[r * (K + 1) + i];
+    for (uint64_t i = 0; i < K; ++i) out.kci_ptr[i + 1] += out.kci_ptr[i];
+    out.kci_read.resize(out.kci_ptr[K]);
+    for (uint64_t i = 0; i < K; ++i) {
+        uint64_t o = out.kci_ptr[i];
+        for (int r = 0; r < P; ++r) {
+            const uint64_t a = kps[r * (K + 1) + i], b = kps[r * (K + 1) + i + 1];
+            for (uint64_t j = a; j < b; ++j) out.kci_read[o++] = krs[hit_off[r] + j];
+        }
+    }
+    return true;
+}
+
+// Connections of every rank's own pivots (each rank's list already in the reference order: score
+// descending, ties by (pivot, candidate), ReadClusteringEngine.cpp:331) merged into the global list.
+struct ConnList {
+    std::vector<uint32_t> x, y;
+    std::vector<uint64_t> s;
+    std::vector<uint8_t> g;
+};
+inline ConnList merge_connections(Xport& xp, const ConnList& in) {
+    const std::vector<uint64_t> cnt = concat(xp, std::vector<uint64_t>{in.x.size()});
+    const std::vector<uint32_t> X = concat(xp, in.x), Y = concat(xp, in.y);
+    const std::vector<uint64_t> S = concat(xp, in.s);
+    const std::vector<uint8_t> G = concat(xp, in.g);
+    const int P = xp.nranks;
+    std::vector<uint64_t> pos(P, 0), end(P, 0);
+    for (int r = 0; r < P; ++r) {
+        pos[r] = r ? end[r - 1] : 0;
+        end[r] = pos[r] + cnt[r];
+    }
+    auto before = [&](uint64_t a, uint64_t b) {   // (score desc, x, y)
+        if (S[a] != S[b]) return S[a] > S[b];
+        if (X[a] != X[b]) return X[a] < X[b];
+        return Y[a] < Y[b];
+    };
+    ConnList out;
+    const uint64_t N = X.size();
+    out.x.reserve(N);
+    out.y.reserve(N);
+    out.s.reserve(N);
+    out.g.reserve(N);
+    while (true) {
+        int best = -1;
+        for (int r = 0; r < P; ++r)
+            if (pos[r] < end[r] && (best < 0 || before(pos[r], pos[best]))) best = r;
+        if (best < 0) break;
+        const uint64_t i = pos[best]++;
+        out.x.push_back(X[i]);
+        out.y.push_back(Y[i]);
+        out.s.push_back(S[i]);
+        out.g.push_back(G[i]);
+    }
+    return out;
+}
+
+}  // namespace proto
+}  // namespace hga

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -126,15 +127,17 @@ struct CountState {
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
         sel_keys, sel_tmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, pk_all, vd_all, blist,
-        binned3, file_start3;
+        binned3, file_start3, xsend, xrecv;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
+    uint64_t g_instances = 0, g_bytes = 0;   // over all ranks (set by count_exchange)
     std::vector<char> tab_host;   // last uploaded per-file tables
     // pre-counted dump rows per file (hga_count_add_rows), merged verbatim at the end of count_run
     std::vector<std::vector<uint64_t>> dump_keys;
     std::vector<std::vector<uint32_t>> dump_cnt;
     uint32_t buckets = 0, fb = 0, max_split = 1;
     bool pending = false;   // count_run's counters not read back yet (count_settle)
+    bool dist = false;      // rows are this rank's owner range after hga_count_exchange
     ~CountState() {
         for (auto* b : seq) delete b;
     }
@@ -155,6 +158,10 @@ struct LookupState {
         scratch2, scratch3, big_list, hll_part;
     std::vector<uint64_t> h_offsets;
     uint64_t windows = 0, hits = 0, firsts = 0, reads_hit = 0;
+    // hga_lookup_gather: the results hold the whole input's index; this rank's own read set is kept
+    bool gathered = false;
+    uint64_t loc_n_reads = 0;
+    uint32_t loc_first_read_id = 1;
 };
 
 struct ConnState {
@@ -162,6 +169,18 @@ struct ConnState {
     uint64_t n = 0, cap_hint = 0;
     DevBuf piv, cat, ctr, rpre, ovf, ovf2, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og, pst, pcnt, sk2, sv2,
         lst;
+};
+
+// Multi-GPU transport of one rank (comm.hip): RCCL over xGMI, or a caller's host-staged hook.
+struct Comm {
+    int rank = 0, nranks = 1;
+    virtual ~Comm() = default;
+    // true: alltoallv moves device memory (RCCL); false: host memory (the caller stages)
+    virtual bool on_device() const = 0;
+    // Collective: send_bytes[p] bytes at send[p] go to rank p; recv_bytes[p] bytes from rank p land at
+    // recv[p].  Every rank calls it in the same order.
+    virtual void alltoallv(hga_ctx* c, const void* const* send, const uint64_t* send_bytes, void* const* recv,
+                           const uint64_t* recv_bytes) = 0;
 };
 
 }  // namespace hga
@@ -176,6 +195,7 @@ struct hga_ctx {
     hga::ConnState conn;
     hga::PinnedBuf pinned;   // small host<->device staging (see count_spec_hist)
     hga::PinnedBuf pinned_sel;   // count_select counters + top-digit histogram
+    std::unique_ptr<hga::Comm> comm;   // hga_comm_init*: the count results become global
 
     // Launch helper: records events around the launch when profiling is on.
     template <class F>
@@ -219,6 +239,21 @@ int count_pack_bits(hga_ctx* c);
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,
                                 uint64_t cap_out, uint64_t* pieces_per_owner);
 void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t min_c);
+
+// comm.hip: multi-GPU counting (hga_comm_*, hga_count_exchange) and the global query answers
+void comm_init_rccl(hga_ctx* c, const void* id, int rank, int nranks);
+void comm_init_host(hga_ctx* c, int rank, int nranks, const hga_transport* t);
+void comm_allgather(hga_ctx* c, const void* mine, uint64_t bytes, void* all);
+std::vector<std::vector<char>> comm_allgatherv(hga_ctx* c, const void* mine, uint64_t bytes);
+void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb);
+std::vector<uint64_t> owner_splitters(int k, int P);
+void count_exchange(hga_ctx* c, uint32_t min_per_file);
+void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out);
+void count_select_global(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* nd);
+void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags);
+void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);
+void lookup_gather(hga_ctx* c);
+void connections_gather(hga_ctx* c, uint64_t* n);
 
 void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n);
 void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, uint64_t n,

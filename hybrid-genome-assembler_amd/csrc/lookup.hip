@@ -852,6 +852,7 @@ void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, ui
     for (uint64_t i = 0; i < n; ++i)
         HGA_REQUIRE(offsets[i + 1] >= offsets[i], HGA_ERR_INVALID, "offsets must be non-decreasing");
     const uint64_t nb = n ? offsets[n] - offsets[0] : 0;
+    L.gathered = false;
     L.n_reads = n;
     L.n_bases = nb;
     L.first_read_id = first_id;
@@ -889,6 +890,11 @@ void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, ui
 
 void lookup_run(hga_ctx* c) {
     auto& L = c->lookup;
+    if (L.gathered) {   // back to this rank's own reads (hga_lookup_gather replaced the results)
+        L.n_reads = L.loc_n_reads;
+        L.first_read_id = L.loc_first_read_id;
+        L.gathered = false;
+    }
     HGA_REQUIRE(L.loaded, HGA_ERR_STATE, "hga_lookup_load not called");
     HGA_REQUIRE(L.have_reads, HGA_ERR_STATE, "hga_lookup_set_reads not called");
     c->conn.ready = false;

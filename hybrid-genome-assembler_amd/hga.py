@@ -46,6 +46,15 @@ class LookupResult(C.Structure):
                 ("kci_ptr", _u64p), ("kci_read", _u32p)]
 
 
+# hga_transport (include/hga.h): one collective all-to-all-v over host memory
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
+                           C.POINTER(C.c_void_p), C.POINTER(C.c_uint64))
+
+
+class Transport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("alltoallv", ALLTOALLV_FN)]
+
+
 _lib = None
 _host = None
 
@@ -87,6 +96,14 @@ HGA_SYMBOLS = {
     "hga_profile_reset": (C.c_int, [_vp]),
     "hga_profile_get": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_double), _u64p]),
     "hga_sync": (C.c_int, [_vp]),
+    "hga_comm_unique_id": (C.c_int, [_vp]),
+    "hga_comm_init": (C.c_int, [_vp, _vp, C.c_int, C.c_int]),
+    "hga_comm_init_host": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(Transport)]),
+    "hga_comm_info": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "hga_comm_destroy": (C.c_int, [_vp]),
+    "hga_count_exchange": (C.c_int, [_vp, C.c_uint32]),
+    "hga_lookup_gather": (C.c_int, [_vp]),
+    "hga_connections_gather": (C.c_int, [_vp, _u64p]),
 }
 
 HOST_SYMBOLS = {
@@ -169,6 +186,31 @@ def _p(arr, ct):
     return arr.ctypes.data_as(C.POINTER(ct))
 
 
+def comm_unique_id() -> bytes:
+    """RCCL unique id (HGA_UNIQUE_ID_BYTES) to hand to every rank's Ctx.comm_init."""
+    b = C.create_string_buffer(128)
+    _ck(lib().hga_comm_unique_id(b))
+    return b.raw
+
+
+def transport_of(alltoallv, nranks: int):
+    """An hga_transport whose callback calls alltoallv(send, recv), each a list of (address, nbytes)
+    per rank; an exception becomes a failed status.  Keep the returned object alive while in use."""
+    def cb(_user, send, sb, recv, rb):
+        try:
+            alltoallv([(send[p] or 0, int(sb[p])) for p in range(nranks)],
+                      [(recv[p] or 0, int(rb[p])) for p in range(nranks)])
+            return 0
+        except Exception as e:   # noqa: BLE001 - reported through the status
+            import sys
+            print(f"hga transport callback failed: {e!r}", file=sys.stderr)
+            return 1
+    fn = ALLTOALLV_FN(cb)
+    t = Transport(None, fn)
+    t._keep = fn
+    return t
+
+
 def device_count() -> int:
     n = C.c_int(0)
     _ck(lib().hga_device_count(C.byref(n)))
@@ -199,6 +241,33 @@ class Ctx:
             self.close()
         except Exception:
             pass
+
+    # ---- multi-GPU (include/hga.h: hga_comm_*, hga_count_exchange)
+    def comm_init(self, unique_id: bytes, rank: int, nranks: int):
+        _ck(lib().hga_comm_init(self._h, C.c_char_p(unique_id), rank, nranks))
+
+    def comm_init_host(self, rank: int, nranks: int, transport: "Transport"):
+        self._transport = transport
+        _ck(lib().hga_comm_init_host(self._h, rank, nranks, C.byref(transport)))
+
+    def comm_info(self):
+        r, n = C.c_int(), C.c_int()
+        _ck(lib().hga_comm_info(self._h, C.byref(r), C.byref(n)))
+        return r.value, n.value
+
+    def comm_destroy(self):
+        _ck(lib().hga_comm_destroy(self._h))
+
+    def count_exchange(self, min_per_file: int = 2):
+        _ck(lib().hga_count_exchange(self._h, min_per_file))
+
+    def lookup_gather(self):
+        _ck(lib().hga_lookup_gather(self._h))
+
+    def connections_gather(self) -> int:
+        n = C.c_uint64()
+        _ck(lib().hga_connections_gather(self._h, C.byref(n)))
+        return n.value
 
     # ---- counting
     def count_begin(self, k: int, n_files: int):

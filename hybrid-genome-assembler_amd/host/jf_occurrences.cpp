@@ -21,6 +21,11 @@
 // estimates for k = 11, 13, ... filled on the GPU (hga_hll_registers), printed per k.
 //
 // HGA_DEVICE selects the GPU (default 0); HGA_PLOT_CMD overrides the plot command.
+//
+// --gpus N (extension, default 1): N ranks in this process, one per GPU (ranks.h), each counting a
+// contiguous share of every file's reads with min 1; hga_count_exchange moves the rows to their owner
+// ranks (RCCL over xGMI, or a host transport when ranks share a GPU) and applies the --bc drop; the
+// histogram, dumps and export are then the whole input's, written by rank 0 exactly as with one GPU.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -36,6 +41,7 @@
 #include "args.h"
 #include "hga.h"
 #include "kmer_analysis.h"
+#include "ranks.h"
 #include "seqio.h"
 
 namespace {
@@ -100,6 +106,9 @@ int main(int argc, char* argv[]) {
     ap.add("k-size", 'k', false, "Size of kmer to analyze & select", [&](const std::string& v) { k = std::stoi(v); });
     ap.add("output", 'o', false, "Output path for the counting bloom filter",
            [&](const std::string& v) { output_path = v; });
+    int gpus = 1;
+    ap.add("gpus", 0, false, "GPUs to count on, one rank each (MI355X build extension; default 1)",
+           [&](const std::string& v) { gpus = std::stoi(v); });
     ap.parse(argc, argv);
     for (auto& p : ap.positional) read_paths.push_back(p);
     if (ap.has("help")) {
@@ -109,18 +118,19 @@ int main(int argc, char* argv[]) {
     if (read_paths.empty()) throw std::invalid_argument("You need to specify paths to read files");
 
     const char* dev_env = std::getenv("HGA_DEVICE");
-    hga_ctx* ctx = nullptr;
-    check(hga_ctx_create(&ctx, dev_env ? std::atoi(dev_env) : 0), "hga_ctx_create");
+    hgah::Ranks ranks(gpus, dev_env ? std::atoi(dev_env) : 0);
+    hga_ctx* ctx = ranks.ctx[0];
+    const int P = ranks.size();
     if (!ap.has("k-size")) {   // :40-44 — SequenceRecordIterator(read_paths, true) + get_unique_k_length
         const hgah::RecordSet rs = hgah::load_records(read_paths, true, false);
         check(hga_lookup_set_reads(ctx, rs.bases.data(), rs.offsets.data(), rs.size(), 1), "hga_lookup_set_reads");
         k = hgah::unique_k_length(ctx, std::cout).first;
     }
-    check(hga_count_begin(ctx, k, (uint32_t)read_paths.size()), "hga_count_begin");
+    for (auto* c : ranks.ctx) check(hga_count_begin(c, k, (uint32_t)read_paths.size()), "hga_count_begin");
     std::vector<uint32_t> counted;
     for (uint32_t f = 0; f < read_paths.size(); ++f) {
         const std::string cache = hgah::dump_cache_path(read_paths[f], k);
-        if (std::filesystem::exists(cache)) {
+        if (std::filesystem::exists(cache)) {   // the dump's rows enter once, on rank 0
             std::vector<uint64_t> dk;
             std::vector<uint32_t> dc;
             hgah::read_kmer_dump(cache, k, dk, dc);
@@ -128,26 +138,44 @@ int main(int argc, char* argv[]) {
             continue;
         }
         const hgah::Bytes s = hgah::jf_stream(read_paths[f]);
-        check(hga_count_add(ctx, f, s.data(), s.size()), "hga_count_add");
+        for (int r = 0; r < P; ++r) {
+            const auto [a, b] = hgah::shard_of(s.data(), s.size(), r, P);
+            check(hga_count_add(ranks.ctx[r], f, s.data() + a, b - a), "hga_count_add");
+        }
         counted.push_back(f);
     }
-    check(hga_count_run(ctx, 2), "hga_count_run");   // jellyfish --bc: per-file singletons dropped
+    if (P == 1) {
+        check(hga_count_run(ctx, 2), "hga_count_run");   // jellyfish --bc: per-file singletons dropped
+    } else {
+        ranks.each([](int, hga_ctx* c) {
+            check(hga_count_run(c, 1), "hga_count_run");   // no drop before the global sum
+            check(hga_count_exchange(c, 2), "hga_count_exchange");
+        });
+    }
     const char* cache_env = std::getenv("HGA_DUMP_CACHE");
     if (!(cache_env && std::string(cache_env) == "0"))
         for (uint32_t f : counted) {
-            uint64_t *dk = nullptr, n_d = 0;
-            uint32_t* dc = nullptr;
-            check(hga_count_dump(ctx, f, &dk, &dc, &n_d), "hga_count_dump");
-            hgah::write_kmer_dump(hgah::dump_cache_path(read_paths[f], k), k, dk, dc, n_d);
-            hga_free(dk);
-            hga_free(dc);
+            std::vector<uint64_t*> dk(P, nullptr);
+            std::vector<uint32_t*> dc(P, nullptr);
+            std::vector<uint64_t> n_d(P, 0);
+            ranks.each([&](int r, hga_ctx* c) { check(hga_count_dump(c, f, &dk[r], &dc[r], &n_d[r]), "hga_count_dump"); });
+            hgah::write_kmer_dump(hgah::dump_cache_path(read_paths[f], k), k, dk[0], dc[0], n_d[0]);
+            for (int r = 0; r < P; ++r) {
+                hga_free(dk[r]);
+                hga_free(dc[r]);
+            }
         }
 
     const std::set<double> thresholds = {70, 85, 90, 95, 99, 100, 100.01};
     const std::vector<double> thr(thresholds.begin(), thresholds.end());
-    int64_t* tri = nullptr;
-    uint64_t n_tri = 0;
-    check(hga_count_spec_hist(ctx, thr.data(), (uint32_t)thr.size(), &tri, &n_tri), "hga_count_spec_hist");
+    std::vector<int64_t*> tris(P, nullptr);
+    std::vector<uint64_t> n_tris(P, 0);
+    ranks.each([&](int r, hga_ctx* c) {
+        check(hga_count_spec_hist(c, thr.data(), (uint32_t)thr.size(), &tris[r], &n_tris[r]), "hga_count_spec_hist");
+    });
+    for (int r = 1; r < P; ++r) hga_free(tris[r]);
+    int64_t* tri = tris[0];
+    const uint64_t n_tri = n_tris[0];
     KmerSpecificity spec;
     for (double t : thr) spec.insert({t, {}});
     for (uint64_t i = 0; i < n_tri; ++i)
@@ -167,10 +195,19 @@ int main(int argc, char* argv[]) {
                       hgah::fmt_double(percent * 100) + "%.txt";
 
     // export_kmers (JellyfishOccurrenceReader.cpp:110-135)
-    uint64_t* keys = nullptr;
-    uint8_t* disc = nullptr;
-    uint64_t n = 0, n_disc_all = 0;
-    check(hga_count_select_ex(ctx, lower, upper, &keys, &disc, &n, &n_disc_all), "hga_count_select_ex");
+    std::vector<uint64_t*> keys_r(P, nullptr);
+    std::vector<uint8_t*> disc_r(P, nullptr);
+    std::vector<uint64_t> n_r(P, 0), nd_r(P, 0);
+    ranks.each([&](int r, hga_ctx* c) {
+        check(hga_count_select_ex(c, lower, upper, &keys_r[r], &disc_r[r], &n_r[r], &nd_r[r]), "hga_count_select_ex");
+    });
+    for (int r = 1; r < P; ++r) {
+        hga_free(keys_r[r]);
+        hga_free(disc_r[r]);
+    }
+    uint64_t* keys = keys_r[0];
+    uint8_t* disc = disc_r[0];
+    const uint64_t n = n_r[0];
     std::random_device dev;
     std::mt19937 rng(dev());
     std::uniform_real_distribution<> dis(0.0, 1.0);
@@ -194,6 +231,5 @@ int main(int argc, char* argv[]) {
     hga_free(disc);
     std::cout << discriminative << " out of " << exported << " exported kmers are discriminative";
     std::cout.flush();
-    hga_ctx_destroy(ctx);
     return 0;
 }

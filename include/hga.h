@@ -163,6 +163,47 @@ hga_status hga_count_merge_packed(hga_ctx* ctx, const uint64_t* pieces, uint64_t
                                   uint32_t min_per_file);
 
 /* ------------------------------------------------------------------------------
+ * Multi-GPU counting inside the library (SURVEY.md §8(b) `hga_comm_init`, §8(e)).  The
+ * reference is single-process; this replaces its one jellyfish run per file with one rank per
+ * GPU, each counting a contiguous shard of every file.  One hga_ctx per rank: one process per
+ * GPU, or one thread per GPU in one process (bin/jf_occurrences --gpus N).
+ *
+ *   every rank:  hga_count_begin / hga_count_add (its shard) / hga_count_run(ctx, 1)
+ *                hga_count_exchange(ctx, min_per_file)   (collective)
+ *   then hga_count_spec_hist / _select / _select_ex / _rows / _dump / _get_stats answer for the
+ *   whole input, identically on every rank (collectives: call them on every rank, same order);
+ *   hga_count_select_device leaves each owner's sorted slice on its device and returns the global
+ *   (n, n_discriminative).  Owners hold ascending disjoint code ranges, so gathered results are
+ *   in the reference's order (JellyfishOccurrenceReader.cpp:63-135).  A later hga_count_run makes
+ *   the ctx local again until the next exchange.
+ * ------------------------------------------------------------------------------ */
+#define HGA_UNIQUE_ID_BYTES 128
+/* RCCL unique id (ncclGetUniqueId): create on one rank, hand the bytes to all ranks. */
+hga_status hga_comm_unique_id(void* id /* HGA_UNIQUE_ID_BYTES */);
+/* RCCL communicator over xGMI for this ctx's device (ncclCommInitRank; blocks until every rank
+ * joined).  Exchanges are enqueued on the ctx stream. */
+hga_status hga_comm_init(hga_ctx* ctx, const void* unique_id, int rank, int nranks);
+
+/* Host-staged transport supplied by the caller (gloo, MPI, sockets, threads of one process).
+ * alltoallv is collective: every rank calls it in the same order; send_bytes[p] bytes at send[p]
+ * go to rank p, recv_bytes[p] bytes from rank p land at recv[p] (host memory; the library stages
+ * device data).  Returns 0 on success. */
+typedef struct hga_transport {
+    void* user;
+    int (*alltoallv)(void* user, const void* const* send, const uint64_t* send_bytes, void* const* recv,
+                     const uint64_t* recv_bytes);
+} hga_transport;
+hga_status hga_comm_init_host(hga_ctx* ctx, int rank, int nranks, const hga_transport* transport);
+/* This ctx's rank and rank count (0 and 1 without a communicator). */
+hga_status hga_comm_info(hga_ctx* ctx, int* rank, int* nranks);
+hga_status hga_comm_destroy(hga_ctx* ctx);
+
+/* Owner exchange after hga_count_run(ctx, 1) on every rank: rows partitioned by canonical code,
+ * one all-to-all-v of packed row pieces (one u64 each; wide rows when they do not pack), owner
+ * merge with the per-file drop count >= min_per_file (jellyfish --bc, run_jellyfish.sh:3-6). */
+hga_status hga_count_exchange(hga_ctx* ctx, uint32_t min_per_file);
+
+/* ------------------------------------------------------------------------------
  * SDK lookup — replaces the per-read loop of ReadClusteringEngine::construct_indices
  * (src/clustering/ReadClusteringEngine.cpp:234-299).  The host keeps SDK loading
  * (src/read_clustering.cpp:18-33) and the KmerID assignment (iteration order of the
@@ -212,6 +253,20 @@ typedef struct hga_lookup_result {
     uint32_t* kci_read;
 } hga_lookup_result;
 hga_status hga_lookup_fetch(hga_ctx* ctx, const hga_lookup_result* out);
+
+/* Sharded lookup on a ctx with a communicator: every rank loads the same
+ * SDK set (hga_lookup_load), sets its contiguous ReadID range of the reads (hga_lookup_set_reads with
+ * first_read_id = the range's first ReadID, ranks in ReadID order) and runs hga_lookup_run; then
+ * hga_lookup_gather (collective) replaces the ctx's results with the whole input's index, identical
+ * on every rank: hga_lookup_get_sizes / hga_lookup_fetch describe all reads in ReadID order, and
+ * kmer_component_index is per KmerID the ranks' lists concatenated in rank order (= ascending, as
+ * ReadClusteringEngine.cpp:282-284 leaves it).  hga_connections_run then sees every read; each rank
+ * passes its own ReadIDs as pivots (categories, if any, for all reads) and hga_connections_gather
+ * (collective) joins the ranks' connections in the reference order (score descending, ties by
+ * (pivot, candidate); :331) for hga_connections_fetch.  The next hga_lookup_run returns to the rank's
+ * own reads. */
+hga_status hga_lookup_gather(hga_ctx* ctx);
+hga_status hga_connections_gather(hga_ctx* ctx, uint64_t* n);
 
 /* ------------------------------------------------------------------------------
  * HyperLogLog k-mer cardinality — replaces get_approximate_kmer_count

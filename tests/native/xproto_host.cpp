@@ -1,0 +1,341 @@
+// TEST HARNESS (not product code): the multi-GPU counting protocol of libhga
+// (hybrid-genome-assembler_amd/csrc/exchange_protocol.hpp, the same source the product compiles)
+// driven on the CPU: a host engine stands in for the device rows (plain std::map counting, the packed
+// piece format of exchange.hip restated), and the transport is the caller's hga_transport hook, as
+// with hga_comm_init_host.  tests/test_dist.py runs it with gloo at world size 2 and 3 and compares
+// with the single-process oracle.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/hga.h"
+#include "../../hybrid-genome-assembler_amd/csrc/exchange_protocol.hpp"
+
+namespace {
+
+using hga::proto::Xport;
+
+struct HostXport : Xport {
+    hga_transport t;
+    void a2a(const void* const* s, const uint64_t* sb, void* const* r, const uint64_t* rb) {
+        if (t.alltoallv(t.user, s, sb, r, rb) != 0) throw std::runtime_error("transport failed");
+    }
+    void allgather(const void* mine, uint64_t bytes, void* all) override {
+        std::vector<const void*> s(nranks, mine);
+        std::vector<void*> r(nranks);
+        std::vector<uint64_t> sz(nranks, bytes);
+        for (int p = 0; p < nranks; ++p) r[p] = static_cast<char*>(all) + p * bytes;
+        a2a(s.data(), sz.data(), r.data(), sz.data());
+    }
+    std::vector<std::vector<char>> allgatherv(const void* mine, uint64_t bytes) override {
+        std::vector<uint64_t> sz(nranks);
+        allgather(&bytes, 8, sz.data());
+        std::vector<std::vector<char>> out(nranks);
+        std::vector<const void*> s(nranks, mine);
+        std::vector<void*> r(nranks);
+        std::vector<uint64_t> sb(nranks, bytes);
+        for (int p = 0; p < nranks; ++p) {
+            out[p].resize(sz[p]);
+            r[p] = out[p].data();
+        }
+        a2a(s.data(), sb.data(), r.data(), sz.data());
+        return out;
+    }
+    void alltoallv_eng(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
+        std::vector<const void*> s(nranks);
+        std::vector<void*> r(nranks);
+        uint64_t so = 0, ro = 0;
+        for (int p = 0; p < nranks; ++p) {
+            s[p] = static_cast<const char*>(send) + so;
+            r[p] = static_cast<char*>(recv) + ro;
+            so += sb[p];
+            ro += rb[p];
+        }
+        a2a(s.data(), sb, r.data(), rb);
+    }
+};
+
+int jf_code(unsigned char c) {
+    switch (c) {
+        case 'A': case 'a': return 0;
+        case 'C': case 'c': return 1;
+        case 'G': case 'g': return 2;
+        case 'T': case 't': return 3;
+        default: return -1;
+    }
+}
+
+struct HostEngine {
+    int k_ = 0;
+    uint32_t F = 0;
+    bool allow_pack = true;
+    std::vector<uint64_t> keys;                 // ascending
+    std::vector<std::vector<uint32_t>> counts;  // per row, F counts
+    std::vector<char> sbuf, rbuf;
+
+    int k() const { return k_; }
+    uint32_t n_files() const { return F; }
+    uint64_t rows() const { return keys.size(); }
+    int pack_bits() const {
+        if (!allow_pack) return 0;
+        const int cb = (64 - 2 * k_) / (int)F;
+        return (F <= 8 && cb >= 4) ? std::min(cb, 32) : 0;
+    }
+    void* send_buf(uint64_t b) { sbuf.assign(b + 64, 0); return sbuf.data(); }
+    void* recv_buf(uint64_t b) { rbuf.assign(b + 64, 0); return rbuf.data(); }
+    void sync() {}
+    static uint32_t owner(const uint64_t* spl, uint32_t P, uint64_t key) {
+        return (uint32_t)(std::upper_bound(spl, spl + (P - 1), key) - spl);
+    }
+    void set_rows(std::map<uint64_t, std::vector<uint64_t>>& m, uint32_t min) {
+        keys.clear();
+        counts.clear();
+        for (auto& kv : m) {
+            std::vector<uint32_t> c(F);
+            bool any = false;
+            for (uint32_t f = 0; f < F; ++f) {
+                const uint64_t v = std::min<uint64_t>(kv.second[f], 0xFFFFFFFFull);
+                c[f] = v >= min ? (uint32_t)v : 0u;
+                any |= c[f] != 0;
+            }
+            if (!any) continue;
+            keys.push_back(kv.first);
+            counts.push_back(c);
+        }
+    }
+    uint64_t partition_packed(const uint64_t* spl, uint32_t P, uint64_t* out, uint64_t cap, uint64_t* per) {
+        const int cb = pack_bits();
+        const uint64_t cmax = (1ull << cb) - 1;
+        std::vector<std::vector<uint64_t>> by(P);
+        for (size_t i = 0; i < keys.size(); ++i) {
+            std::vector<uint64_t> left(counts[i].begin(), counts[i].end());
+            auto& o = by[owner(spl, P, keys[i])];
+            while (true) {
+                uint64_t v = keys[i];
+                bool more = false;
+                for (uint32_t f = 0; f < F; ++f) {
+                    const uint64_t c = std::min(left[f], cmax);
+                    left[f] -= c;
+                    more |= left[f] != 0;
+                    v |= c << (2 * k_ + f * cb);
+                }
+                o.push_back(v);
+                if (!more) break;
+            }
+        }
+        uint64_t tot = 0;
+        for (uint32_t p = 0; p < P; ++p) tot += (per[p] = by[p].size());
+        if (tot > cap) return tot;
+        for (auto& v : by)
+            for (auto x : v) *out++ = x;
+        return tot;
+    }
+    void merge_packed(const uint64_t* in, uint64_t n, uint32_t min) {
+        const int cb = pack_bits();
+        const uint64_t kmask = 2 * k_ >= 64 ? ~0ull : (1ull << (2 * k_)) - 1, cmax = (1ull << cb) - 1;
+        std::map<uint64_t, std::vector<uint64_t>> m;
+        for (uint64_t i = 0; i < n; ++i) {
+            auto& c = m.try_emplace(in[i] & kmask, std::vector<uint64_t>(F, 0)).first->second;
+            for (uint32_t f = 0; f < F; ++f) c[f] += (in[i] >> (2 * k_ + f * cb)) & cmax;
+        }
+        set_rows(m, min);
+    }
+    void partition(const uint64_t* spl, uint32_t P, uint64_t* ko, uint32_t* co, uint64_t* per) {
+        std::vector<std::vector<size_t>> by(P);
+        for (size_t i = 0; i < keys.size(); ++i) by[owner(spl, P, keys[i])].push_back(i);
+        for (uint32_t p = 0; p < P; ++p) {
+            per[p] = by[p].size();
+            for (size_t i : by[p]) {
+                *ko++ = keys[i];
+                for (uint32_t f = 0; f < F; ++f) *co++ = counts[i][f];
+            }
+        }
+    }
+    void merge(const uint64_t* ki, const uint32_t* ci, uint64_t n, uint32_t min) {
+        std::map<uint64_t, std::vector<uint64_t>> m;
+        for (uint64_t i = 0; i < n; ++i) {
+            auto& c = m.try_emplace(ki[i], std::vector<uint64_t>(F, 0)).first->second;
+            for (uint32_t f = 0; f < F; ++f) c[f] += ci[i * F + f];
+        }
+        set_rows(m, min);
+    }
+};
+
+struct Rank {
+    HostEngine e;
+    HostXport x;
+    std::vector<std::string> shard;
+};
+
+template <class T>
+T* dup(const std::vector<T>& v) {
+    T* p = (T*)std::malloc(std::max<size_t>(1, v.size() * sizeof(T)));
+    if (!v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(T));
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+void xt_free(void* p) { std::free(p); }
+
+void* xt_create(int k, int n_files, int rank, int nranks, const hga_transport* t, int allow_pack) {
+    auto* r = new Rank();
+    r->e.k_ = k;
+    r->e.F = (uint32_t)n_files;
+    r->e.allow_pack = allow_pack != 0;
+    r->x.rank = rank;
+    r->x.nranks = nranks;
+    r->x.t = *t;
+    r->shard.resize(n_files);
+    return r;
+}
+
+void xt_destroy(void* h) { delete static_cast<Rank*>(h); }
+
+void xt_add(void* h, int file, const char* seq, uint64_t n) { static_cast<Rank*>(h)->shard[file].append(seq, n); }
+
+// local count with min 1 (every canonical window of every ACGT run), then the protocol's exchange
+int xt_count_exchange(void* h, uint32_t min) {
+    auto* r = static_cast<Rank*>(h);
+    const int k = r->e.k_;
+    const uint64_t mask = k >= 32 ? ~0ull : (1ull << (2 * k)) - 1;
+    std::map<uint64_t, std::vector<uint64_t>> m;
+    for (uint32_t f = 0; f < r->e.F; ++f) {
+        uint64_t fwd = 0, rc = 0;
+        int run = 0;
+        for (unsigned char ch : r->shard[f]) {
+            const int c = jf_code(ch);
+            if (c < 0) { run = 0; fwd = rc = 0; continue; }
+            fwd = ((fwd << 2) | (uint64_t)c) & mask;
+            rc = (rc >> 2) | ((uint64_t)(3 - c) << (2 * (k - 1)));
+            if (++run >= k) m.try_emplace(std::min(fwd, rc), std::vector<uint64_t>(r->e.F, 0)).first->second[f]++;
+        }
+    }
+    r->e.set_rows(m, 1);
+    try {
+        hga::proto::count_exchange(r->e, r->x, min);
+    } catch (...) {
+        return -1;
+    }
+    return 0;
+}
+
+// global histogram: (threshold index, total, count) triples, (threshold, total) order
+int64_t xt_spec_hist(void* h, const double* thr, int n_thr, int64_t** out) {
+    auto* r = static_cast<Rank*>(h);
+    std::set<double> T(thr, thr + n_thr);
+    std::vector<double> tv(T.begin(), T.end());
+    std::map<std::pair<int64_t, int64_t>, int64_t> bins;
+    for (auto& c : r->e.counts) {
+        int64_t tot = 0, prev = 0;
+        for (auto v : c) { tot += v; prev = std::max<int64_t>(prev, v); }
+        const double x = ((double)prev / (double)tot) * 100;
+        const int64_t ti = std::upper_bound(tv.begin(), tv.end(), x) - tv.begin();
+        bins[{ti, tot}] += 1;
+    }
+    std::vector<int64_t> local;
+    for (auto& b : bins) { local.push_back(b.first.first); local.push_back(b.first.second); local.push_back(b.second); }
+    const std::vector<int64_t> g = hga::proto::spec_hist_global(r->x, local);
+    *out = dup(g);
+    return (int64_t)g.size() / 3;
+}
+
+// global export: keys ascending (owners in rank order), flags; *n_discr over all owners
+int64_t xt_select(void* h, int64_t lower, int64_t upper, uint64_t** keys, uint8_t** flags, uint64_t* n_discr) {
+    auto* r = static_cast<Rank*>(h);
+    std::vector<uint64_t> k;
+    std::vector<uint8_t> f;
+    uint64_t d = 0;
+    for (size_t i = 0; i < r->e.keys.size(); ++i) {
+        int64_t tot = 0;
+        int nz = 0;
+        for (auto v : r->e.counts[i]) { tot += v; nz += v > 0; }
+        if (lower <= tot && tot <= upper) {
+            k.push_back(r->e.keys[i]);
+            f.push_back(nz == 1);
+            d += nz == 1;
+        }
+    }
+    const auto gk = hga::proto::concat(r->x, k);
+    const auto gf = hga::proto::concat(r->x, f);
+    *n_discr = hga::proto::sum_u64(r->x, {d})[0];
+    *keys = dup(gk);
+    *flags = dup(gf);
+    return (int64_t)gk.size();
+}
+
+// global rows: keys ascending, counts row-major
+int64_t xt_rows(void* h, uint64_t** keys, uint32_t** counts) {
+    auto* r = static_cast<Rank*>(h);
+    std::vector<uint32_t> c;
+    for (auto& v : r->e.counts) c.insert(c.end(), v.begin(), v.end());
+    const auto gk = hga::proto::concat(r->x, r->e.keys);
+    const auto gc = hga::proto::concat(r->x, c);
+    *keys = dup(gk);
+    *counts = dup(gc);
+    return (int64_t)gk.size();
+}
+
+// ---- sharded categorization: construct_indices output of this rank's reads -> the whole input's
+struct XIndex {   // flat C view of proto::CsrIndex (host arrays)
+    uint64_t n, windows, reads_hit, H, U;
+    uint32_t first_read_id, n_sdk;
+    uint64_t *hit_ptr, *first_ptr, *kci_ptr;
+    uint32_t *hit_kid, *hit_pos, *sorted_kid, *first_kid, *first_pos, *kci_read;
+};
+
+int xt_index_gather(void* h, const XIndex* in, XIndex* out) {
+    auto* r = static_cast<Rank*>(h);
+    hga::proto::CsrIndex a, g;
+    a.n = in->n;
+    a.windows = in->windows;
+    a.reads_hit = in->reads_hit;
+    a.first_read_id = in->first_read_id;
+    a.n_sdk = in->n_sdk;
+    a.hit_ptr.assign(in->hit_ptr, in->hit_ptr + in->n + 1);
+    a.first_ptr.assign(in->first_ptr, in->first_ptr + in->n + 1);
+    a.kci_ptr.assign(in->kci_ptr, in->kci_ptr + in->n_sdk + 1);
+    a.hit_kid.assign(in->hit_kid, in->hit_kid + in->H);
+    a.hit_pos.assign(in->hit_pos, in->hit_pos + in->H);
+    a.sorted_kid.assign(in->sorted_kid, in->sorted_kid + in->H);
+    a.kci_read.assign(in->kci_read, in->kci_read + in->H);
+    a.first_kid.assign(in->first_kid, in->first_kid + in->U);
+    a.first_pos.assign(in->first_pos, in->first_pos + in->U);
+    if (!hga::proto::gather_index(r->x, a, g)) return -1;
+    *out = XIndex{g.n, g.windows, g.reads_hit, g.hit_kid.size(), g.first_kid.size(), g.first_read_id, g.n_sdk,
+                  dup(g.hit_ptr), dup(g.first_ptr), dup(g.kci_ptr), dup(g.hit_kid), dup(g.hit_pos),
+                  dup(g.sorted_kid), dup(g.first_kid), dup(g.first_pos), dup(g.kci_read)};
+    return 0;
+}
+
+// this rank's connections (reference order) -> the global list
+int64_t xt_merge_connections(void* h, uint64_t n, const uint32_t* x, const uint32_t* y, const uint64_t* s,
+                             const uint8_t* g, uint32_t** ox, uint32_t** oy, uint64_t** os, uint8_t** og) {
+    auto* r = static_cast<Rank*>(h);
+    hga::proto::ConnList in;
+    in.x.assign(x, x + n);
+    in.y.assign(y, y + n);
+    in.s.assign(s, s + n);
+    in.g.assign(g, g + n);
+    const hga::proto::ConnList m = hga::proto::merge_connections(r->x, in);
+    *ox = dup(m.x);
+    *oy = dup(m.y);
+    *os = dup(m.s);
+    *og = dup(m.g);
+    return (int64_t)m.x.size();
+}
+
+// splitters of the protocol (for the test of owner ranges)
+void xt_splitters(int k, int P, uint64_t* out) {
+    const auto s = hga::proto::owner_splitters(k, P);
+    std::copy(s.begin(), s.end(), out);
+}
+
+}  // extern "C"

@@ -199,3 +199,29 @@ def test_categorization_clusters_and_export(tmp_path, hga_mod, args, cfg):
         exp = "".join(f">{headers[r - 1]}\n{rec['bases'][rec['offsets'][r - 1]:rec['offsets'][r]].decode()}\n"
                       for r in members)
         assert text == exp
+
+
+@pytest.mark.parametrize("gpus,cache", [(2, False), (3, False), (2, True)])
+def test_jf_occurrences_multi_rank(tmp_path, hga_mod, gpus, cache):
+    """--gpus N: N ranks in one process (on a one-GPU box they share it through the library's host
+    transport; one rank per GPU over RCCL otherwise), each counting a share of every file, then
+    hga_count_exchange.  Export file, stdout, plot wire and the dump caches equal the oracle's, and
+    an existing cache (read on rank 0 only) is merged exactly as with one GPU."""
+    k, lower, upper = 17, 3, 12
+    paths = stage_reads(tmp_path)
+    streams = [hga_mod.jf_stream(p) for p in paths]
+    o = oracle.count_pipeline(streams, k, lower, upper)
+    if cache:   # file 0 comes from its dump cache (JellyfishOccurrenceReader.cpp:19-24)
+        open(f"{paths[0]}_{k}-mers_sorted", "w").write(dump_text(*o["dumps"][0], k))
+    env = dict(os.environ, HGA_PLOT_CMD=f"cat > {tmp_path}/wire.txt")
+    out = subprocess.run([os.path.join(BIN, "jf_occurrences"), *paths, "-k", str(k), "--gpus", str(gpus)],
+                         input=f"{lower} {upper} 1\n", text=True, capture_output=True, cwd=tmp_path, env=env,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout == ("0\nEnter lower and upper bounds for exported kmers as well as percentage\n"
+                          f"{o['n_discr']} out of {len(o['selected'])} exported kmers are discriminative")
+    assert open(tmp_path / "wire.txt").read() == expected_wire(o["hist"], k)
+    assert open(tmp_path / f"{k}-mers_{lower}_{upper}_100%.txt").read() == \
+        "".join(kmer_str(c, k) + "\n" for c in o["selected"])
+    for f in range(2):
+        assert open(f"{paths[f]}_{k}-mers_sorted").read() == dump_text(*o["dumps"][f], k)

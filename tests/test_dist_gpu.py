@@ -5,9 +5,10 @@
     the union of owner rows must equal the oracle's merged rows over all reads with the `--bc`
     drop (run_jellyfish.sh:3-6), and the per-owner histograms / exports must add up to the
     single-context results.
-(b) The product protocol (hga_dist.OwnerExchange + HgaEngine) in 2 processes sharing cuda:0,
-    collectives over gloo with host staging (RCCL needs one GPU per rank; the 8-GPU RCCL run is
-    the driver's bench)."""
+(b) The product path in the C ABI (hga_comm_init_host + hga_count_exchange, set up by
+    hga_dist.OwnerExchange) in 2 and 3 processes sharing cuda:0, the library's transport hook over
+    gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run is the driver's bench): every rank's
+    global rows, dumps, histogram, export and stats equal the single-process oracle."""
 import socket
 
 import numpy as np
@@ -92,40 +93,52 @@ def test_partition_merge_min_counts_and_empty_owner():
     assert np.array_equal(keys, rk) and np.array_equal(counts, rc)
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, k):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     ctx = hga.Ctx(0)
     try:
         streams = make_streams()
-        ctx.count_begin(13, len(streams))
+        ctx.count_begin(k, len(streams))
         for f, s in enumerate(streams):
             ctx.count_add(f, hga_dist.shard_reads(s, rank, world))
-        ex = hga_dist.OwnerExchange(hga_dist.HgaEngine(ctx, 13, len(streams), "cuda:0"))
+        ex = hga_dist.OwnerExchange(ctx)
+        assert ctx.comm_info() == (rank, world)
         ex.count(2)
         hist = ex.spec_hist(THR)
         keys, flags = ex.select(3, 40)
         n, d = ex.select_counts(3, 40)
-        if rank == 0:
-            np.savez(out_path, hist=hist, keys=keys, flags=flags, n=n, d=d)
+        rk, rc = ctx.rows()
+        d0 = ctx.dump(0)
+        st = ctx.count_stats()
+        np.savez(out_path + f".{rank}.npz", hist=hist, keys=keys, flags=flags, n=n, d=d, rk=rk, rc=rc, d0k=d0[0],
+                 d0c=d0[1], inst=st.instances, rows=st.distinct_rows)
     finally:
         ctx.close()
         dist.destroy_process_group()
 
 
-def test_owner_exchange_two_processes(tmp_path):
+@pytest.mark.parametrize("world,k", [(2, 13), (3, 27)])
+def test_count_exchange_processes(tmp_path, world, k):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    out = str(tmp_path / "d.npz")
-    mp.start_processes(_worker, args=(2, port, out), nprocs=2, start_method="spawn")
-    r = np.load(out)
-    ref = oracle.count_pipeline(make_streams(), 13, 3, 40)
-    assert np.array_equal(r["hist"], ref["hist"])
-    assert np.array_equal(r["keys"], ref["selected"])
-    assert int(r["n"]) == len(ref["selected"]) and int(r["d"]) == ref["n_discr"]
+    out = str(tmp_path / "d")
+    mp.start_processes(_worker, args=(world, port, out, k), nprocs=world, start_method="spawn")
+    streams = make_streams()
+    ref = oracle.count_pipeline(streams, k, 3, 40)
+    inst = sum(oracle.count_instances(x, k) for x in streams)
+    for rank in range(world):
+        r = np.load(out + f".{rank}.npz")
+        assert np.array_equal(r["hist"], ref["hist"])
+        assert np.array_equal(r["keys"], ref["selected"])
+        assert int(r["flags"].sum()) == ref["n_discr"]
+        assert int(r["n"]) == len(ref["selected"]) and int(r["d"]) == ref["n_discr"]
+        assert np.array_equal(r["rk"], ref["keys"]) and np.array_equal(r["rc"], ref["counts"])
+        assert np.array_equal(r["d0k"], ref["dumps"][0][0]) and np.array_equal(r["d0c"], ref["dumps"][0][1])
+        assert int(r["inst"]) == inst and int(r["rows"]) == len(ref["keys"])
 
 
 def _sim_packed(streams, k, G, min_c):
@@ -233,3 +246,57 @@ def test_merge_packed_many_pieces(skew, one_pass, monkeypatch):
         c.close()
     assert np.array_equal(kk, u[keep])
     assert np.array_equal(cc.reshape(-1, F).astype(np.int64), tot[keep])
+
+
+def _lk_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    from test_dist import lookup_case
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ctx = hga.Ctx(0)
+    try:
+        hga_dist.attach(ctx)
+        reads, sdk = lookup_case()
+        a, b = len(reads) * rank // world, len(reads) * (rank + 1) // world
+        mine = reads[a:b]
+        ctx.lookup_load(13, sdk)
+        ctx.lookup_set_reads(b"".join(mine), np.cumsum([0] + [len(r) for r in mine]).astype(np.uint64), 1 + a)
+        ctx.lookup_run()
+        ctx.lookup_gather()
+        got = ctx.lookup_fetch()
+        sz = ctx.lookup_sizes()
+        cat = (np.arange(len(reads)) % 3).astype(np.int32)
+        ctx.connections_run(pivots=np.arange(1 + a, 1 + b, dtype=np.uint32), min_score=2, categories=cat)
+        n = ctx.connections_gather()
+        x, y, s, g = (np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint8))
+        hga.lib().hga_connections_fetch(ctx._h, x.ctypes.data_as(hga._u32p), y.ctypes.data_as(hga._u32p),
+                                        s.ctypes.data_as(hga._u64p), g.ctypes.data_as(hga._u8p))
+        np.savez(out_path + f".{rank}.npz", x=x, y=y, s=s, g=g, n_reads=sz.n_reads, hits=sz.hits, **got)
+        ctx.lookup_run()   # back to this rank's own reads
+        assert ctx.lookup_sizes().n_reads == len(mine)
+    finally:
+        ctx.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_lookup_gather_and_connections(tmp_path, world):
+    """SURVEY.md §8(e) row 2 through the C ABI: each rank looks up its contiguous ReadID range,
+    hga_lookup_gather builds the whole input's index on every rank, each rank's pivots are connected
+    over it and hga_connections_gather joins them: equal to the single-process oracle
+    (construct_indices, ReadClusteringEngine.cpp:234-299; get_connections, :301-333)."""
+    import torch.multiprocessing as mp
+    from test_dist import _free_port, lookup_case
+    out = str(tmp_path / "lk")
+    mp.start_processes(_lk_worker, args=(world, _free_port(), out), nprocs=world, start_method="spawn")
+    reads, sdk = lookup_case()
+    offs = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    ref = oracle.construct_indices(b"".join(reads), offs, 13, sdk, first_read_id=1)
+    cat = (np.arange(len(reads)) % 3).astype(np.int32)
+    rx, ry, rs, rg = oracle.connections(ref, min_score=2, categories=cat)
+    for rank in range(world):
+        r = np.load(out + f".{rank}.npz")
+        assert int(r["n_reads"]) == len(reads) and int(r["hits"]) == len(ref["hit_kid"])
+        for name in ref:
+            assert np.array_equal(r[name], ref[name]), name
+        assert np.array_equal(r["x"], rx) and np.array_equal(r["y"], ry)
+        assert np.array_equal(r["s"], rs) and np.array_equal(r["g"], rg)
