@@ -90,8 +90,7 @@ void comm_allgather(hga_ctx* c, const void* mine, uint64_t bytes, void* all) {
         m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
         return;
     }
-    DevBuf d;
-    char* ds = static_cast<char*>(d.ensure(bytes * (P + 1) + 16));
+    char* ds = static_cast<char*>(m.stage.ensure(bytes * (P + 1) + 16));
     HGA_HIP(hipMemcpyAsync(ds, mine, bytes, hipMemcpyHostToDevice, c->stream));
     for (int p = 0; p < P; ++p) {
         sp[p] = ds;
@@ -123,8 +122,7 @@ std::vector<std::vector<char>> comm_allgatherv(hga_ctx* c, const void* mine, uin
     }
     uint64_t tot = 0;
     for (auto v : sz) tot += v;
-    DevBuf d;
-    char* ds = static_cast<char*>(d.ensure(bytes + tot + 16));
+    char* ds = static_cast<char*>(m.stage.ensure(bytes + tot + 16));
     if (bytes) HGA_HIP(hipMemcpyAsync(ds, mine, bytes, hipMemcpyHostToDevice, c->stream));
     uint64_t o = bytes;
     for (int p = 0; p < P; ++p) {

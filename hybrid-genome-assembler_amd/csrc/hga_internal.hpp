@@ -174,6 +174,7 @@ struct ConnState {
 // Multi-GPU transport of one rank (comm.hip): RCCL over xGMI, or a caller's host-staged hook.
 struct Comm {
     int rank = 0, nranks = 1;
+    DevBuf stage;   // device staging of host-memory collectives over RCCL (grow-only: no hipMalloc per call)
     virtual ~Comm() = default;
     // true: alltoallv moves device memory (RCCL); false: host memory (the caller stages)
     virtual bool on_device() const = 0;
