@@ -16,6 +16,11 @@
 // lookup's device-resident indices), union-find, merging, spanning-tree tails, spectral
 // clustering and the per-component FASTA/FASTQ export with the reference's timing lines.
 // With --index-out <path> the constructed index is also written as a binary file.
+//
+// --gpus N (extension, default 1): N ranks in this process, one per GPU
+// (ranks.h).  Every rank loads the whole SDK set and looks up a contiguous ReadID range of the
+// reads; hga_lookup_gather gives every rank the whole input's index; the device connection pass
+// splits its pivots over the ranks and hga_connections_gather joins them in the reference order.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +35,7 @@
 #include "args.h"
 #include "clustering.h"
 #include "hga.h"
+#include "ranks.h"
 #include "seqio.h"
 
 namespace {
@@ -84,6 +90,9 @@ int main(int argc, char* argv[]) {
     ap.add("threads", 't', false, "Number of threads to use", [&](const std::string& v) { threads = std::stoi(v); });
     ap.add("index-out", 0, false, "Write the constructed index (binary) to this path",
            [&](const std::string& v) { index_out = v; });
+    int gpus = 1;
+    ap.add("gpus", 0, false, "GPUs for the lookup and the first connection pass, one rank each (MI355X build "
+           "extension; default 1)", [&](const std::string& v) { gpus = std::stoi(v); });
     ap.parse(argc, argv);
     for (auto& p : ap.positional) read_paths.push_back(p);
     if (ap.has("help")) {
@@ -102,12 +111,22 @@ int main(int argc, char* argv[]) {
     const bool engine_debug = rs.file_meta.size() == rs.categories;   // ReadClusteringEngine.cpp:229
 
     const char* dev_env = std::getenv("HGA_DEVICE");
-    hga_ctx* ctx = nullptr;
-    check(hga_ctx_create(&ctx, dev_env ? std::atoi(dev_env) : 0), "hga_ctx_create");
+    hgah::Ranks ranks(gpus, dev_env ? std::atoi(dev_env) : 0);
+    hga_ctx* ctx = ranks.ctx[0];
+    const int P = ranks.size();
+    const uint64_t n_reads = rs.size();
+    auto share = [&](int r) { return std::make_pair(n_reads * (uint64_t)r / P, n_reads * (uint64_t)(r + 1) / P); };
     const auto t0 = std::chrono::steady_clock::now();
-    check(hga_lookup_load(ctx, k, kk.first.data(), (uint32_t)kk.first.size()), "hga_lookup_load");
-    check(hga_lookup_set_reads(ctx, rs.bases.data(), rs.offsets.data(), rs.size(), 1), "hga_lookup_set_reads");
-    check(hga_lookup_run(ctx), "hga_lookup_run");
+    ranks.each([&](int r, hga_ctx* c) {   // rank r: the whole SDK set, its contiguous ReadID range
+        const auto [a, b] = share(r);
+        std::vector<uint64_t> offs(rs.offsets.begin() + (int64_t)a, rs.offsets.begin() + (int64_t)b + 1);
+        for (auto& o : offs) o -= rs.offsets[a];
+        check(hga_lookup_load(c, k, kk.first.data(), (uint32_t)kk.first.size()), "hga_lookup_load");
+        check(hga_lookup_set_reads(c, rs.bases.data() + rs.offsets[a], offs.data(), b - a, (uint32_t)(1 + a)),
+              "hga_lookup_set_reads");
+        check(hga_lookup_run(c), "hga_lookup_run");
+        if (P > 1) check(hga_lookup_gather(c), "hga_lookup_gather");   // every rank: the whole index
+    });
     hga_lookup_sizes sz;
     check(hga_lookup_get_sizes(ctx, &sz), "hga_lookup_get_sizes");
     std::vector<uint64_t> hit_ptr(sz.n_reads + 1), first_ptr(sz.n_reads + 1), kci_ptr((size_t)sz.n_sdk + 1);
@@ -162,8 +181,38 @@ int main(int argc, char* argv[]) {
     hgah::ClusteringEngine engine(cfg, engine_debug, rs, 1, std::move(hit_ptr), std::move(sorted_kid),
                                   std::move(first_ptr), std::move(first_kid), std::move(first_pos), kci_ptr, kci_read,
                                   ctx);
+    if (P > 1) {   // the device connection pass with the pivots split over the ranks
+        std::vector<int32_t> cats;
+        if (engine_debug) cats.assign(rs.category.begin(), rs.category.end());
+        engine.set_device_connections([&](const std::vector<hgah::ComponentID>& pivots, hgah::Score min_score,
+                                          uint32_t min_kmers) {
+            std::vector<uint64_t> ns(P, 0);
+            ranks.each([&](int r, hga_ctx* c) {
+                std::vector<uint32_t> piv;
+                if (min_kmers > 0) {   // "every read with >= min_kmers KmerIDs": this rank's ReadID range
+                    const auto [a, b] = share(r);
+                    for (uint64_t i = a; i < b; ++i) piv.push_back((uint32_t)(1 + i));
+                } else {
+                    piv.assign(pivots.begin() + (int64_t)(pivots.size() * r / P),
+                               pivots.begin() + (int64_t)(pivots.size() * (r + 1) / P));
+                }
+                uint64_t n = 0;
+                uint32_t none = 0;   // an empty list is not NULL (NULL would mean every read)
+                check(hga_connections_run(c, piv.empty() ? &none : piv.data(), piv.size(), min_kmers > 0 ? min_kmers : 1, min_score,
+                                          engine_debug ? cats.data() : nullptr, &n), "hga_connections_run");
+                check(hga_connections_gather(c, &ns[r]), "hga_connections_gather");
+            });
+            const uint64_t n = ns[0];
+            std::vector<uint32_t> x(n), y(n);
+            std::vector<uint64_t> sc(n);
+            std::vector<uint8_t> g(n);
+            check(hga_connections_fetch(ctx, x.data(), y.data(), sc.data(), g.data()), "hga_connections_fetch");
+            std::vector<hgah::Connection> out(n);
+            for (uint64_t i = 0; i < n; ++i) out[i] = {x[i], y[i], sc[i], g[i] != 0};
+            return out;
+        });
+    }
     const std::vector<hgah::ComponentID> cluster_ids = engine.run(std::cout);   // run_clustering (:699-802)
     engine.export_components(cluster_ids, output_folder_path, std::cout);       // read_clustering.cpp:82
-    hga_ctx_destroy(ctx);
     return 0;
 }

@@ -531,8 +531,12 @@ std::vector<Connection> ClusteringEngine::host_connections(const std::vector<Com
 
 std::vector<Connection> ClusteringEngine::get_connections(const std::vector<ComponentID>& pivots, Score min_score,
                                                           uint32_t min_kmers) {
-    if (!(pristine_ && gpu_)) return host_connections(pivots, min_score);
+    if (!(pristine_ && (gpu_ || dev_conn_))) return host_connections(pivots, min_score);
     if (min_kmers == 0 && pivots.empty()) return {};   // (a null pivot list means "every read" there)
+    if (dev_conn_) {
+        ++gpu_calls_;
+        return dev_conn_(pivots, min_score, min_kmers);
+    }
     // construct_indices' state is on the device: hga_connections_run (connect.hip)
     std::vector<int32_t> cats;
     if (debug_) cats.assign(reads_.category.begin(), reads_.category.end());
@@ -553,7 +557,7 @@ std::vector<Connection> ClusteringEngine::get_connections(const std::vector<Comp
 }
 
 std::vector<Connection> ClusteringEngine::get_all_connections(Score min_score) {   // :335-339
-    if (pristine_ && gpu_) return get_connections({}, min_score, 1);
+    if (pristine_ && (gpu_ || dev_conn_)) return get_connections({}, min_score, 1);
     std::vector<ComponentID> ids;
     for (auto& kv : index_) ids.push_back(kv.first);
     return host_connections(ids, min_score);

@@ -28,6 +28,7 @@
 #include <set>
 #include <string>
 #include <utility>
+#include <functional>
 #include <vector>
 
 #include "hga.h"
@@ -106,6 +107,11 @@ class ClusteringEngine {
     const std::map<ComponentID, Component>& components() const { return index_; }
     const std::vector<std::vector<ComponentID>>& kmer_component_index() const { return kci_; }
     bool used_gpu() const { return gpu_calls_ > 0; }
+    // Device connection pass over several ranks (categorization --gpus N): fn(pivots or empty for
+    // "every read", min_score, min_kmers) -> connections in the reference order; replaces the
+    // single-ctx call while the device indices describe the state.
+    using DeviceConnections = std::function<std::vector<Connection>(const std::vector<ComponentID>&, Score, uint32_t)>;
+    void set_device_connections(DeviceConnections fn) { dev_conn_ = std::move(fn); }
 
    private:
     std::vector<KmerID> accumulate_kmer_ids(const std::vector<ComponentID>& ids) const;
@@ -128,6 +134,7 @@ class ClusteringEngine {
     std::map<ComponentID, Component> index_;
     std::vector<std::vector<ComponentID>> kci_;
     hga_ctx* gpu_;
+    DeviceConnections dev_conn_;
     bool pristine_ = true;   // no merge yet: the device indices still describe the state
     int gpu_calls_ = 0;
 };

@@ -225,3 +225,33 @@ def test_jf_occurrences_multi_rank(tmp_path, hga_mod, gpus, cache):
         "".join(kmer_str(c, k) + "\n" for c in o["selected"])
     for f in range(2):
         assert open(f"{paths[f]}_{k}-mers_sorted").read() == dump_text(*o["dumps"][f], k)
+
+
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_categorization_multi_rank_equals_one(tmp_path, hga_mod, gpus):
+    """categorization --gpus N (sharded lookup + hga_lookup_gather, the device connection pass split
+    over the ranks + hga_connections_gather): the index file, the printed lines (timings aside) and the
+    exported clusters equal the one-GPU run's."""
+    k = 15
+    ga = hga_mod.gen_genome(40_000, 5)
+    gb = hga_mod.gen_haplotype(ga, 0.02, 0, 6)
+    paths = [str(tmp_path / "hapA.fa"), str(tmp_path / "hapB.fa")]
+    hga_mod.write_nanosim_fasta(ga, "hapA", 180, 7, paths[0])
+    hga_mod.write_nanosim_fasta(gb, "hapB", 180, 8, paths[1])
+    ka, _ = oracle.kmer_windows(ga, k)
+    kb, _ = oracle.kmer_windows(gb, k)
+    sdk = np.setxor1d(np.unique(ka), np.unique(kb))
+    (tmp_path / "sdk.txt").write_text("".join(kmer_str(c, k) + "\n" for c in sdk))
+    res = {}
+    for g in (1, gpus):
+        out = subprocess.run([os.path.join(BIN, "categorization"), *paths, "-k", str(tmp_path / "sdk.txt"), "-d",
+                              "-o", str(tmp_path / f"cl{g}"), "--index-out", str(tmp_path / f"idx{g}.bin"),
+                              "--sc_min_size", "5", "--core_enrichment", "8", "--tail_amplification", "10",
+                              "--gpus", str(g)], capture_output=True, text=True, cwd=tmp_path, timeout=300)
+        assert out.returncode == 0, out.stderr
+        lines = [l for l in out.stdout.splitlines() if " took " not in l]
+        files = {f: open(tmp_path / f"cl{g}" / f).read() for f in sorted(os.listdir(tmp_path / f"cl{g}"))}
+        res[g] = (lines, files, open(tmp_path / f"idx{g}.bin", "rb").read())
+    assert res[1][2] == res[gpus][2]
+    assert res[1][0] == res[gpus][0]
+    assert res[1][1] == res[gpus][1] and len(res[1][1]) > 1
