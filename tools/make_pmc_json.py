@@ -11,16 +11,29 @@ import re
 import sys
 
 
+GATHER = {"lk_scan", "cn_wave", "cn_local", "cn_global", "cn_gather", "kx_mb_merge", "lk_first_count",
+          "lk_first_write", "lk_wsort", "lk_segsort"}
+
+
 def main(src, out_dir):
     d = json.load(open(src))
     os.makedirs(out_dir, exist_ok=True)
     for k, row in d.items():
-        base = re.sub(r"<.*", "", k)
-        rd, wr = row["read_bytes_corr"], row["write_bytes"]
+        base = re.sub(r"<.*", "", k).strip()
+        if not re.match(r"^[A-Za-z_][A-Za-z0-9_]*$", base):
+            continue   # not a kernel label this tool can name a file after
+        # MI355X_MICROARCH.md establishes the x2 FETCH_SIZE correction for wide coalesced streaming
+        # reads only; random gathers (table probes, index walks) are reported raw
+        gather = base in GATHER
+        rd = row["read_bytes_corr"] / 2 if gather else row["read_bytes_corr"]
+        wr = row["write_bytes"]
         rec = {"kernel": k, "hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
+               "fetch_size_raw_bytes": int(row["read_bytes_corr"] / 2), "read_access": "gather" if gather else "stream",
                "ms_median": row["ms_median"], "dispatches": row["dispatches"],
-               "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KB->B, mean over dispatches; "
-                       "separate --pmc passes over tools/kprof.py (MI355X_MICROARCH.md HBM section)"}
+               "note": ("FETCH_SIZE raw (random gathers: the x2 correction is not established for them)" if gather else
+                        "FETCH_SIZE x2 (gfx950 wide streaming-read correction)") +
+                       " + WRITE_SIZE, KB->B, mean over dispatches; separate --pmc passes over tools/kprof.py "
+                       "(MI355X_MICROARCH.md HBM section)"}
         name = f"pmc_{base}.json"
         p = os.path.join(out_dir, name)
         # keep the heaviest instantiation when a template kernel has several

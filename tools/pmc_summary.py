@@ -16,8 +16,14 @@ import sys
 
 
 def kname(full):
-    m = re.search(r"\b((?:kc|lk|rs|sc|cn|hll)_[A-Za-z0-9_]+|pack_kernel)(<[^>]*>)?", full)
-    return (m.group(1) + (m.group(2) or "")) if m else full.split("(")[0][:40]
+    """Kernel label: the function name without namespaces, keeping template arguments
+    (e.g. 'hga::(anonymous namespace)::kx_mb_merge<2048, 2>(...)' -> 'kx_mb_merge<2048, 2>')."""
+    m = re.search(r"\b((?:kc|lk|rs|sc|cn|hll|kx|ss)_[A-Za-z0-9_]+|pack_kernel)(<[^>]*>)?", full)
+    if m:
+        return m.group(1) + (m.group(2) or "")
+    head = full.split("(")[0]
+    head = re.sub(r"\(anonymous namespace\)::", "", head)
+    return re.sub(r"^.*::", "", head)[:40] or full[:40]
 
 
 def main(dirs, out=None):
