@@ -16,6 +16,9 @@ xGMI for backend nccl, the host transport hook otherwise; hga_dist.attach):
            (hga_lookup_run), hga_lookup_gather -> the whole index on every rank;
   graph    each rank connects its own reads (hga_connections_run, min_score 1) over the whole index,
            hga_connections_gather joins them (get_all_connections, ReadClusteringEngine.cpp:335-339).
+Timed per k (barrier + device sync on both sides): the uploads of the short reads (hga_count_add) and
+of the SDK table + long reads (hga_lookup_load / hga_lookup_set_reads) separately from the three device
+stages count (run, exchange, histogram, export), lookup (run + gather) and graph.
 Synthetic data (no simulators offline): genome i.i.d. ACGT, haplotype B with d = 0.001 substitutions;
 reads from host/gen.cpp's ART-like / Nanosim-like generators, each rank drawing its
 own share with its own seeds.  Rank 0 prints one JSON line with per-k stage times (max over ranks).
@@ -108,10 +111,13 @@ def run(rank, world, args, group_ready=False):
         return r, time.perf_counter() - t0
 
     for k in args.ks:
-        def count():
+        def upload_short():
             ctx.count_begin(k, 2)
             for f in range(2):
                 ctx.count_add(f, art[f].seq)
+        _, t_up_short = timed(upload_short)
+
+        def count():
             if world > 1:
                 ctx.count_run(1)
                 ctx.count_exchange(2)
@@ -123,9 +129,12 @@ def run(rank, world, args, group_ready=False):
         (hist, sdk, nd), t_count = timed(count)
         st = ctx.count_stats()
 
-        def lookup():
+        def upload_long():
             ctx.lookup_load(k, sdk)
             ctx.lookup_set_reads(lr_bases, lr_offsets, first_id)
+        _, t_up_long = timed(upload_long)
+
+        def lookup():
             ctx.lookup_run()
             if world > 1:
                 ctx.lookup_gather()
@@ -140,9 +149,13 @@ def run(rank, world, args, group_ready=False):
         n_conn, t_graph = timed(graph)
         out["per_k"][k] = {"instances": int(st.instances), "distinct_rows": int(st.distinct_rows),
                            "exported": int(len(sdk)), "discriminative": int(nd),
+                           "upload_short_reads_s": round(t_up_short, 4),
                            "count_s": round(t_count, 4), "k_mers_per_s": round(st.instances / t_count, 1),
                            "long_reads": int(sz.n_reads), "windows": int(sz.windows), "hits": int(sz.hits),
-                           "lookup_s": round(t_lookup, 4), "connections": int(n_conn), "graph_s": round(t_graph, 4)}
+                           "upload_long_reads_and_sdk_s": round(t_up_long, 4),
+                           "lookup_s": round(t_lookup, 4), "windows_per_s": round(sz.windows / t_lookup, 1),
+                           "connections": int(n_conn), "graph_s": round(t_graph, 4),
+                           "pipeline_device_s": round(t_count + t_lookup + t_graph, 4)}
         if args.check:
             checks[k] = {"hist": hist, "sdk": sdk, "nd": nd, "idx": ctx.lookup_fetch(), "conn": _fetch_conn(ctx, n_conn)}
         log(f"[rank {rank}] k={k}: {out['per_k'][k]}")
