@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -41,13 +42,16 @@ struct RcclComm : Comm {
     bool on_device() const override { return true; }
     void alltoallv(hga_ctx* c, const void* const* send, const uint64_t* sb, void* const* recv,
                    const uint64_t* rb) override {
-        if (sb[rank]) {
+        // HGA_RCCL_SELF (test hook, read per call): the rank's own slice also goes through
+        // ncclSend/ncclRecv, so a one-GPU box exercises the grouped point-to-point calls
+        const bool self_p2p = std::getenv("HGA_RCCL_SELF") != nullptr;
+        if (sb[rank] && !self_p2p) {
             HGA_REQUIRE(rb[rank] == sb[rank], HGA_ERR_COMM, "alltoallv: self sizes disagree");
             HGA_HIP(hipMemcpyAsync(recv[rank], send[rank], sb[rank], hipMemcpyDeviceToDevice, c->stream));
         }
         HGA_NCCL(ncclGroupStart());
         for (int p = 0; p < nranks; ++p) {
-            if (p == rank) continue;
+            if (p == rank && !self_p2p) continue;
             if (sb[p]) HGA_NCCL(ncclSend(send[p], sb[p], ncclUint8, p, comm, c->stream));
             if (rb[p]) HGA_NCCL(ncclRecv(recv[p], rb[p], ncclUint8, p, comm, c->stream));
         }

@@ -1,0 +1,70 @@
+"""The RCCL transport of the C ABI (hga_comm_init, comm.hip RcclComm) on the one GPU a test box has.
+
+RCCL refuses two ranks on one device ("Duplicate GPU detected"), so the multi-rank protocol is
+tested over the host transport hook (test_dist_gpu.py) and the 8-GPU RCCL run belongs to the
+driver's scaling bench.  Here a one-rank RCCL communicator runs the same C entry points:
+ncclGetUniqueId / ncclCommInitRank, the device staging of the host-memory collectives, and — with
+HGA_RCCL_SELF — the rank's own slice through grouped ncclSend / ncclRecv on the ctx stream.  Every
+result must equal the single-process oracle (run_jellyfish.sh:3-6, JellyfishOccurrenceReader.cpp:
+63-135, ReadClusteringEngine.cpp:234-339)."""
+import numpy as np
+import pytest
+
+import hga
+import oracle
+from test_dist import lookup_case, make_streams
+
+pytestmark = pytest.mark.gpu
+THR = oracle.THRESHOLDS
+
+
+@pytest.mark.parametrize("self_p2p", [False, True])
+@pytest.mark.parametrize("k", [13, 27])
+def test_rccl_one_rank_count_exchange(monkeypatch, self_p2p, k):
+    if self_p2p:
+        monkeypatch.setenv("HGA_RCCL_SELF", "1")
+    streams = make_streams()
+    ref = oracle.count_pipeline(streams, k, 3, 40)
+    with hga.Ctx(0) as ctx:
+        ctx.comm_init(hga.comm_unique_id(), 0, 1)
+        assert ctx.comm_info() == (0, 1)
+        ctx.count_begin(k, len(streams))
+        for f, s in enumerate(streams):
+            ctx.count_add(f, s)
+        ctx.count_run(1)
+        ctx.count_exchange(2)
+        assert np.array_equal(ctx.spec_hist(THR), ref["hist"])
+        keys, flags, nd = ctx.select(3, 40)
+        assert np.array_equal(keys, ref["selected"]) and nd == ref["n_discr"]
+        rk, rc = ctx.rows()
+        assert np.array_equal(rk, ref["keys"]) and np.array_equal(rc, ref["counts"])
+        d0 = ctx.dump(0)
+        assert np.array_equal(d0[0], ref["dumps"][0][0]) and np.array_equal(d0[1], ref["dumps"][0][1])
+        ctx.comm_destroy()
+
+
+@pytest.mark.parametrize("self_p2p", [False, True])
+def test_rccl_one_rank_lookup_and_connections_gather(monkeypatch, self_p2p):
+    if self_p2p:
+        monkeypatch.setenv("HGA_RCCL_SELF", "1")
+    reads, sdk = lookup_case()
+    offs = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    ref = oracle.construct_indices(b"".join(reads), offs, 13, sdk, first_read_id=1)
+    cat = (np.arange(len(reads)) % 3).astype(np.int32)
+    rx, ry, rs, rg = oracle.connections(ref, min_score=2, categories=cat)
+    with hga.Ctx(0) as ctx:
+        ctx.comm_init(hga.comm_unique_id(), 0, 1)
+        ctx.lookup_load(13, sdk)
+        ctx.lookup_set_reads(b"".join(reads), offs, 1)
+        ctx.lookup_run()
+        ctx.lookup_gather()
+        got = ctx.lookup_fetch()
+        for name in ref:
+            assert np.array_equal(got[name], ref[name]), name
+        ctx.connections_run(pivots=np.arange(1, 1 + len(reads), dtype=np.uint32), min_score=2, categories=cat)
+        n = ctx.connections_gather()
+        x, y, s, g = (np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint8))
+        hga.lib().hga_connections_fetch(ctx._h, x.ctypes.data_as(hga._u32p), y.ctypes.data_as(hga._u32p),
+                                        s.ctypes.data_as(hga._u64p), g.ctypes.data_as(hga._u8p))
+        assert np.array_equal(x, rx) and np.array_equal(y, ry)
+        assert np.array_equal(s, rs) and np.array_equal(g, rg)
