@@ -81,7 +81,9 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
-        if self.world > 1:
+        # HGA_BENCH_FORCE_DIST=1 (under torchrun): the N>1 code path at one rank — the library's
+        # RCCL communicator, the exchange and the global queries — on a one-GPU box
+        if self.world > 1 or os.environ.get("HGA_BENCH_FORCE_DIST") == "1":
             import torch
             import torch.distributed as dist
             # HGA_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks
@@ -445,7 +447,7 @@ def main():
     ctx.count_add(0, ra.seq)
     ctx.count_add(1, rb.seq)
     ex = None
-    if D.world > 1:
+    if D.pg:
         import hga_dist
         ex = hga_dist.OwnerExchange(ctx)   # the library's RCCL communicator (hga_comm_init)
     step = (lambda: dist_count_step(ex)) if ex else (lambda: count_step(ctx))
