@@ -7,7 +7,7 @@
 //                 starts inside (start, end].
 //   lk_build      read-only table {canonical code -> KmerID}, 5 keys + 5 ids per 64-B bucket,
 //                 and a minimizer-blocked Bloom filter (16-B block per minimizer, 3 bits per
-//                 key in one word, 2 MiB at C3) small enough to stay in every XCD's L2.
+//                 key in one word; a power of two of >= 11 bits per key: 4 MiB at C3, mostly L2/MALL-resident).
 //                 KmerIDs come from the host (std::unordered_set order,
 //                 ReadClusteringEngine.cpp:237-241).
 //   lk_scan<0>    32 window ends per thread from packed frames: closed-form canonical codes,
