@@ -90,18 +90,36 @@ __device__ __forceinline__ uint32_t mmer_hash(uint64_t canon_m) {
 __device__ __forceinline__ uint64_t filter_word(uint32_t minh, uint64_t h, uint64_t fmask) {
     return ((((uint64_t)minh) << 2) | ((h >> 56) & 3u)) & fmask;
 }
-// Build side: the minimizer hash of canonical k-mer x.
-__device__ __forceinline__ uint32_t key_minimizer(uint64_t x, int k, int km) {
+// Build side: the minimizer hash of canonical k-mer x (and the xor of its first and last
+// m-mer hashes, see end_mix).
+__device__ __forceinline__ uint32_t key_minimizer(uint64_t x, int k, int km, uint32_t* ends = nullptr) {
     const int m = k - km;
     const uint64_t mm = m >= 32 ? ~0ull : ((1ull << (2 * m)) - 1);
-    uint32_t best = 0xFFFFFFFFu;
+    uint32_t best = 0xFFFFFFFFu, e = 0;
     for (int i = 0; i <= km; ++i) {
         const uint64_t fm = (x >> (2 * (km - i))) & mm;
         const uint64_t rm = revcomp_code(fm, m);
         const uint32_t hh = mmer_hash(fm < rm ? fm : rm);
         best = hh < best ? hh : best;
+        if (i == 0 || i == km) e ^= hh;
     }
+    if (ends) *ends = e;
     return best;
+}
+
+// Filter word and bits of a k-mer inside its minimizer block (km > 0): from the hashes
+// of the k-mer's first and last canonical m-mers, which a strand flip swaps, so their xor is a
+// function of the canonical k-mer — the scan has both in registers already (the minimizer pass), so
+// a window costs one 32-bit multiply instead of the 64-bit k-mer hash (lk_scan<0> 1.87 -> 1.81 ms at
+// C3); the canonical code is formed only for the windows that pass.
+__device__ __forceinline__ uint32_t end_mix(uint32_t e) {
+    return (e ^ (e >> 16)) * 0x9E3779B1u;
+}
+__device__ __forceinline__ uint32_t end_bits(uint32_t x) {   // bits 15..29: three bits of the word
+    return (1u << ((x >> 15) & 31)) | (1u << ((x >> 20) & 31)) | (1u << ((x >> 25) & 31));
+}
+__device__ __forceinline__ uint64_t end_word(uint32_t minh, uint32_t x, uint64_t fmask) {
+    return ((((uint64_t)minh) << 2) | (x >> 30)) & fmask;
 }
 
 __global__ void lk_fill(Bucket* __restrict__ t, uint64_t nbk) {
@@ -116,7 +134,14 @@ __global__ void lk_build(const uint64_t* __restrict__ keys, uint32_t n, Bucket* 
     if (i >= n) return;
     const uint64_t key = keys[i];
     const uint64_t h = tab_hash(key);
-    atomicOr(&filt[filter_word(key_minimizer(key, k, km), h, fmask)], bloom_bits(h));
+    if (km > 0) {
+        uint32_t e;
+        const uint32_t mz = key_minimizer(key, k, km, &e);
+        const uint32_t x = end_mix(e);
+        atomicOr(&filt[end_word(mz, x, fmask)], end_bits(x));
+    } else {
+        atomicOr(&filt[filter_word(key_minimizer(key, k, km), h, fmask)], bloom_bits(h));
+    }
     uint64_t b = bucket_of(h, nbk);
     while (true) {
         for (int s = 0; s < BKT; ++s) {
@@ -317,13 +342,20 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
                     blk = filt4[bi];
                     cur = bi;
                 }
-                const uint64_t key = lk_canon(f, j, mask);
-                const uint64_t h = tab_hash(key);
-                const uint32_t sel = (uint32_t)(h >> 56) & 3u;
+                uint32_t sel, bb;
+                if constexpr (KM > 0) {
+                    const uint32_t x = end_mix(mh[j] ^ mh[j + KM]);
+                    sel = x >> 30;
+                    bb = end_bits(x);
+                } else {
+                    const uint64_t h = tab_hash(lk_canon(f, j, mask));
+                    sel = (uint32_t)(h >> 56) & 3u;
+                    bb = bloom_bits(h);
+                }
                 const uint32_t wv = sel == 0 ? blk.x : sel == 1 ? blk.y : sel == 2 ? blk.z : blk.w;
-                const uint32_t bb = bloom_bits(h);
                 const bool pass = (((wv & bb) == bb) || ((force >> j) & 1u)) && ((wm >> j) & 1u);
                 if (pass) {
+                    const uint64_t key = lk_canon(f, j, mask);
                     const uint32_t pos = atomicAdd(&qcnt[wave], 1u);
                     if (pos < LK_QN) {
                         qkey[wave][pos] = key;
