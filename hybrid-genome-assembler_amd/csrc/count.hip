@@ -352,39 +352,124 @@ __global__ void kc_fs(const uint64_t* __restrict__ off, const BinFile* __restric
 // Inputs with far more than 2^MAX_FB x 65536 instances (a C4 rank shard: ~800 K per fine bucket)
 // would make every count workgroup re-read its bucket once per LDS-sized sub-range.  One more
 // level instead: one workgroup per fine bucket b splits each file's run by the top fb3 bits of
-// the remainder into S = 2^fb3 sub-buckets, laid out (sub-bucket, file)-major, and strips those
-// bits, so the count kernels run unchanged on nb * S buckets of rbits - fb3 bit remainders
-// (((b << fb3 | s) << (rbits - fb3)) | rem == (b << rbits) | v).  fs3 is fs for the sub-buckets.
+// the remainder into S = 2^fb3 sub-buckets and strips those bits, so the count kernels run
+// unchanged on nb * S buckets of rbits - fb3 bit remainders
+// (((b << fb3 | s) << (rbits - fb3)) | rem == (b << rbits) | v).
+// One read of the bucket: sub-bucket sizes of a hashed key are near-uniform, so each gets a slab of
+// cap = 1.25x its share + 64 in the bucket's output region [R(b), R(b+1)), R(b) = a + a/4 + b*S*64
+// for the bucket's input start a; files are written one after the other into every slab, so fs3
+// keeps its (sub-bucket, file) start + sub-bucket end form (sub-buckets need not be adjacent).  A
+// slab that would overflow (a key repeated far more often than the rest) makes the workgroup redo
+// its bucket exactly: a histogram pass, then the scatter, packed from R(b).
 constexpr int NT_3 = 1024;
 constexpr int R_3 = 8;   // elements per thread in flight
 constexpr uint32_t MAX_SF3 = 4096;
+constexpr uint32_t SLACK_3 = 64;   // extra slots per sub-bucket slab
 template <class E>
 __global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, const uint64_t* __restrict__ fs,
                                                   uint32_t F, uint32_t fb3, uint32_t rbits, E* __restrict__ out,
                                                   uint64_t* __restrict__ fs3) {
     constexpr uint32_t BT = (uint32_t)NT_3 * R_3;   // batch: staged in LDS, written in sub-bucket runs
-    __shared__ uint32_t h[MAX_SF3];                   // counts, then output cursors, per (sub-bucket, file)
+    __shared__ uint32_t h[MAX_SF3];                   // per (sub-bucket, file): counts, then cursors
     __shared__ uint32_t bc[256], bo[256];             // per-batch sub-bucket counts / offsets
     __shared__ E stage[BT];
     __shared__ uint32_t ws[NT_3 / 64 + 1];
+    __shared__ uint32_t s_ovf;
     const uint32_t tid = threadIdx.x, b = blockIdx.x, S = 1u << fb3, SF = S * F;
     const uint64_t* f = fs + (uint64_t)b * (F + 1);
     const uint32_t sh = rbits - fb3;
     const E rm = (E)(((E)1 << sh) - 1);
+    const uint64_t a0 = f[0], e0 = f[F];
+    const uint64_t R0 = a0 + (a0 >> 2) + (uint64_t)b * S * SLACK_3;
+    const uint64_t R1 = e0 + (e0 >> 2) + (uint64_t)(b + 1) * S * SLACK_3;
+    const uint64_t cap = (R1 - R0) / S;
+    // one batch of file ff's run [a, e) from i0: ranked by sub-bucket, staged, written in runs to
+    // dst(t) + h[t * hs] + rank; returns nothing, sets s_ovf if a run would pass lim (0: no limit)
+    auto load_batch = [&](uint64_t i0, uint64_t e, E (&v)[R_3]) {
+#pragma unroll
+        for (int q = 0; q < R_3; ++q) {
+            const uint64_t i = i0 + (uint64_t)q * NT_3 + tid;
+            v[q] = i < e ? in[i] : (E)0;
+        }
+    };
+    // the next batch's elements are loaded before this one is ranked, so they are in flight meanwhile
+    auto scatter_batch = [&](uint64_t i0, uint64_t e, uint32_t hs, uint32_t hoff, uint64_t lim, auto dst,
+                             E (&nx)[R_3]) {
+        E v[R_3];
+        uint32_t sb[R_3], rk[R_3];
+#pragma unroll
+        for (int q = 0; q < R_3; ++q) v[q] = nx[q];
+        if (i0 + BT < e) load_batch(i0 + BT, e, nx);
+        for (uint32_t j = tid; j < S; j += NT_3) bc[j] = 0;
+        lds_barrier();   // LDS only: the next batch's loads stay in flight
+#pragma unroll
+        for (int q = 0; q < R_3; ++q) {
+            sb[q] = (uint32_t)(v[q] >> sh);
+            rk[q] = i0 + (uint64_t)q * NT_3 + tid < e ? atomicAdd(&bc[sb[q]], 1u) : 0u;
+        }
+        lds_barrier();   // LDS only: the next batch's loads stay in flight
+        if (tid < 64) {   // batch offsets per sub-bucket (S <= 256): one wave, four per lane
+            uint32_t c[4], t4 = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = tid * 4 + q < S ? bc[tid * 4 + q] : 0u;
+                t4 += c[q];
+            }
+            uint32_t o = wave_incl_scan(t4, (int)tid) - t4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (tid * 4 + q < S) bo[tid * 4 + q] = o;
+                o += c[q];
+            }
+        }
+        lds_barrier();   // LDS only: the next batch's loads stay in flight
+#pragma unroll
+        for (int q = 0; q < R_3; ++q)
+            if (i0 + (uint64_t)q * NT_3 + tid < e) stage[bo[sb[q]] + rk[q]] = v[q];
+        lds_barrier();   // LDS only: the next batch's loads stay in flight
+        const uint32_t m = (uint32_t)((e - i0) < (uint64_t)BT ? (e - i0) : BT);
+        for (uint32_t j = tid; j < m; j += NT_3) {   // staged order: one run per sub-bucket
+            const E x = stage[j];
+            const uint32_t t = (uint32_t)(x >> sh);
+            const uint64_t pos = (uint64_t)h[t * hs + hoff] + (j - bo[t]);
+            if (lim && pos >= lim) {
+                s_ovf = 1u;
+                continue;
+            }
+            out[dst(t) + pos] = x & rm;
+        }
+        lds_barrier();   // LDS only: the next batch's loads stay in flight
+        for (uint32_t t = tid; t < S; t += NT_3) h[t * hs + hoff] += bc[t];
+        lds_barrier();   // LDS only: the next batch's loads stay in flight
+    };
+    // 1) optimistic: one read, every sub-bucket in its slab (h[t] = the slab's fill)
+    for (uint32_t j = tid; j < S; j += NT_3) h[j] = 0;
+    if (tid == 0) s_ovf = 0;
+    __syncthreads();
+    for (uint32_t ff = 0; ff < F; ++ff) {
+        for (uint32_t t = tid; t < S; t += NT_3) fs3[((uint64_t)b * S + t) * (F + 1) + ff] = R0 + t * cap + h[t];
+        const uint64_t a = f[ff], e = f[ff + 1];
+        E nx[R_3];
+        if (a < e) load_batch(a, e, nx);
+        for (uint64_t i0 = a; i0 < e; i0 += BT)
+            scatter_batch(i0, e, 1u, 0u, cap, [&](uint32_t t) { return R0 + (uint64_t)t * cap; }, nx);
+    }
+    if (!s_ovf) {
+        for (uint32_t t = tid; t < S; t += NT_3) fs3[((uint64_t)b * S + t) * (F + 1) + F] = R0 + t * cap + h[t];
+        return;
+    }
+    // 2) a slab overflowed: exact two-pass layout, packed from R0
+    __syncthreads();
     for (uint32_t j = tid; j < SF; j += NT_3) h[j] = 0;
     __syncthreads();
     for (uint32_t ff = 0; ff < F; ++ff) {
         const uint64_t a = f[ff], e = f[ff + 1];
         for (uint64_t i0 = a; i0 < e; i0 += BT) {
-            E v[R_3];
 #pragma unroll
             for (int q = 0; q < R_3; ++q) {
                 const uint64_t i = i0 + (uint64_t)q * NT_3 + tid;
-                v[q] = i < e ? in[i] : (E)0;
+                if (i < e) atomicAdd(&h[(uint32_t)(in[i] >> sh) * F + ff], 1u);
             }
-#pragma unroll
-            for (int q = 0; q < R_3; ++q)
-                if (i0 + (uint64_t)q * NT_3 + tid < e) atomicAdd(&h[(uint32_t)(v[q] >> sh) * F + ff], 1u);
         }
     }
     __syncthreads();
@@ -398,58 +483,25 @@ __global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, cons
     }
     uint32_t tot;
     uint32_t run = block_excl_scan<NT_3>(sum, ws, &tot);
-    const uint64_t base = f[0];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t j = tid * 4 + q;
         if (j < SF) {
             h[j] = run;
-            fs3[((uint64_t)b * S + j / F) * (F + 1) + j % F] = base + run;
+            fs3[((uint64_t)b * S + j / F) * (F + 1) + j % F] = R0 + run;
             run += loc[q];
         }
     }
     __syncthreads();
     for (uint32_t sb = tid; sb < S; sb += NT_3)
-        fs3[((uint64_t)b * S + sb) * (F + 1) + F] = sb + 1 < S ? base + h[(sb + 1) * F] : f[F];
+        fs3[((uint64_t)b * S + sb) * (F + 1) + F] = sb + 1 < S ? R0 + h[(sb + 1) * F] : R0 + (e0 - a0);
+    __syncthreads();
     for (uint32_t ff = 0; ff < F; ++ff) {
         const uint64_t a = f[ff], e = f[ff + 1];
-        for (uint64_t i0 = a; i0 < e; i0 += BT) {
-            E v[R_3];
-            uint32_t sb[R_3], rk[R_3];
-#pragma unroll
-            for (int q = 0; q < R_3; ++q) {
-                const uint64_t i = i0 + (uint64_t)q * NT_3 + tid;
-                v[q] = i < e ? in[i] : (E)0;
-            }
-            for (uint32_t j = tid; j < S; j += NT_3) bc[j] = 0;
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < R_3; ++q) {
-                sb[q] = (uint32_t)(v[q] >> sh);
-                rk[q] = i0 + (uint64_t)q * NT_3 + tid < e ? atomicAdd(&bc[sb[q]], 1u) : 0u;
-            }
-            __syncthreads();
-            {   // batch offsets per sub-bucket (S <= 256: the first 256 threads)
-                const uint32_t c0 = tid < S ? bc[tid] : 0u;
-                uint32_t bt;
-                const uint32_t ex = block_excl_scan<NT_3>(c0, ws, &bt);
-                if (tid < S) bo[tid] = ex;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < R_3; ++q)
-                if (i0 + (uint64_t)q * NT_3 + tid < e) stage[bo[sb[q]] + rk[q]] = v[q];
-            __syncthreads();
-            const uint32_t m = (uint32_t)((e - i0) < (uint64_t)BT ? (e - i0) : BT);
-            for (uint32_t j = tid; j < m; j += NT_3) {   // staged order: one run per sub-bucket
-                const E x = stage[j];
-                const uint32_t t = (uint32_t)(x >> sh);
-                out[base + h[t * F + ff] + (j - bo[t])] = x & rm;
-            }
-            __syncthreads();
-            for (uint32_t t = tid; t < S; t += NT_3) h[t * F + ff] += bc[t];
-            __syncthreads();
-        }
+        E nx[R_3];
+        if (a < e) load_batch(a, e, nx);
+        for (uint64_t i0 = a; i0 < e; i0 += BT)
+            scatter_batch(i0, e, F, ff, 0ull, [&](uint32_t) { return R0; }, nx);
     }
 }
 
@@ -1635,7 +1687,8 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     }
     if (fb3) {
         const uint32_t S = 1u << fb3;
-        void* binned3 = s.binned3.ensure(std::max<size_t>(total_bytes, 1) * esz);
+        // output regions: 1.25x every bucket + SLACK_3 per sub-bucket (kc_split3's slabs)
+        void* binned3 = s.binned3.ensure((total_bytes + total_bytes / 4 + (uint64_t)nb * S * SLACK_3 + 64) * esz);
         uint64_t* fs3 = static_cast<uint64_t*>(s.file_start3.ensure((size_t)nb * S * (F + 1) * 8));
         c->launch("kc_split3", [&] {
             if (e32)

@@ -239,6 +239,18 @@ def test_count_split3_forced_vs_oracle(gpu_ctx, monkeypatch, fb3, k, n_files):
     assert r["stats"].buckets > 1
 
 
+def test_count_split3_slab_overflow(gpu_ctx, monkeypatch):
+    # kc_split3 gives every sub-bucket a slab of 1.25x its share: one k-mer repeated ~260 K times
+    # (poly-A reads) fills its sub-bucket's slab, and that bucket is redone by the exact two-pass layout
+    monkeypatch.setenv("HGA_SPLIT3_FORCE", "5")
+    streams = random_streams(77, 2, 400, 120, "ACGT")
+    streams[0] = streams[0] + b"\n" + b"\n".join([b"A" * 150] * 2000)
+    streams[1] = streams[1] + b"\n" + b"\n".join([b"T" * 150] * 300)
+    o = oracle.count_pipeline(streams, 19, 2, 6)
+    r = run_gpu(gpu_ctx, streams, 19, 2, 6)
+    assert_same(r, o)
+
+
 def test_count_split3_c1_scale(gpu_ctx, hga_mod, monkeypatch):
     monkeypatch.setenv("HGA_SPLIT3_FORCE", "6")
     ga = hga_mod.gen_genome(500_000, 1)
