@@ -1357,39 +1357,80 @@ __global__ void __launch_bounds__(NT_HC) kc_hist_compact(unsigned long long* __r
 }
 
 #ifndef HGA_SEL_GRID
-#define HGA_SEL_GRID 1024u   // kc_select workgroups (each loops over the chunks beyond the grid)
+#define HGA_SEL_GRID 1024u   // kc_select workgroups (each takes a contiguous range of chunks)
 #endif
-constexpr int SEL_R = 16;   // rows per thread: one cursor atomic (and one count atomic) per 4096 rows
+constexpr int SEL_R = 16;   // rows per thread: chunks of NT_H * SEL_R = 4096 rows
 constexpr uint32_t SEL_HB = 4096;   // top-12-bit histogram of the kept keys (the export sort's MSD pass)
-// Persistent over chunks of NT_H * SEL_R rows (each chunk: one cursor atomic pair); with dhist_rows
-// the workgroup also counts its kept keys by the top 12 bits of the sort width (hshift = 2k - 12),
-// written as one row of SEL_HB counts per workgroup.
+
+// block_excl_scan with LDS-only barriers (global loads issued before it stay in flight)
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan_lb(uint32_t v, uint32_t* ws, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int NW = NT / 64;
+    const uint32_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) ws[wave] = inc;
+    lds_barrier();
+    if (wave == 0) {
+        const uint32_t t = lane < NW ? ws[lane] : 0u;
+        const uint32_t ti = wave_incl_scan(t, lane);
+        if (lane < NW) ws[lane] = ti - t;
+        if (lane == NW - 1) ws[NW] = ti;
+    }
+    lds_barrier();
+    const uint32_t r = ws[wave] + inc - v;
+    *total = ws[NW];
+    lds_barrier();
+    return r;
+}
+
+// Each workgroup takes `cpw` consecutive chunks of 4096 rows and writes its kept keys, in row order,
+// to its own region of wkeys (region = cpw * 4096 slots): no device-wide cursor (one same-address
+// atomic per chunk serialised at ≈88/µs: 3 ms at a C4 shard's 126 K chunks); kc_sel_compact then
+// moves the regions together.  The next chunk's counts are loaded while this one is selected
+// (LDS-only barriers keep them in flight).  With dhist_rows the workgroup also counts its kept keys
+// by the top 12 bits of the sort width (hshift = 2k - 12), one row of SEL_HB counts per workgroup.
 __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ keys,
                                                   const uint32_t* __restrict__ cnt, uint64_t rows,
                                                   uint64_t cap, uint32_t F, int64_t lower,
-                                                  int64_t upper, uint64_t* __restrict__ out,
-                                                  uint32_t* __restrict__ out_flag, bool flag_bit,
-                                                  unsigned long long* __restrict__ stat,
+                                                  int64_t upper, uint64_t* __restrict__ wkeys,
+                                                  uint32_t* __restrict__ wflag, bool flag_bit, uint32_t cpw,
+                                                  unsigned long long* __restrict__ wcnt,
                                                   uint32_t* __restrict__ dhist_rows, int hshift) {
     __shared__ uint32_t ws[NT_H / 64 + 1];
-    __shared__ unsigned long long s_base;
     __shared__ uint64_t stage[NT_H * SEL_R];
     __shared__ uint8_t sflag[NT_H * SEL_R];
     __shared__ uint32_t dh[SEL_HB];
     if (dhist_rows)
         for (uint32_t i = threadIdx.x; i < SEL_HB; i += NT_H) dh[i] = 0;
     const uint64_t chunks = (rows + NT_H * SEL_R - 1) / (NT_H * SEL_R);
-    for (uint64_t ch = blockIdx.x; ch < chunks; ch += gridDim.x) {
+    const uint64_t ch0 = (uint64_t)blockIdx.x * cpw;
+    const uint64_t ch1 = ch0 + cpw < chunks ? ch0 + cpw : chunks;
+    const uint64_t region = (uint64_t)cpw * NT_H * SEL_R;
+    uint64_t* __restrict__ wk = wkeys + blockIdx.x * region;
+    uint32_t* __restrict__ wf = flag_bit ? nullptr : wflag + blockIdx.x * region;
+    uint64_t wo = 0, wd = 0;   // this workgroup's kept / discriminative rows so far (uniform)
+    // the first two files' counts of a chunk's SEL_R rows per thread (rows < cap are allocated)
+    uint32_t n0[SEL_R], n1[SEL_R];
+    auto load_counts = [&](uint64_t ch) {
+        const uint64_t bn = ch * NT_H * SEL_R;
+#pragma unroll
+        for (int q = 0; q < SEL_R; ++q) {
+            const uint64_t r = bn + (uint64_t)q * NT_H + threadIdx.x;
+            n0[q] = r < cap ? cnt[r] : 0u;
+            n1[q] = (F > 1 && r < cap) ? cnt[cap + r] : 0u;
+        }
+    };
+    if (ch0 < ch1) load_counts(ch0);
+    for (uint64_t ch = ch0; ch < ch1; ++ch) {
         const uint64_t base = ch * NT_H * SEL_R;
         uint64_t take = 0, disc = 0;   // bit q: row base + q*NT_H + tid
-        // the first two files' counts of all SEL_R rows loaded together (rows < cap are allocated)
         uint32_t c0[SEL_R], c1[SEL_R];
 #pragma unroll
         for (int q = 0; q < SEL_R; ++q) {
-            const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
-            c0[q] = r < cap ? cnt[r] : 0u;
-            c1[q] = (F > 1 && r < cap) ? cnt[cap + r] : 0u;
+            c0[q] = n0[q];
+            c1[q] = n1[q];
         }
+        if (ch + 1 < ch1) load_counts(ch + 1);
 #pragma unroll
         for (int q = 0; q < SEL_R; ++q) {
             const uint64_t r = base + (uint64_t)q * NT_H + threadIdx.x;
@@ -1406,20 +1447,14 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
                 if (nz == 1) disc |= 1ull << q;
             }
         }
-        // the kept rows' keys requested now: their latency overlaps the scans and the cursor atomic
+        // the kept rows' keys requested now: their latency overlaps the scans
         uint64_t kv[SEL_R];
 #pragma unroll
         for (int q = 0; q < SEL_R; ++q)
             kv[q] = ((take >> q) & 1ull) ? keys[base + (uint64_t)q * NT_H + threadIdx.x] : 0ull;
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan<NT_H>((uint32_t)__popcll(take), ws, &tot);
-        // same-address device atomics serialise (≈88/µs chip-wide): one pair per chunk
-        uint32_t dtot;
-        (void)block_excl_scan<NT_H>((uint32_t)__popcll(disc), ws, &dtot);
-        if (threadIdx.x == 0) {
-            s_base = tot ? atomicAdd(&stat[0], (unsigned long long)tot) : 0ull;
-            if (dtot) atomicAdd(&stat[1], (unsigned long long)dtot);
-        }
+        uint32_t tot, dtot;
+        const uint32_t ex = block_excl_scan_lb<NT_H>((uint32_t)__popcll(take), ws, &tot);
+        (void)block_excl_scan_lb<NT_H>((uint32_t)__popcll(disc), ws, &dtot);
         // kept keys staged in LDS (row order), then written out coalesced
         uint32_t o = ex;
 #pragma unroll
@@ -1429,17 +1464,64 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
                 if (!flag_bit) sflag[o - 1] = (uint8_t)((disc >> q) & 1ull);
                 if (dhist_rows) atomicAdd(&dh[(uint32_t)(kv[q] >> hshift) & (SEL_HB - 1)], 1u);
             }
-        __syncthreads();
-        const uint64_t ob = s_base;
+        lds_barrier();
         for (uint32_t j = threadIdx.x; j < tot; j += NT_H) {
-            out[ob + j] = stage[j];
-            if (!flag_bit) out_flag[ob + j] = sflag[j];
+            wk[wo + j] = stage[j];
+            if (!flag_bit) wf[wo + j] = sflag[j];
         }
-        __syncthreads();   // stage and s_base are reused by the next chunk
+        wo += tot;
+        wd += dtot;
+        lds_barrier();   // stage is reused by the next chunk
+    }
+    if (threadIdx.x == 0) {
+        wcnt[2 * blockIdx.x] = wo;
+        wcnt[2 * blockIdx.x + 1] = wd;
     }
     if (dhist_rows) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < SEL_HB; i += NT_H) dhist_rows[(uint64_t)blockIdx.x * SEL_HB + i] = dh[i];
+    }
+}
+
+// Workgroup w of kc_select's grid: its kept keys (and flags) to out[sum of the kept counts of
+// workgroups < w ...]; workgroup 0 also leaves the totals in stat[0] (kept) and stat[1]
+// (discriminative).  The grid's counts are summed by every workgroup (<= HGA_SEL_GRID of them).
+__global__ void __launch_bounds__(256) kc_sel_compact(const uint64_t* __restrict__ wkeys,
+                                                      const uint32_t* __restrict__ wflag, uint64_t region,
+                                                      const unsigned long long* __restrict__ wcnt, uint32_t grid,
+                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ out_flag,
+                                                      bool flag_bit, unsigned long long* __restrict__ stat) {
+    __shared__ unsigned long long red[3][4];
+    const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long pre = 0, tk = 0, td = 0;
+    for (uint32_t i = tid; i < grid; i += 256) {
+        const unsigned long long k = wcnt[2 * i], d = wcnt[2 * i + 1];
+        pre += i < w ? k : 0ull;
+        tk += k;
+        td += d;
+    }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        pre += __shfl_xor(pre, o, 64);
+        tk += __shfl_xor(tk, o, 64);
+        td += __shfl_xor(td, o, 64);
+    }
+    if (lane == 0) {
+        red[0][wave] = pre;
+        red[1][wave] = tk;
+        red[2][wave] = td;
+    }
+    __syncthreads();
+    pre = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    if (w == 0 && tid == 0) {
+        stat[0] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        stat[1] = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    }
+    const uint64_t n = wcnt[2 * w];
+    const uint64_t* __restrict__ src = wkeys + (uint64_t)w * region;
+    for (uint64_t j = tid; j < n; j += 256) {
+        out[pre + j] = src[j];
+        if (!flag_bit) out_flag[pre + j] = wflag[(uint64_t)w * region + j];
     }
 }
 
@@ -1933,9 +2015,15 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     // flag rides in the key; kc_select counts the kept keys by the top 12 bits of the code
     const bool msd = flag_bit && bits >= 16 && s.rows >= (1u << 15);
     const uint64_t chunks = blocks_for(std::max<uint64_t>(s.rows, 1), NT_H * SEL_R);
-    const unsigned grid = (unsigned)std::min<uint64_t>(chunks, (uint64_t)HGA_SEL_GRID);
+    const uint32_t cpw = (uint32_t)blocks_for(chunks, HGA_SEL_GRID);   // chunks per workgroup
+    const unsigned grid = (unsigned)blocks_for(chunks, cpw);
+    const uint64_t region = (uint64_t)cpw * NT_H * SEL_R;
     const size_t hb = (size_t)SEL_HB * 4;
-    char* tb = static_cast<char*>(s.sel_tmp.ensure(64 + hb + 1024 + (msd ? (size_t)grid * hb : 0)));
+    char* tb = static_cast<char*>(s.sel_tmp.ensure(64 + hb + 1024 + (size_t)grid * 16 + (msd ? (size_t)grid * hb : 0)));
+    auto* wcnt = reinterpret_cast<unsigned long long*>(tb + 64 + hb + 1024 + (msd ? (size_t)grid * hb : 0));
+    char* wt = static_cast<char*>(s.sel_wtmp.ensure((size_t)grid * region * (flag_bit ? 8 : 12) + 64));
+    uint64_t* wkeys = reinterpret_cast<uint64_t*>(wt);
+    uint32_t* wflag = reinterpret_cast<uint32_t*>(wt + (size_t)grid * region * 8);
     auto* stat = reinterpret_cast<unsigned long long*>(tb);
     uint32_t* dhist = reinterpret_cast<uint32_t*>(tb + 64);                // SEL_HB top-12-bit counts
     uint32_t* dig256 = reinterpret_cast<uint32_t*>(tb + 64 + hb);          // the MSD digit counts
@@ -1944,8 +2032,11 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     if (s.rows) {
         c->launch("kc_select", [&] {
             hipLaunchKernelGGL(kc_select, dim3(grid), dim3(NT_H), 0, c->stream, s.rows_key.as<uint64_t>(),
-                               s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, lower, upper, out, flag,
-                               flag_bit, stat, dhist_rows, bits - 12);
+                               s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, lower, upper, wkeys, wflag,
+                               flag_bit, cpw, wcnt, dhist_rows, bits - 12);
+            hipLaunchKernelGGL(kc_sel_compact, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys,
+                               (const uint32_t*)wflag, region, (const unsigned long long*)wcnt, grid, out, flag,
+                               flag_bit, stat);
             if (msd)
                 hipLaunchKernelGGL(kc_dhist_reduce, dim3(SEL_HB / 256, (grid + 31) / 32), dim3(256), 0, c->stream,
                                    dhist_rows, grid, dhist);
