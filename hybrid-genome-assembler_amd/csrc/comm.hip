@@ -232,12 +232,11 @@ void count_exchange(hga_ctx* c, uint32_t min_per_file) {
     HGA_REQUIRE(s.min_per_file == 1, HGA_ERR_STATE, "the local count must keep singletons: hga_count_run(ctx, 1)");
     HGA_REQUIRE(min_per_file >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
     CtxXport x(c);
-    // instances / bytes this rank counted, summed for the global stats
-    std::vector<uint64_t> mine{s.instances, 0};
+    // instances / bytes this rank counted, summed for the global stats (in the piece-count gather)
+    std::vector<uint64_t> mine{s.instances, 0}, g;
     for (auto l : s.seq_len) mine[1] += l;
-    const std::vector<uint64_t> g = proto::sum_u64(x, mine);
     DevEngine e{c};
-    proto::count_exchange(e, x, min_per_file);
+    proto::count_exchange(e, x, min_per_file, mine, &g);
     s.g_instances = g[0];
     s.g_bytes = g[1];
     s.dist = true;

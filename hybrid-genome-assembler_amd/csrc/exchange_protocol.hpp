@@ -14,6 +14,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <map>
 #include <utility>
 #include <vector>
@@ -55,16 +56,26 @@ inline std::vector<uint64_t> owner_splitters(int k, int P) {
 //   void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per);
 //   void merge(const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min);
 //   void sync();
-// Returns the pieces / rows this owner received.
+// Returns the pieces / rows this owner received.  `extra` (same length on every rank) rides in the
+// piece-count all-gather; *extra_sum receives its element-wise sums over the ranks (one collective
+// less per exchange).
 template <class E>
-uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file) {
+uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file, const std::vector<uint64_t>& extra = {},
+                        std::vector<uint64_t>* extra_sum = nullptr) {
     const int P = x.nranks;
+    const size_t X = extra.size(), W = (size_t)P + X;
     const std::vector<uint64_t> spl = owner_splitters(e.k(), P);
-    std::vector<uint64_t> per(P), all((size_t)P * P), rn(P), sb(P), rb(P);
+    std::vector<uint64_t> per(W), all((size_t)P * W), rn(P), sb(P), rb(P);
+    for (size_t i = 0; i < X; ++i) per[P + i] = extra[i];
     auto recv_counts = [&] {
-        x.allgather(per.data(), 8 * (uint64_t)P, all.data());
+        x.allgather(per.data(), 8 * (uint64_t)W, all.data());
         uint64_t n = 0;
-        for (int p = 0; p < P; ++p) n += (rn[p] = all[(size_t)p * P + x.rank]);
+        for (int p = 0; p < P; ++p) n += (rn[p] = all[(size_t)p * W + x.rank]);
+        if (extra_sum) {
+            extra_sum->assign(X, 0);
+            for (int p = 0; p < P; ++p)
+                for (size_t i = 0; i < X; ++i) (*extra_sum)[i] += all[(size_t)p * W + P + i];
+        }
         return n;
     };
     if (e.pack_bits() > 0) {   // one u64 piece per row (a count past the piece width: several pieces)
@@ -114,8 +125,29 @@ uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file) {
 }
 
 // Owners' (threshold index, total, count) triples -> the global histogram, (threshold, total) order.
+// One fixed-size all-gather of [n, up to HIST_CAP triples] per rank; only when some rank has more
+// triples (very wide count ranges) a variable-size all-gather follows.
+constexpr size_t HIST_CAP = 1024;
 inline std::vector<int64_t> spec_hist_global(Xport& x, const std::vector<int64_t>& local) {
-    const auto parts = x.allgatherv(local.data(), local.size() * 8);
+    const size_t P = (size_t)x.nranks, slot = 1 + 3 * HIST_CAP;
+    std::vector<int64_t> mine(slot, 0), all(P * slot);
+    const size_t n = local.size() / 3;
+    mine[0] = (int64_t)n;
+    for (size_t i = 0; i < 3 * n && i < 3 * HIST_CAP; ++i) mine[1 + i] = local[i];
+    x.allgather(mine.data(), slot * 8, all.data());
+    bool fits = true;
+    for (size_t p = 0; p < P; ++p) fits = fits && (size_t)all[p * slot] <= HIST_CAP;
+    std::vector<std::vector<char>> parts;
+    if (fits) {
+        parts.resize(P);
+        for (size_t p = 0; p < P; ++p) {
+            const size_t np = (size_t)all[p * slot];
+            parts[p].resize(np * 24);
+            if (np) std::memcpy(parts[p].data(), &all[p * slot + 1], np * 24);
+        }
+    } else {
+        parts = x.allgatherv(local.data(), local.size() * 8);
+    }
     std::map<std::pair<int64_t, int64_t>, int64_t> bins;
     for (const auto& pt : parts) {
         const int64_t* t = reinterpret_cast<const int64_t*>(pt.data());

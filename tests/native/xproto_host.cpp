@@ -247,6 +247,16 @@ int64_t xt_spec_hist(void* h, const double* thr, int n_thr, int64_t** out) {
     return (int64_t)g.size() / 3;
 }
 
+// the protocol's histogram merge on given triples (both the one-gather path and the variable-size
+// fallback for more than proto::HIST_CAP triples on a rank)
+int64_t xt_hist_merge(void* h, const int64_t* local, int64_t n_triples, int64_t** out) {
+    auto* r = static_cast<Rank*>(h);
+    const std::vector<int64_t> v(local, local + 3 * n_triples);
+    const std::vector<int64_t> g = hga::proto::spec_hist_global(r->x, v);
+    *out = dup(g);
+    return (int64_t)g.size() / 3;
+}
+
 // global export: keys ascending (owners in rank order), flags; *n_discr over all owners
 int64_t xt_select(void* h, int64_t lower, int64_t upper, uint64_t** keys, uint8_t** flags, uint64_t* n_discr) {
     auto* r = static_cast<Rank*>(h);

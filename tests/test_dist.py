@@ -126,6 +126,46 @@ def test_exchange_protocol_matches_single_process(world, packed, k, heavy, tmp_p
         assert int(r["d"]) == ref["n_discr"] and int(r["flags"].sum()) == ref["n_discr"]
 
 
+def _hist_worker(rank, world, port, sizes, out_path):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        L = xlib()
+        L.xt_hist_merge.restype = C.c_int64
+        L.xt_hist_merge.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_void_p)]
+        t = hga_dist.gloo_transport()
+        h = L.xt_create(K, 2, rank, world, C.addressof(t), 1)
+        rng = np.random.default_rng(rank)
+        n = sizes[rank]
+        loc = np.stack([rng.integers(0, 8, n), rng.integers(1, 5000, n), rng.integers(1, 100, n)], 1).astype(np.int64)
+        order = np.lexsort((loc[:, 1], loc[:, 0]))
+        loc = loc[order]
+        _, first = np.unique(loc[:, :2], axis=0, return_index=True)
+        loc = np.ascontiguousarray(loc[np.sort(first)])
+        p = C.c_void_p()
+        m = L.xt_hist_merge(h, loc.ctypes.data, len(loc), C.byref(p))
+        got = _take(L, p, 3 * m, np.int64).reshape(-1, 3)
+        L.xt_destroy(h)
+        np.savez(out_path + f".{rank}.npz", loc=loc, got=got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [(300, 700), (1500, 40), (0, 2000, 5)])
+def test_histogram_merge_fixed_and_fallback_gathers(tmp_path, sizes):
+    # spec_hist_global: one fixed-size all-gather when every rank has <= HIST_CAP (1024) triples, the
+    # variable-size all-gather otherwise; both give the per-(threshold, total) sums in std::map order
+    world = len(sizes)
+    out = str(tmp_path / "h")
+    mp.start_processes(_hist_worker, args=(world, _free_port(), sizes, out), nprocs=world, start_method="spawn")
+    acc = {}
+    for rank in range(world):
+        for ti, tot, c in np.load(out + f".{rank}.npz")["loc"]:
+            acc[(int(ti), int(tot))] = acc.get((int(ti), int(tot)), 0) + int(c)
+    want = np.array([[a, b, acc[(a, b)]] for a, b in sorted(acc)], np.int64).reshape(-1, 3)
+    for rank in range(world):
+        assert np.array_equal(np.load(out + f".{rank}.npz")["got"], want)
+
+
 def test_splitters_and_shards():
     L = xlib()
     for k in (1, 5, 19, 32):
