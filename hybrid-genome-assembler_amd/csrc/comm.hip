@@ -210,7 +210,7 @@ struct DevEngine {
     void* send_buf(uint64_t bytes) { return c->count.xsend.ensure(bytes + 64); }
     void* recv_buf(uint64_t bytes) { return c->count.xrecv.ensure(bytes + 64); }
     uint64_t partition_packed(const uint64_t* spl, uint32_t P, uint64_t* out, uint64_t cap, uint64_t* per) {
-        return count_partition_packed(c, spl, P, out, cap, per);
+        return count_partition_packed(c, spl, P, out, cap, per, false);
     }
     void merge_packed(const uint64_t* in, uint64_t n, uint32_t min) { count_merge_packed(c, in, n, min); }
     void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per) {

@@ -647,7 +647,7 @@ int count_pack_bits(hga_ctx* c) {
 // Packs this rank's rows by owner into `out` (capacity cap_out pieces).  Returns the number of
 // pieces; if it exceeds cap_out nothing is written (the caller retries with more room).
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,
-                                uint64_t cap_out, uint64_t* pieces_per_owner) {
+                                uint64_t cap_out, uint64_t* pieces_per_owner, bool sync_out) {
     auto& s = c->count;
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
@@ -692,7 +692,9 @@ uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t 
                            s.rows_cnt.as<uint32_t>(), s.rows_cap, rows, spl, n_own, pf, hist, n_tiles, out);
     });
     c->check_launch("kx_pack_scatter");
-    c->sync();
+    // the C entry point hands `out` to the caller; the exchange protocol's next use of it is ordered
+    // on this stream (RCCL) or behind a synchronising copy (host transport)
+    if (sync_out) c->sync();
     return total;
 }
 

@@ -238,7 +238,7 @@ void connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t* score, ui
 void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts, uint64_t n);
 int count_pack_bits(hga_ctx* c);
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,
-                                uint64_t cap_out, uint64_t* pieces_per_owner);
+                                uint64_t cap_out, uint64_t* pieces_per_owner, bool sync_out = true);
 void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t min_c);
 
 // comm.hip: multi-GPU counting (hga_comm_*, hga_count_exchange) and the global query answers
