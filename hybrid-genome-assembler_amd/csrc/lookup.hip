@@ -68,13 +68,12 @@ __device__ __forceinline__ uint32_t bloom_bits(uint64_t h) {
 // function of the canonical k-mer; consecutive windows of a read share minimizers, so a
 // thread's 32 windows load a few filter blocks instead of 32 (the scan is bound by the L2
 // request rate, not by bytes).  Only used for ACGT-only windows (see lk_scan).
-#ifndef HGA_KM_MINK
-#define HGA_KM_MINK 15
-#endif
-#ifndef HGA_LK_KM
-#define HGA_LK_KM 7
-#endif
-constexpr int LK_KM = HGA_LK_KM;   // m = k - 7 for k >= 15 (eight m-mers per window); k < 15: plain hashing
+// Minimizer width: m = k - km m-mers, km + 1 of them per window.  km = 7 (eight m-mers per window)
+// for k >= 18; for 15 <= k <= 17 km shrinks so that m stays 11: with fewer distinct m-mers (4^m) the
+// filter's blocks would not spread (k = 15 with m = 8: 65 K minimizer blocks for the whole SDK set,
+// filter words saturate and most windows pass); k < 15: plain per-window hashing (km = 0).
+constexpr int LK_KM = 7;
+inline int lk_km_for(int k) { return k >= 18 ? LK_KM : (k >= 15 ? k - 11 : 0); }
 __device__ __forceinline__ uint64_t revcomp_code(uint64_t x, int m) {
     uint64_t y = ~x;                                           // complement: c -> 3 - c
     y = __builtin_bitreverse64(y);                             // reverse bits (and each pair)
@@ -854,7 +853,7 @@ void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n) {
     L.slots = nbk;   // buckets
     L.fwords = fw;
     L.k = k;
-    L.km = k >= HGA_KM_MINK ? LK_KM : 0;
+    L.km = lk_km_for(k);
     L.n_sdk = n;
     Bucket* tb = static_cast<Bucket*>(L.tab_key.ensure(nbk * sizeof(Bucket)));
     auto* filt = static_cast<uint32_t*>(L.filter.ensure(fw * 4));
@@ -957,9 +956,11 @@ void lookup_run(hga_ctx* c) {
                        nb, offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, (uint32_t*)nullptr,      \
                        (uint32_t*)nullptr, (uint32_t*)nullptr)
             if (L.km == LK_KM && k == 19) HGA_LK_SCAN(LK_KM, 19);   // compile-time k for the usual SDK k
-            else if (L.km == LK_KM && k == 17) HGA_LK_SCAN(LK_KM, 17);
             else if (L.km == LK_KM && k == 21) HGA_LK_SCAN(LK_KM, 21);
             else if (L.km == LK_KM) HGA_LK_SCAN(LK_KM, 0);
+            else if (L.km == 6) HGA_LK_SCAN(6, 17);   // k = 17
+            else if (L.km == 5) HGA_LK_SCAN(5, 16);
+            else if (L.km == 4) HGA_LK_SCAN(4, 15);
             else HGA_LK_SCAN(0, 0);
 #undef HGA_LK_SCAN
         });
