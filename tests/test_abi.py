@@ -46,3 +46,33 @@ def test_library_is_gfx950_code_object():
     so = os.path.join(ROOT, "hybrid-genome-assembler_amd", "lib", "libhga.so")
     data = open(so, "rb").read()
     assert b"gfx950" in data
+
+
+def test_header_is_plain_c_and_links(tmp_path):
+    # the boundary is a C ABI (cgo / JNI / ctypes bind it): hga.h must compile as strict C99 and a C
+    # program must link against libhga.so and get status codes back (no GPU: the error path)
+    import subprocess
+    src = tmp_path / "use_hga.c"
+    src.write_text(r'''
+#include "hga.h"
+#include <stdio.h>
+#include <string.h>
+int main(void) {
+    hga_ctx* c = 0;
+    int n = -1;
+    hga_status st = hga_device_count(&n);
+    if (st == HGA_OK && n > 0) { puts("gpu"); return 0; }
+    st = hga_ctx_create(&c, 0);
+    if (st == HGA_OK || strlen(hga_last_error()) == 0) return 2;
+    if (hga_count_run(0, 2) != HGA_ERR_INVALID) return 3;
+    puts("ok");
+    return 0;
+}
+''')
+    lib = os.path.join(ROOT, "hybrid-genome-assembler_amd", "lib")
+    exe = tmp_path / "use_hga"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    str(src), "-L", lib, "-lhga", f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() in ("ok", "gpu")
