@@ -1927,7 +1927,9 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     auto* ctrl = reinterpret_cast<unsigned long long*>(base + hbytes + over_cap * 8);
     double* dthr = reinterpret_cast<double*>(ctrl + 4);
     // pinned staging: [thresholds | ctrl readback (4 u64) | first SPEC_CHUNK compacted triples]
-    constexpr uint64_t SPEC_CHUNK = 1u << 12;
+    // 1024 triples (16 KB) cover a C2-sized histogram; the speculative read-back of 4096 (64 KB)
+    // cost ~20 us per call in the bench step
+    constexpr uint64_t SPEC_CHUNK = 1u << 10;
     char* hp = static_cast<char*>(c->pinned.ensure(MAX_THR * 8 + 32 + SPEC_CHUNK * 16 + 64));
     double* hthr = reinterpret_cast<double*>(hp);
     auto* hc = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8);
