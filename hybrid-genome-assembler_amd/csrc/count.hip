@@ -1537,6 +1537,53 @@ __global__ void __launch_bounds__(256) kc_dhist_reduce(const uint32_t* __restric
     if (s) atomicAdd(&hist[b], s);
 }
 
+// The export sort's MSD digit from the 12-bit histogram, on the device (so only 1 KB comes back):
+// the occupied bins [lo, hi], the smallest lg with (hi >> lg) - (lo >> lg) < 256, dbase = lo >> lg,
+// and the 256 digit counts dig[d] = sum of bins b in [lo, hi] with (b >> lg) - dbase == d.
+// span = {lo, hi, lg, dbase}; all zero when no key was kept.  One 256-thread workgroup.
+__global__ void __launch_bounds__(256) kc_sel_span(const uint32_t* __restrict__ hist, uint32_t* __restrict__ span,
+                                                   uint32_t* __restrict__ dig) {
+    __shared__ uint32_t s_lo[4], s_hi[4];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t b = t; b < SEL_HB; b += 256)
+        if (hist[b]) {
+            lo = min(lo, b);
+            hi = max(hi, b);
+        }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor(lo, o, 64));
+        hi = max(hi, (uint32_t)__shfl_xor(hi, o, 64));
+    }
+    if (lane == 0) {
+        s_lo[wave] = lo;
+        s_hi[wave] = hi;
+    }
+    __syncthreads();
+    lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
+    hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
+    if (lo > hi) {   // nothing kept
+        dig[t] = 0;
+        if (t < 4) span[t] = 0;
+        return;
+    }
+    uint32_t lg = 0;
+    while ((hi >> lg) - (lo >> lg) + 1 > 256) ++lg;
+    const uint32_t dbase = lo >> lg;
+    uint32_t sum = 0;
+    const uint32_t b0 = (dbase + t) << lg;
+    for (uint32_t b = b0; b < b0 + (1u << lg); ++b)
+        if (b >= lo && b <= hi) sum += hist[b];
+    dig[t] = sum;
+    if (t == 0) {
+        span[0] = lo;
+        span[1] = hi;
+        span[2] = lg;
+        span[3] = dbase;
+    }
+}
+
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
@@ -2039,33 +2086,28 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
             hipLaunchKernelGGL(kc_sel_compact, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys,
                                (const uint32_t*)wflag, region, (const unsigned long long*)wcnt, grid, out, flag,
                                flag_bit, stat);
-            if (msd)
+            if (msd) {
                 hipLaunchKernelGGL(kc_dhist_reduce, dim3(SEL_HB / 256, (grid + 31) / 32), dim3(256), 0, c->stream,
                                    dhist_rows, grid, dhist);
+                hipLaunchKernelGGL(kc_sel_span, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)dhist,
+                                   reinterpret_cast<uint32_t*>(stat + 4), dig256);
+            }
         });
         c->check_launch("kc_select");
     }
-    // one synchronisation: counts and the top-12-bit histogram together (pinned staging)
-    char* hp = static_cast<char*>(c->pinned_sel.ensure(64 + hb + 1024));
+    // one synchronisation: counts, the MSD digit span and its 256 digit counts (kc_sel_span) together
+    char* hp = static_cast<char*>(c->pinned_sel.ensure(64 + 1024));
     auto* hs = reinterpret_cast<unsigned long long*>(hp);
-    const uint32_t* h12 = reinterpret_cast<const uint32_t*>(hp + 64);
-    uint32_t* h256 = reinterpret_cast<uint32_t*>(hp + 64 + hb);
-    HGA_HIP(hipMemcpyAsync(hs, stat, msd ? 64 + hb : 64, hipMemcpyDeviceToHost, c->stream));
+    uint32_t* h256 = reinterpret_cast<uint32_t*>(hp + 64);
+    HGA_HIP(hipMemcpyAsync(hs, stat, 64, hipMemcpyDeviceToHost, c->stream));
+    if (msd) HGA_HIP(hipMemcpyAsync(h256, dig256, 1024, hipMemcpyDeviceToHost, c->stream));
     c->sync();
     const uint64_t n = hs[0];
     if (msd && n > 1) {
         // digit = (code >> shift) - dbase over the occupied 12-bit bins [lo, hi], <= 256 digits
-        uint32_t lo = 0, hi = SEL_HB - 1;
-        while (lo < hi && !h12[lo]) ++lo;
-        while (hi > lo && !h12[hi]) --hi;
-        int lg = 0;
-        while ((hi >> lg) - (lo >> lg) + 1 > 256) ++lg;
-        const int shift = bits - 12 + lg;
-        const uint32_t dbase = lo >> lg;
-        std::memset(h256, 0, 1024);
-        for (uint32_t b = lo; b <= hi; ++b) h256[(b >> lg) - dbase] += h12[b];
-        HGA_HIP(hipMemcpyAsync(dig256, h256, 1024, hipMemcpyHostToDevice, c->stream));
-        sort_export_u64(c, out, n, shift, dbase, dig256, h256, s.scratch);
+        const uint32_t* span = reinterpret_cast<const uint32_t*>(hs + 4);   // written at stat + 4
+        const int shift = bits - 12 + (int)span[2];
+        sort_export_u64(c, out, n, shift, span[3], dig256, h256, s.scratch);
     } else {
         radix_sort_u64(c, out, flag_bit ? nullptr : flag, n, bits, s.scratch);
     }
