@@ -1985,7 +1985,10 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     std::memcpy(hthr, thr.data(), n_thr * 8);
     if (fresh) HGA_HIP(hipMemsetAsync(base, 0, hbytes, c->stream));   // kept clear by kc_hist_compact
     HGA_HIP(hipMemsetAsync(ctrl, 0, 32, c->stream));
-    HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
+    if (fresh || s.thr_dev != thr) {   // the same thresholds as last time are already there
+        HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
+        s.thr_dev = thr;
+    }
     // an unsettled count_run: rows come from its device cursor, the counters ride in this readback
     const bool pend = s.pending;
     const uint64_t rows_hint = pend ? s.rows_cap : s.rows;
