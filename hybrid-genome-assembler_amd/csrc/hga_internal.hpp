@@ -198,6 +198,11 @@ struct hga_ctx {
     hga::PinnedBuf pinned;   // small host<->device staging (see count_spec_hist)
     hga::PinnedBuf pinned_sel;   // count_select counters + top-digit histogram
     std::unique_ptr<hga::Comm> comm;   // hga_comm_init*: the count results become global
+    // single-pass scans (sort.hip sc_onepass): per-tile status words tagged with the scan's epoch,
+    // and a tile counter that only ever grows (its value at a launch is passed as the tile base)
+    hga::DevBuf scan_state;
+    uint64_t scan_tiles = 0;
+    uint32_t scan_epoch = 0;
 
     // Launch helper: records events around the launch when profiling is on.
     template <class F>

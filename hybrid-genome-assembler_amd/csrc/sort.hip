@@ -374,94 +374,101 @@ __global__ void __launch_bounds__(SS_T) ss_segsort(const uint64_t* __restrict__ 
 }
 
 // ---- exclusive scans --------------------------------------------------------------
-template <class T>
-__global__ void __launch_bounds__(SC_T) sc_reduce(const T* __restrict__ in, uint64_t n,
-                                                  uint64_t* __restrict__ sums) {
-    __shared__ uint64_t ws[SC_T / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_I;
-    uint64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < SC_I; ++j)
-        if (base + j < n) s += (uint64_t)in[base + j];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    s = wave_incl_scan64(s, lane);
-    if (lane == 63) ws[wave] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (int w = 0; w < SC_T / 64; ++w) t += ws[w];
-        sums[blockIdx.x] = t;
-    }
-}
+// Single-pass exclusive scan (chained scan with decoupled look-back, one launch): each workgroup
+// takes the next tile id from a counter that only grows (tile = counter - the value at launch),
+// scans its SC_TILE elements, publishes its aggregate (A) and then its inclusive prefix (P) in a
+// 64-bit status word [flag 2 | epoch 22 | value 40] with agent-scope relaxed stores, after adding
+// the predecessors' words (newest first) until a P.  Words of other scans carry another epoch and
+// count as unpublished, so the status array is never cleared between scans (it is when the epoch
+// wraps).  A tile only waits on tiles with smaller ids, which have started.
+constexpr uint64_t SCS_A = 1ull << 62, SCS_P = 2ull << 62, SCS_F = 3ull << 62;
+constexpr uint64_t SCS_V = (1ull << 40) - 1;
+constexpr uint32_t SCS_EPOCHS = 1u << 22;
 
-// Exclusive scan of one tile with a carried-in block offset; in -> out (may alias).
 template <class T>
-__global__ void __launch_bounds__(SC_T) sc_scan(const T* in, T* out, uint64_t n,
-                                                const uint64_t* __restrict__ block_off) {
-    __shared__ uint64_t ws[SC_T / 64 + 1];
-    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_I;
+__global__ void __launch_bounds__(SC_T) sc_onepass(T* data, uint64_t n, unsigned long long* __restrict__ status,
+                                                   unsigned long long* __restrict__ ctr, uint64_t tbase,
+                                                   uint32_t epoch) {
+    __shared__ uint64_t ws[SC_T / 64];
+    __shared__ uint64_t s_tile, s_pre;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ctr, 1ull) - tbase;
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    const uint64_t base = tile * SC_TILE + (uint64_t)threadIdx.x * SC_I;
     uint64_t v[SC_I];
-    uint64_t s = 0;
+    uint64_t sum = 0;
 #pragma unroll
     for (int j = 0; j < SC_I; ++j) {
-        v[j] = base + j < n ? (uint64_t)in[base + j] : 0ull;
-        s += v[j];
+        v[j] = base + j < n ? (uint64_t)data[base + j] : 0ull;
+        sum += v[j];
     }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t inc = wave_incl_scan64(s, lane);
+    const uint64_t inc = wave_incl_scan64(sum, lane);
     if (lane == 63) ws[wave] = inc;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (int w = 0; w < SC_T / 64; ++w) { uint64_t x = ws[w]; ws[w] = t; t += x; }
+        uint64_t agg = 0;
+        for (int w = 0; w < SC_T / 64; ++w) {
+            const uint64_t x = ws[w];
+            ws[w] = agg;
+            agg += x;
+        }
+        const uint64_t tag = (uint64_t)epoch << 40;
+        unsigned long long* st = status + tile;
+        uint64_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(st, SCS_P | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st, SCS_A | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t t = (int64_t)tile - 1;
+            while (true) {
+                const uint64_t w = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t f = (((w >> 40) & (SCS_EPOCHS - 1)) == epoch) ? (w & SCS_F) : 0ull;
+                if (f == SCS_P) {
+                    excl += w & SCS_V;
+                    break;
+                }
+                if (f == SCS_A) {
+                    excl += w & SCS_V;
+                    --t;
+                }   // else: tile t has not published yet, read it again
+            }
+            __hip_atomic_store(st, SCS_P | tag | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_pre = excl;
     }
     __syncthreads();
-    uint64_t run = (block_off ? block_off[blockIdx.x] : 0ull) + ws[wave] + inc - s;
+    uint64_t run = s_pre + ws[wave] + inc - sum;
 #pragma unroll
     for (int j = 0; j < SC_I; ++j) {
-        if (base + j < n) out[base + j] = (T)run;
+        if (base + j < n) data[base + j] = (T)run;
         run += v[j];
     }
 }
 
 template <class T>
-uint64_t excl_scan_impl(hga_ctx* c, T* data, uint64_t n, DevBuf& scratch, size_t scratch_off) {
-    if (n == 0) return 0;
-    const uint64_t nb = (n + SC_TILE - 1) / SC_TILE;
-    // scratch layout: [sums(nb)] [recursive scratch...]
-    uint64_t* sums = reinterpret_cast<uint64_t*>(static_cast<char*>(scratch.p) + scratch_off);
-    uint64_t total = 0;
-    if (nb == 1) {
-        c->launch("scan", [&] {
-            hipLaunchKernelGGL(sc_scan<T>, dim3(1), dim3(SC_T), 0, c->stream, data, data, n,
-                               (const uint64_t*)nullptr);
-        });
-        c->check_launch("sc_scan");
-        // total = last exclusive + last input is lost in place; recompute via reduce
-    } else {
-        c->launch("scan", [&] {
-            hipLaunchKernelGGL(sc_reduce<T>, dim3((unsigned)nb), dim3(SC_T), 0, c->stream, data,
-                               n, sums);
-        });
-        c->check_launch("sc_reduce");
-        excl_scan_impl<uint64_t>(c, sums, nb, scratch, scratch_off + ((nb * 8 + 255) & ~255ull));
-        c->launch("scan", [&] {
-            hipLaunchKernelGGL(sc_scan<T>, dim3((unsigned)nb), dim3(SC_T), 0, c->stream, data,
-                               data, n, (const uint64_t*)sums);
-        });
-        c->check_launch("sc_scan");
+void excl_scan_impl(hga_ctx* c, T* data, uint64_t n) {
+    if (n == 0) return;
+    const uint64_t nt = (n + SC_TILE - 1) / SC_TILE;
+    const size_t need = 256 + nt * 8;
+    const bool fresh = need > c->scan_state.cap;
+    auto* st = static_cast<unsigned long long*>(c->scan_state.ensure(std::max<size_t>(need, 1 << 16)));
+    if (fresh) {   // a new allocation: zero words are unpublished under every epoch; the counter restarts
+        HGA_HIP(hipMemsetAsync(st, 0, c->scan_state.cap, c->stream));
+        c->scan_tiles = 0;
     }
-    (void)total;
-    return 0;
-}
-
-size_t scan_scratch_bytes(uint64_t n) {
-    size_t b = 0;
-    while (n > (uint64_t)SC_TILE) {
-        n = (n + SC_TILE - 1) / SC_TILE;
-        b += ((n * 8 + 255) & ~255ull);
+    if (++c->scan_epoch == SCS_EPOCHS) {   // wrap: clear the words of old scans
+        HGA_HIP(hipMemsetAsync(st + 32, 0, c->scan_state.cap - 256, c->stream));
+        c->scan_epoch = 1;
     }
-    return b + 256;
+    unsigned long long* ctr = st;        // first 256 B: the tile counter
+    unsigned long long* status = st + 32;
+    c->launch("scan", [&] {
+        hipLaunchKernelGGL(sc_onepass<T>, dim3((unsigned)nt), dim3(SC_T), 0, c->stream, data, n, status, ctr,
+                           c->scan_tiles, c->scan_epoch);
+    });
+    c->check_launch("sc_onepass");
+    c->scan_tiles += nt;
 }
 
 // n below which the onesweep path is used (env HGA_ONESWEEP_MAX overrides per call; 0 disables).
@@ -489,8 +496,7 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
     const size_t kb = ((n * sizeof(K) + 255) & ~255ull);
     const size_t vb = vals ? ((n * 4 + 255) & ~255ull) : 0;
     const size_t cb = ((n_cnt * 4 + 255) & ~255ull);
-    const size_t sb = scan_scratch_bytes(n_cnt);
-    char* base = static_cast<char*>(scratch.ensure(kb + vb + cb + sb));
+    char* base = static_cast<char*>(scratch.ensure(kb + vb + cb));
     K* k2 = reinterpret_cast<K*>(base);
     uint32_t* v2 = vals ? reinterpret_cast<uint32_t*>(base + kb) : nullptr;
     uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kb + vb);
@@ -567,7 +573,7 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
                                shift, dm, cnt, n_tiles);
         });
         c->check_launch("rs_upsweep");
-        excl_scan_impl<uint32_t>(c, cnt, n_cnt, scratch, kb + vb + cb);
+        excl_scan_impl<uint32_t>(c, cnt, n_cnt);
         if (vals) {
             c->launch("radix_downsweep", [&] {
                 hipLaunchKernelGGL((rs_downsweep<K, true>), dim3(n_tiles), dim3(RS_T), 0, c->stream,
@@ -657,8 +663,8 @@ void radix_sort_u32_from(hga_ctx* c, const uint32_t* src_k, const uint32_t* src_
     radix_sort_impl<uint32_t>(c, keys, vals, n, bits > 32 ? 32 : bits, scratch, src_k, src_v);
 }
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch) {
-    scratch.ensure(scan_scratch_bytes(n));
-    excl_scan_impl<uint64_t>(c, data, n, scratch, 0);
+    (void)scratch;   // the single-pass scan keeps its state in the ctx
+    excl_scan_impl<uint64_t>(c, data, n);
 }
 
 }  // namespace hga
