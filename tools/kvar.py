@@ -16,7 +16,7 @@ ctx = hga.Ctx(0); ctx.count_begin(19, 2); ctx.count_add(0, ra.seq); ctx.count_ad
 def step():
     try:
         return bench.count_step(ctx)
-    except hga.HgaError as e:   # timing-experiment builds (HGA_EXP_*) produce wrong data on purpose
+    except hga.HgaError as e:   # timing-experiment variants may produce wrong data on purpose
         return str(e)[:60]
 for _ in range(2): step()
 ctx.profile(True); ctx.profile_reset()
