@@ -149,7 +149,7 @@ def dist_count_step(ex):
 
 KERNEL_BYTES = {
     # algorithmic bytes per step, from the per-unit figures in DESIGN.md §4
-    "kc_bin1": lambda s: 0.375 * s["bytes"] + 4 * s["instances"],   # packed codes+valid read, 4 B/instance written
+    "kc_bin1": lambda s: 1.0 * s["bytes"] + 4 * s["instances"],   # ASCII bases read (packed in LDS), 4 B/instance written
     "kc_rebin": lambda s: 8 * s["instances"],                          # 4 B/instance read + 4 B written
     "kc_count": lambda s: 4 * s["instances"] + (8 + 4 * s["files"]) * s["rows"],   # read binned, write rows
 }
@@ -404,7 +404,7 @@ def scale_leg(dev, reps=2):
         c4.profile(True)
         c4.profile_reset()
         count_step(c4)
-        names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
+        names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
                  "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
         ker = {nm: round(c4.profile_get(nm)[0], 3) for nm in names if c4.profile_get(nm)[1]}
         c4.profile(False)
@@ -458,7 +458,7 @@ def main():
     st = ctx.count_stats()
     stats = {"bytes": st.bytes, "instances": st.instances, "rows": st.distinct_rows, "files": 2}
     # 1) untimed profiled pass: per-kernel breakdown (events around every launch)
-    names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
+    names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
              "kx_partition", "kx_piece_hist", "kx_pack_scatter", "kx_merge", "kx_mb_hist", "kx_mb_scatter",
              "kx_mb_merge", "kx_mb_compact", "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
     ctx.profile(True)

@@ -3,9 +3,10 @@
 // k-way merge passes of JellyfishOccurrenceReader (JellyfishOccurrenceReader.cpp:63-135).
 //
 // Pipeline (integer / byte work, no MFMA; DESIGN.md §4 has each kernel's bound):
-//   P  kc_pack   ASCII -> 2-bit codes (u32 per 16 bases) + base-valid bits (u16 per 16).
-//   B1 kc_bin1   per tile of 8K window ends: closed-form canonical k-mer of every valid
-//                window from packed frames, bijective 2k-bit mix; the top fb1 (<= 6) bits
+//   B1 kc_bin1   per tile of 8K window ends: the tile's ASCII bases packed once into LDS
+//                (2-bit codes + base-valid bits, 16 bases per thread, the next tile's bytes
+//                in flight meanwhile), closed-form canonical k-mer of every valid window
+//                from packed frames, bijective 2k-bit mix; the top fb1 (<= 6) bits
 //                pick a level-1 region, ranked through LDS so every region's run leaves as
 //                one coalesced segment (>= 512 B); space reserved with one returning atomic
 //                per (tile, region); per-fine-bucket histogram kept in LDS, flushed once.
@@ -146,7 +147,6 @@ __device__ __forceinline__ uint32_t new_block(unsigned long long* gstat, Blk* ta
 // One level-1 binning launch covers every file: workgroup w belongs to file f when
 // files[f].w0 <= w < files[f+1].w0 (file-major, so per-file runs stay contiguous).
 struct BinFile {
-    uint64_t woff;   // first word of the file's region in the packed buffers
     uint64_t n;      // bases
     uint32_t w0, pad;
     const uint8_t* seq;   // the file's ASCII bases
@@ -159,9 +159,7 @@ struct BinFile {
 #define HGA_B1_WAVES 1
 #endif
 template <class E1>
-__global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __restrict__ pk_all,
-                                                const uint16_t* __restrict__ vd_all,
-                                                const BinFile* __restrict__ files, uint32_t F,
+__global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __restrict__ files, uint32_t F,
                                                 uint64_t st_pos, KP kp,
                                                 Blk* __restrict__ table, uint64_t table_cap,
                                                 uint64_t pool_cap, E1* __restrict__ out1,
@@ -178,13 +176,13 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
     __shared__ uint32_t fhist[MAX_NB];
     __shared__ E1 stage[TP_B];
     __shared__ uint32_t ws[NT_B / 64 + 1];
+    // packed words [t0/16 - 2, t0/16 + 512) of this tile and the next (code | valid << 32)
+    __shared__ uint64_t lpw[2][TP_B / 16 + 2];
     const int tid = threadIdx.x;
     const uint32_t nb1 = kp.nb1, nb = kp.nb;
     const uint32_t w = blockIdx.x;
     uint32_t file = 0;
     while (file + 1 < F && files[file + 1].w0 <= w) ++file;
-    [[maybe_unused]] const uint32_t* __restrict__ pk = pk_all + files[file].woff;
-    [[maybe_unused]] const uint16_t* __restrict__ vd = vd_all + files[file].woff;
     const uint64_t n = files[file].n;
     const uint32_t tag0 = w << 8;
     for (uint32_t b = tid; b < nb; b += NT_B) fhist[b] = 0;
@@ -203,10 +201,49 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
     const uint64_t start = (uint64_t)(w - files[file].w0) * st_pos;
     const uint64_t end = start + st_pos < n ? start + st_pos : n;
     uint32_t inst = 0;
+    static_assert(P_B == 16 && Frame<P_B>::NW == 3, "one packed word per thread, frames of three");
+    const uint8_t* __restrict__ seq = files[file].seq;
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+    // tile t's words are packed into lpw[t & 1] while tile t-1 is binned, so the tile's own
+    // barriers publish them; the raw bytes of tile t+1 are in flight meanwhile
+    auto pack_into = [&](uint64_t* dst, const uint4 a, const uint4 h) {
+        uint32_t cw, vw;
+        pack_bytes<false>(a, cw, vw);
+        dst[tid + 2] = cw | ((uint64_t)vw << 32);
+        if (tid < 2) {
+            pack_bytes<false>(h, cw, vw);
+            dst[tid] = cw | ((uint64_t)vw << 32);
+        }
+    };
+    auto load_raw = [&](uint64_t t, uint4& a, uint4& h) {
+        a = z4;
+        h = z4;
+        if (t < end) {
+            a = load16(seq, (int64_t)(t + 16 * (uint64_t)tid), n);
+            if (tid < 2) h = load16(seq, (int64_t)t - 32 + 16 * tid, n);
+        }
+    };
+    uint4 nraw, nhalo;
+    load_raw(start, nraw, nhalo);
+    pack_into(lpw[0], nraw, nhalo);
+    load_raw(start + TP_B, nraw, nhalo);
+    lds_barrier();
+    uint32_t buf = 0;
     for (uint64_t t0 = start; t0 < end; t0 += TP_B) {
-        const uint64_t p0 = t0 + (uint64_t)tid * P_B;
         Frame<P_B> f;
-        const uint64_t v64 = load_frame<P_B, false>(pk, vd, PAD_WORDS + p0 / 16 - 2, kp.k, f);
+        FrameRaw<P_B> fr;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint64_t wv = lpw[buf][tid + i];
+            fr.x[i] = (uint32_t)wv;
+            fr.v[i] = (uint32_t)(wv >> 32);
+        }
+        if (t0 + TP_B < end) {
+            pack_into(lpw[buf ^ 1], nraw, nhalo);
+            load_raw(t0 + 2 * TP_B, nraw, nhalo);
+        }
+        buf ^= 1;
+        const uint64_t v64 = build_frame<P_B, false>(fr, kp.k, f);
         const uint32_t wm = (uint32_t)(runs_of(v64, kp.k) >> 32);   // bit j: window at p0+j valid
         uint32_t dd[P_B], rk[P_B];
         E1 ee[P_B];
@@ -274,49 +311,10 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const uint32_t* __
     if (tid == 0 && tot) atomicAdd(&gstat[4], (unsigned long long)tot);
 }
 
-// ---------------------------------------------------------------- pack
-// One launch packs every file into its [pad | words | tail] region of the shared buffers
-// (pad and tail zero = invalid) and initialises the pipeline counters.
-struct PackFile {
-    const uint8_t* seq;
-    uint64_t n, woff, nw;
-};
-#ifndef HGA_PK_W
-#define HGA_PK_W 4
-#endif
-constexpr int PK_W = HGA_PK_W;   // words per thread (grid-strided: every load instruction coalesced)
-__global__ void kc_pack_files(const PackFile* __restrict__ files, uint32_t F, uint64_t total_words,
-                              uint32_t* __restrict__ pk, uint16_t* __restrict__ vd,
-                              unsigned long long* __restrict__ gstat, uint64_t n_first) {
-    const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    if (g0 < 8) gstat[g0] = g0 == 3 ? (unsigned long long)n_first : 0ull;
-    uint4 raw[PK_W];
-    PackFile pf[PK_W];
-    uint64_t wl[PK_W];
-    bool in[PK_W];
-#pragma unroll
-    for (int u = 0; u < PK_W; ++u) {   // all loads first
-        const uint64_t g = g0 + (uint64_t)u * stride;
-        uint32_t f = 0;
-        while (f + 1 < F && files[f + 1].woff <= g) ++f;
-        pf[u] = files[f];
-        wl[u] = g - pf[u].woff;
-        in[u] = g < total_words && wl[u] >= (uint64_t)PAD_WORDS && wl[u] - PAD_WORDS < pf[u].nw;
-        raw[u] = in[u] ? load16(pf[u].seq, (int64_t)((wl[u] - PAD_WORDS) * 16), pf[u].n) : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int u = 0; u < PK_W; ++u) {
-        const uint64_t g = g0 + (uint64_t)u * stride;
-        if (g >= total_words) continue;
-        uint32_t code = 0, valid = 0;
-        if (in[u]) pack_bytes<false>(raw[u], code, valid);
-        pk[g] = code;
-        vd[g] = (uint16_t)valid;
-    }
+// Pipeline counters: gstat[3] = the first spill block, the rest 0.
+__global__ void kc_init_stat(unsigned long long* __restrict__ gstat, uint64_t n_first) {
+    if (threadIdx.x < 8) gstat[threadIdx.x] = threadIdx.x == 3 ? (unsigned long long)n_first : 0ull;
 }
-
-// Pipeline counters when there is no pack pass: gstat[3] = the first spill block, the rest 0.
 // ---------------------------------------------------------------- layout
 // off[b * W + w] = wcnt[w * nb + b] (64 x 64 LDS tiles), off[nb * W] = 0.  One exclusive scan
 // of off then gives every (fine bucket, workgroup) its first output slot: buckets in order,
@@ -1655,7 +1653,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     auto& s = c->count;
     HGA_REQUIRE(s.begun, HGA_ERR_STATE, "hga_count_begin not called");
     // A previous run nobody consumed is discarded, errors included: this run replaces its rows
-    // (the stream is in order, and kc_pack re-initialises the counters it would have read).
+    // (the stream is in order, and kc_init_stat re-initialises the counters it would have read).
     s.pending = false;
     const uint32_t F = s.n_files;
     s.min_per_file = min_per_file;
@@ -1711,31 +1709,17 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     uint32_t* wcnt = static_cast<uint32_t*>(s.fine_hist.ensure((size_t)std::max<uint32_t>(W, 1) * nb * 4));
     auto* off = static_cast<unsigned long long*>(s.cursor2.ensure(((size_t)W * nb + 1) * 8));
     uint32_t* nblk = static_cast<uint32_t*>(s.nblk.ensure((size_t)std::max<uint32_t>(W, 1) * nb1 * 4));
-    // P: pack every file (2-bit codes + valid bits) into one buffer (one kernel argument, so
-    // kc_bin1's loads stay global loads), each file [pad | words | tail], pad/tail zero (= invalid)
-    const uint64_t tail_words = ST_ALIGN / 16 + 8;
-    std::vector<uint64_t> woff(F + 1, 0);
-    for (uint32_t f = 0; f < F; ++f) woff[f + 1] = woff[f] + PAD_WORDS + (s.seq_len[f] + 15) / 16 + tail_words;
-    uint32_t* pk_all = static_cast<uint32_t*>(s.pk_all.ensure(woff[F] * 4));
-    uint16_t* vd_all = static_cast<uint16_t*>(s.vd_all.ensure(woff[F] * 2));
-    std::vector<PackFile> pf(F);
-    for (uint32_t f = 0; f < F; ++f) {
-        pf[f] = PackFile{s.seq[f]->as<uint8_t>(), s.seq_len[f], woff[f], (s.seq_len[f] + 15) / 16};
-        bf[f].woff = woff[f];
-        bf[f].seq = s.seq[f]->as<uint8_t>();
-    }
+    for (uint32_t f = 0; f < F; ++f) bf[f].seq = s.seq[f]->as<uint8_t>();
     // per-file tables: uploaded only when they change (they are fixed for repeated runs)
-    const size_t tb = sizeof(BinFile) * F + sizeof(PackFile) * F;
+    const size_t tb = sizeof(BinFile) * F;
     std::vector<char> tab(tb);
-    std::memcpy(tab.data(), bf.data(), sizeof(BinFile) * F);
-    std::memcpy(tab.data() + sizeof(BinFile) * F, pf.data(), sizeof(PackFile) * F);
+    std::memcpy(tab.data(), bf.data(), tb);
     char* d_tab = static_cast<char*>(s.bin_files.ensure(tb));
     if (s.tab_host != tab) {
         HGA_HIP(hipMemcpy(d_tab, tab.data(), tb, hipMemcpyHostToDevice));
         s.tab_host = tab;
     }
     BinFile* d_bf = reinterpret_cast<BinFile*>(d_tab);
-    const PackFile* d_pf = reinterpret_cast<const PackFile*>(d_tab + sizeof(BinFile) * F);
 
     const size_t esz1 = e1_32 ? 4 : 8, esz = e32 ? 4 : 8;
     uint64_t cap = (total_bytes / std::max<uint32_t>(1, min_per_file) + 4) & ~3ull;   // x4: 16-B row groups
@@ -1755,21 +1739,18 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const uint64_t pool_cap = table_cap * BLK;
     void* binned1 = s.binned1.ensure(pool_cap * esz1);
     Blk* table = static_cast<Blk*>(s.regions.ensure(table_cap * sizeof(Blk)));
-    // P: pack all files + counter init, one launch
-    c->launch("kc_pack", [&] {
-        hipLaunchKernelGGL(kc_pack_files, dim3(blocks_for(std::max<uint64_t>(woff[F], 8), 256 * PK_W)), dim3(256),
-                           0, c->stream, d_pf, F, woff[F], pk_all, vd_all, gstat, n_first);
-    });
-    c->check_launch("kc_pack");
+    // pipeline counters (the ASCII bases are packed inside kc_bin1)
+    c->launch("kc_init", [&] { hipLaunchKernelGGL(kc_init_stat, dim3(1), dim3(64), 0, c->stream, gstat, n_first); });
+    c->check_launch("kc_init");
 
     // B1: level-1 binning of every file into pool blocks + per-workgroup fine histograms
     if (W) {
         c->launch("kc_bin1", [&] {
             if (e1_32)
-                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(W), dim3(NT_B), 0, c->stream, pk_all, vd_all, d_bf, F, st_pos, kp, table,
+                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
                                    table_cap, pool_cap, static_cast<uint32_t*>(binned1), wcnt, nblk, gstat);
             else
-                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(W), dim3(NT_B), 0, c->stream, pk_all, vd_all, d_bf, F, st_pos, kp, table,
+                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
                                    table_cap, pool_cap, static_cast<uint64_t*>(binned1), wcnt, nblk, gstat);
         });
         c->check_launch("kc_bin1");

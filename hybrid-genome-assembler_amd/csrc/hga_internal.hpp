@@ -126,7 +126,7 @@ struct CountState {
     std::vector<uint64_t> seq_len;
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
-        sel_keys, sel_tmp, sel_wtmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, pk_all, vd_all, blist,
+        sel_keys, sel_tmp, sel_wtmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, blist,
         binned3, file_start3, xsend, xrecv;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;

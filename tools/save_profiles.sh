@@ -12,5 +12,5 @@ cp gpurun_out/pmc_$TAG/pmc_*.json profiles/
 tail -3 gpurun_out/pytest_$TAG.log > profiles/${TAG}_pytest_gpu.txt
 # SQ / LDS counter passes (tools/gpu_pmc_sq.sh, tools/gpu_pmc_lds.sh), when present
 [ -f gpurun_out/pmc_$TAG.json ] && cp gpurun_out/pmc_$TAG.json profiles/${TAG}_sq_pmc.json
-ls -d gpurun_out/pmc_${TAG}_SQ_* >/dev/null 2>&1 && python3 tools/pmc_raw.py "gpurun_out/pmc_${TAG}_SQ_*" kc_pack_files kc_bin1 kc_rebin kc_count_s kc_spec_hist kc_select rs_onesweep ss_segsort lk_scan hll_scan cn_wave > profiles/${TAG}_sq_lds_counters.txt
+ls -d gpurun_out/pmc_${TAG}_SQ_* >/dev/null 2>&1 && python3 tools/pmc_raw.py "gpurun_out/pmc_${TAG}_SQ_*" kc_bin1 kc_rebin kc_count_s kc_spec_hist kc_select rs_onesweep ss_segsort lk_scan hll_scan cn_wave > profiles/${TAG}_sq_lds_counters.txt
 true

@@ -50,7 +50,7 @@ def run_k(ctx, k, ra, rb, reps):
         ctx.sync()
         ms = (time.perf_counter() - t) * 1e3
         st = ctx.count_stats()
-        names = ("kc_pack", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
+        names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
                  "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
         ker = {nm: round(ctx.profile_get(nm)[0], 3) for nm in names if ctx.profile_get(nm)[1]}
         print(f"k={k} rep {rep}: {ms:.2f} ms, {st.instances / ms / 1e6:.1f} G k-mers/s, instances {st.instances}, "
