@@ -83,7 +83,7 @@ __device__ __forceinline__ uint4 load16(const uint8_t* s, int64_t base, uint64_t
 }
 
 // ---------------------------------------------------------------- packed frames (K1/K2)
-// The sequence stream is packed once (kc_pack / lk_pack): per 16 bases one u32 of 2-bit
+// The sequence stream is packed once (lk_pack; kc_bin1 per tile into LDS): per 16 bases one u32 of 2-bit
 // codes (first base in the top bits) and one u16 of base-valid bits (bit b = base b).
 // Two leading pad words (all invalid) let every frame read two words before its start.
 constexpr int PAD_WORDS = 2;
@@ -200,7 +200,7 @@ __device__ __forceinline__ uint64_t load_frame(const uint32_t* __restrict__ pk,
     return build_frame<P, REF>(r, k, f);
 }
 
-// ASCII -> packed frames (kc_pack / lk_pack).  REF = KmerIterator semantics (upper-case
+// ASCII -> packed frames (lk_pack, kc_bin1).  REF = KmerIterator semantics (upper-case
 // ACGT only), otherwise jellyfish semantics (either case).
 // One thread per 16 bases: packed codes (first base in bits 31:30) and valid bits.
 // 16 bases starting at 16w -> 2-bit codes (MSB-first) + valid bits.
