@@ -51,6 +51,9 @@ constexpr uint64_t ST_ALIGN = TP_B;    // super-tiles are whole tiles
 #ifndef HGA_LDS_TAB_KB
 #define HGA_LDS_TAB_KB 128
 #endif
+#ifndef HGA_PB_P
+#define HGA_PB_P 65536
+#endif
 constexpr int MAX_FB = HGA_MAX_FB;
 constexpr int MAX_NB = 1 << MAX_FB;
 #ifndef HGA_MAX_FB1
@@ -951,7 +954,13 @@ constexpr uint32_t MAXPROBE_P = 64;     // groups probed before the table counts
 // reads 4 keys with one ds_read_b128, a hit is one ds_add_u32 on the count word (32 banks
 // for the count array instead of the odd half of 64), a claim is ds_cmpst_b32 on the key then
 // the add.
-constexpr uint32_t T_S = 8192;          // slots (32 KB keys + 32 KB counts)
+#ifndef HGA_T_S
+#define HGA_T_S 8192
+#endif
+#ifndef HGA_CS_WAVES
+#define HGA_CS_WAVES 4
+#endif
+constexpr uint32_t T_S = HGA_T_S;       // slots (32 KB keys + 32 KB counts)
 constexpr uint32_t GS_S = 4;            // keys per probe group (one ds_read_b128)
 constexpr uint32_t G_S = T_S / GS_S;
 
@@ -994,7 +1003,7 @@ __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t
     return false;
 }
 
-__global__ void __launch_bounds__(NT_P, 4) kc_count_s(const uint32_t* __restrict__ binned,
+__global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t* __restrict__ binned,
                                                       const uint64_t* __restrict__ fs, uint32_t F,
                                                       uint32_t min_count, KP kp, uint64_t* __restrict__ out_key,
                                                       uint32_t* __restrict__ out_cnt, uint64_t cap,
@@ -1670,7 +1679,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     // packed-count counting (kc_count_s): F <= 2 and u32 remainders; ~64K windows per bucket
     const bool legacy = std::getenv("HGA_COUNT_LEGACY") != nullptr;   // test hook: generic kc_count for F <= 2
     const bool packed = F <= 2 && nbits - std::min<uint32_t>(MAX_FB, nbits) <= 31 && !legacy;
-    const uint64_t per_bucket = packed ? 65536 : 16384;
+    const uint64_t per_bucket = packed ? HGA_PB_P : 16384;
     uint32_t fb = 0, fb_max = MAX_FB;
     if (const char* e = std::getenv("HGA_FB_MAX")) fb_max = std::min<uint32_t>(MAX_FB, (uint32_t)std::atoi(e));
     while (fb < fb_max && fb < nbits && (total_bytes >> fb) > per_bucket) ++fb;
