@@ -365,10 +365,16 @@ __global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint3
 // owner-map state, so a workgroup walks four pivots at once without workgroup barriers (a
 // wave's LDS accesses are ordered) and a CU keeps ~28 pivots' dependent load chains in flight.
 // A pivot whose distinct candidates pass 3/4 of the table goes to the cn_local list.
-constexpr uint32_t CNW_CAP = 512;
+#ifndef HGA_CNW_CAP
+#define HGA_CNW_CAP 512
+#endif
+#ifndef HGA_CNW_WAVES
+#define HGA_CNW_WAVES 4
+#endif
+constexpr uint32_t CNW_CAP = HGA_CNW_CAP;
 constexpr uint32_t CNW_W = 512;            // pairs per owner-map window
 constexpr int CNW_U = CNW_W / 64;
-constexpr int CNW_WAVES = 4;
+constexpr int CNW_WAVES = HGA_CNW_WAVES;
 constexpr uint32_t CNW_GRAB = 8;         // pivots per work-counter atomic
 
 struct CnWaveLds {
