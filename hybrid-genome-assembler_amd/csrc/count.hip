@@ -2057,7 +2057,12 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     // flag rides in the key; kc_select counts the kept keys by the top 12 bits of the code
     const bool msd = flag_bit && bits >= 16 && s.rows >= (1u << 15);
     const uint64_t chunks = blocks_for(std::max<uint64_t>(s.rows, 1), NT_H * SEL_R);
-    const uint32_t cpw = (uint32_t)blocks_for(chunks, HGA_SEL_GRID);   // chunks per workgroup
+    if (!s.sel_grid) {   // one resident round of workgroups: a second, partial round would run alone
+        int nb = 0;      // (C4 shard: 1024 workgroups at 3 per CU took two rounds)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kc_select, NT_H, 0) != hipSuccess || nb < 1) nb = 1;
+        s.sel_grid = (uint32_t)std::min<uint64_t>((uint64_t)nb * c->num_cu, HGA_SEL_GRID);
+    }
+    const uint32_t cpw = (uint32_t)blocks_for(chunks, s.sel_grid);   // chunks per workgroup
     const unsigned grid = (unsigned)blocks_for(chunks, cpw);
     const uint64_t region = (uint64_t)cpw * NT_H * SEL_R;
     const size_t hb = (size_t)SEL_HB * 4;
