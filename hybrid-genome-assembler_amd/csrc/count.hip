@@ -1340,7 +1340,8 @@ __global__ void __launch_bounds__(NT_S) kc_spec_hist(const uint32_t* __restrict_
 constexpr int NT_HC = 256;
 __global__ void __launch_bounds__(NT_HC) kc_hist_compact(unsigned long long* __restrict__ hist, uint32_t n_thr,
                                                          unsigned long long* __restrict__ out,
-                                                         unsigned long long* __restrict__ ctrl, uint64_t cap) {
+                                                         unsigned long long* __restrict__ ctrl, uint64_t cap,
+                                                         unsigned long long* __restrict__ hout, uint64_t hcap) {
     __shared__ uint32_t ws[NT_HC / 64 + 1];
     __shared__ unsigned long long s_base;
     const uint64_t i = (uint64_t)blockIdx.x * NT_HC + threadIdx.x;
@@ -1361,6 +1362,22 @@ __global__ void __launch_bounds__(NT_HC) kc_hist_compact(unsigned long long* __r
         out[2 * o] = ((unsigned long long)ti << 56) | tot;
         out[2 * o + 1] = v;
     }
+    if (v && o < hcap) {   // the first triples also straight into the host's mapped staging
+        hout[2 * o] = ((unsigned long long)ti << 56) | tot;
+        hout[2 * o + 1] = v;
+    }
+}
+
+// The spec_hist counters (and an unsettled count_run's) into the host's mapped staging, then ctrl
+// cleared for the next call: no copy or fill operations in the step.
+__global__ void kc_spec_publish(unsigned long long* __restrict__ ctrl, const unsigned long long* __restrict__ run,
+                                unsigned long long* __restrict__ hctrl, unsigned long long* __restrict__ hrun) {
+    const uint32_t t = threadIdx.x;
+    if (t < 4) {
+        hctrl[t] = ctrl[t];
+        ctrl[t] = 0;
+    }
+    if (run && t < 8) hrun[t] = run[t];
 }
 
 #ifndef HGA_SEL_GRID
@@ -1402,8 +1419,14 @@ __global__ void __launch_bounds__(NT_H) kc_select(const uint64_t* __restrict__ k
                                                   int64_t upper, uint64_t* __restrict__ wkeys,
                                                   uint32_t* __restrict__ wflag, bool flag_bit, uint32_t cpw,
                                                   unsigned long long* __restrict__ wcnt,
-                                                  uint32_t* __restrict__ dhist_rows, int hshift) {
+                                                  uint32_t* __restrict__ dhist_rows, int hshift,
+                                                  unsigned long long* __restrict__ zstat, uint32_t* __restrict__ zdh) {
     __shared__ uint32_t ws[NT_H / 64 + 1];
+    // clear what the next kernels of the select accumulate into (kc_sel_compact: stat; kc_dhist_reduce:
+    // the 12-bit histogram) — nothing here reads them
+    if (blockIdx.x == 0 && threadIdx.x < 8) zstat[threadIdx.x] = 0;
+    if (zdh)
+        for (uint32_t i = blockIdx.x * NT_H + threadIdx.x; i < SEL_HB; i += gridDim.x * NT_H) zdh[i] = 0;
     __shared__ uint64_t stage[NT_H * SEL_R];
     __shared__ uint8_t sflag[NT_H * SEL_R];
     __shared__ uint32_t dh[SEL_HB];
@@ -1549,7 +1572,8 @@ __global__ void __launch_bounds__(256) kc_dhist_reduce(const uint32_t* __restric
 // and the 256 digit counts dig[d] = sum of bins b in [lo, hi] with (b >> lg) - dbase == d.
 // span = {lo, hi, lg, dbase}; all zero when no key was kept.  One 256-thread workgroup.
 __global__ void __launch_bounds__(256) kc_sel_span(const uint32_t* __restrict__ hist, uint32_t* __restrict__ span,
-                                                   uint32_t* __restrict__ dig) {
+                                                   uint32_t* __restrict__ dig, const unsigned long long* __restrict__ stat,
+                                                   unsigned long long* __restrict__ hstat, uint32_t* __restrict__ hdig) {
     __shared__ uint32_t s_lo[4], s_hi[4];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint32_t lo = 0xFFFFFFFFu, hi = 0;
@@ -1570,9 +1594,17 @@ __global__ void __launch_bounds__(256) kc_sel_span(const uint32_t* __restrict__ 
     __syncthreads();
     lo = min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3]));
     hi = max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3]));
+    // the counts (stat[0..1], from kc_sel_compact), span (stat + 4) and digit counts also go straight
+    // into the host's mapped staging
+    auto publish = [&](uint32_t d) {
+        dig[t] = d;
+        hdig[t] = d;
+        __syncthreads();   // span (thread 0) before the copy of stat
+        if (t < 8) hstat[t] = stat[t];
+    };
     if (lo > hi) {   // nothing kept
-        dig[t] = 0;
         if (t < 4) span[t] = 0;
+        publish(0u);
         return;
     }
     uint32_t lg = 0;
@@ -1582,13 +1614,13 @@ __global__ void __launch_bounds__(256) kc_sel_span(const uint32_t* __restrict__ 
     const uint32_t b0 = (dbase + t) << lg;
     for (uint32_t b = b0; b < b0 + (1u << lg); ++b)
         if (b >= lo && b <= hi) sum += hist[b];
-    dig[t] = sum;
     if (t == 0) {
         span[0] = lo;
         span[1] = hi;
         span[2] = lg;
         span[3] = dbase;
     }
+    publish(sum);
 }
 
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
@@ -1973,8 +2005,8 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     auto* hcomp = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8 + 32);
     auto* hrun = reinterpret_cast<unsigned long long*>(hp + MAX_THR * 8 + 32 + SPEC_CHUNK * 16);
     std::memcpy(hthr, thr.data(), n_thr * 8);
-    if (fresh) HGA_HIP(hipMemsetAsync(base, 0, hbytes, c->stream));   // kept clear by kc_hist_compact
-    HGA_HIP(hipMemsetAsync(ctrl, 0, 32, c->stream));
+    // hist is kept clear by kc_hist_compact, ctrl by kc_spec_publish
+    if (fresh) HGA_HIP(hipMemsetAsync(base, 0, hbytes + over_cap * 8 + 256, c->stream));
     if (fresh || s.thr_dev != thr) {   // the same thresholds as last time are already there
         HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
         s.thr_dev = thr;
@@ -1998,13 +2030,14 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     const uint64_t nd = (uint64_t)n_thr * TD;
     c->launch("kc_spec_hist", [&] {
         hipLaunchKernelGGL(kc_hist_compact, dim3(blocks_for(nd, NT_HC)), dim3(NT_HC), 0, c->stream, hist, n_thr, comp,
-                           ctrl, ncap);
+                           ctrl, ncap, c->pinned.dev(hcomp), SPEC_CHUNK);
+        // one synchronisation: counters and (speculatively) the first chunk of triples together,
+        // written into the mapped staging by the kernels themselves
+        hipLaunchKernelGGL(kc_spec_publish, dim3(1), dim3(64), 0, c->stream, ctrl,
+                           pend ? static_cast<const unsigned long long*>(s.cursor.p) : nullptr, c->pinned.dev(hc),
+                           c->pinned.dev(hrun));
     });
     c->check_launch("kc_hist_compact");
-    // one synchronisation: counters and (speculatively) the first chunk of triples together
-    HGA_HIP(hipMemcpyAsync(hc, ctrl, 32, hipMemcpyDeviceToHost, c->stream));
-    HGA_HIP(hipMemcpyAsync(hcomp, comp, SPEC_CHUNK * 16, hipMemcpyDeviceToHost, c->stream));
-    if (pend) HGA_HIP(hipMemcpyAsync(hrun, s.cursor.p, 64, hipMemcpyDeviceToHost, c->stream));
     c->sync();
     if (pend) count_settle(c, hrun);
     HGA_REQUIRE(!(hc[1] & 1ull), HGA_ERR_INVALID, "a row's specificity is above the last threshold");
@@ -2075,12 +2108,15 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     uint32_t* dhist = reinterpret_cast<uint32_t*>(tb + 64);                // SEL_HB top-12-bit counts
     uint32_t* dig256 = reinterpret_cast<uint32_t*>(tb + 64 + hb);          // the MSD digit counts
     uint32_t* dhist_rows = msd ? reinterpret_cast<uint32_t*>(tb + 64 + hb + 1024) : nullptr;
-    HGA_HIP(hipMemsetAsync(stat, 0, 64 + (msd ? hb : 0), c->stream));
+    char* hp = static_cast<char*>(c->pinned_sel.ensure(64 + 1024));
+    auto* hs = reinterpret_cast<unsigned long long*>(hp);
+    uint32_t* h256 = reinterpret_cast<uint32_t*>(hp + 64);
+    if (!s.rows) HGA_HIP(hipMemsetAsync(stat, 0, 64, c->stream));   // else kc_select clears stat and dhist
     if (s.rows) {
         c->launch("kc_select", [&] {
             hipLaunchKernelGGL(kc_select, dim3(grid), dim3(NT_H), 0, c->stream, s.rows_key.as<uint64_t>(),
                                s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, lower, upper, wkeys, wflag,
-                               flag_bit, cpw, wcnt, dhist_rows, bits - 12);
+                               flag_bit, cpw, wcnt, dhist_rows, bits - 12, stat, msd ? dhist : nullptr);
             hipLaunchKernelGGL(kc_sel_compact, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys,
                                (const uint32_t*)wflag, region, (const unsigned long long*)wcnt, grid, out, flag,
                                flag_bit, stat);
@@ -2088,17 +2124,15 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
                 hipLaunchKernelGGL(kc_dhist_reduce, dim3(SEL_HB / 256, (grid + 31) / 32), dim3(256), 0, c->stream,
                                    dhist_rows, grid, dhist);
                 hipLaunchKernelGGL(kc_sel_span, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)dhist,
-                                   reinterpret_cast<uint32_t*>(stat + 4), dig256);
+                                   reinterpret_cast<uint32_t*>(stat + 4), dig256, (const unsigned long long*)stat,
+                                   c->pinned_sel.dev(hs), c->pinned_sel.dev(h256));
             }
         });
         c->check_launch("kc_select");
     }
-    // one synchronisation: counts, the MSD digit span and its 256 digit counts (kc_sel_span) together
-    char* hp = static_cast<char*>(c->pinned_sel.ensure(64 + 1024));
-    auto* hs = reinterpret_cast<unsigned long long*>(hp);
-    uint32_t* h256 = reinterpret_cast<uint32_t*>(hp + 64);
-    HGA_HIP(hipMemcpyAsync(hs, stat, 64, hipMemcpyDeviceToHost, c->stream));
-    if (msd) HGA_HIP(hipMemcpyAsync(h256, dig256, 1024, hipMemcpyDeviceToHost, c->stream));
+    // one synchronisation: counts, the MSD digit span and its 256 digit counts together (kc_sel_span
+    // writes them into the mapped staging; without it, one copy)
+    if (!(s.rows && msd)) HGA_HIP(hipMemcpyAsync(hs, stat, 64, hipMemcpyDeviceToHost, c->stream));
     c->sync();
     const uint64_t n = hs[0];
     if (msd && n > 1) {

@@ -76,9 +76,18 @@ struct PinnedBuf {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        HGA_HIP(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault));
+        // mapped + coherent: small results are also written straight into it by kernels (device
+        // address from dev()), read by the host after the stream is synchronised
+        HGA_HIP(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocMapped | hipHostMallocCoherent));
         cap = bytes ? bytes : 16;
+        HGA_HIP(hipHostGetDevicePointer(&dp, p, 0));
         return p;
+    }
+    void* dp = nullptr;   // device address of p
+    // device address of host address h inside the buffer
+    template <class T>
+    T* dev(T* h) const {
+        return reinterpret_cast<T*>(static_cast<char*>(dp) + (reinterpret_cast<char*>(h) - static_cast<char*>(p)));
     }
 };
 
