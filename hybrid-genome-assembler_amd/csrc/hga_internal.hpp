@@ -294,7 +294,8 @@ void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch)
 void count_settle(hga_ctx* c, const unsigned long long* h = nullptr);
 // stable per-segment sort by the low kbits of sk (lookup.hip); false when a segment passes 16384
 bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxlen, int kbits, uint64_t* sk,
-                  uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label);
+                  uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label,
+                  uint32_t* lists = nullptr, const unsigned long long* lists_n = nullptr);
 void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t dbase, const uint32_t* d_hist,
                      const uint32_t* h_hist, DevBuf& scratch);
 }  // namespace hga

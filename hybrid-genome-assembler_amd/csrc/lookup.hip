@@ -517,6 +517,34 @@ __global__ void __launch_bounds__(1024) lk_nonempty(const uint64_t* __restrict__
     }
 }
 
+// lk_nonempty + the reads with more than 512 / 2048 hits listed for the per-read sort tiers (order
+// irrelevant; one list atomic per workgroup): out[0] non-empty reads, out[1] largest, out[2] / out[3]
+// the two list lengths — all read back with one synchronisation.
+__global__ void __launch_bounds__(1024) lk_seg_stats(const uint64_t* __restrict__ ptr, uint64_t nseg,
+                                                     unsigned long long* __restrict__ out, uint32_t* __restrict__ mid,
+                                                     uint32_t* __restrict__ big, uint32_t lo_mid, uint32_t lo_big) {
+    __shared__ uint32_t ws[1024 / 64 + 1];
+    __shared__ unsigned long long smax, s_mid, s_big;
+    const uint64_t s = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+    const uint64_t len = s < nseg ? ptr[s + 1] - ptr[s] : 0;
+    if (threadIdx.x == 0) smax = 0;
+    __syncthreads();
+    if (len) atomicMax(&smax, (unsigned long long)len);
+    uint32_t tot, nm, nbg;
+    (void)block_excl_scan<1024>(len ? 1u : 0u, ws, &tot);
+    const uint32_t em = block_excl_scan<1024>(len > lo_mid ? 1u : 0u, ws, &nm);
+    const uint32_t eb = block_excl_scan<1024>(len > lo_big ? 1u : 0u, ws, &nbg);
+    if (threadIdx.x == 0) {
+        if (tot) atomicAdd(&out[0], (unsigned long long)tot);
+        if (smax) atomicMax(&out[1], smax);
+        s_mid = nm ? atomicAdd(&out[2], (unsigned long long)nm) : 0ull;
+        s_big = nbg ? atomicAdd(&out[3], (unsigned long long)nbg) : 0ull;
+    }
+    __syncthreads();
+    if (len > lo_mid) mid[s_mid + em] = (uint32_t)s;
+    if (len > lo_big) big[s_big + eb] = (uint32_t)s;
+}
+
 // Reads with more than `lo` hits (order irrelevant).
 __global__ void lk_big_reads(const uint64_t* __restrict__ hptr, uint64_t n, uint64_t lo,
                              uint32_t* __restrict__ list, unsigned long long* __restrict__ cnt) {
@@ -798,7 +826,8 @@ inline int bits_for(uint64_t n) {   // bits to hold values in [0, n)
 // up to 512 entries, listed segments on 256- and 1024-thread workgroups above.  Leaves
 // sk = s << kbits | key (segments of one entry are not touched: sk must arrive composed).  maxlen ~0: measured here.  `ctr2`: two device counters of scratch.
 bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxlen, int kbits, uint64_t* sk,
-                  uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label) {
+                  uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label, uint32_t* lists,
+                  const unsigned long long* lists_n) {
     if (maxlen == ~0ull) {   // unknown: the longest segment first
         unsigned long long h2[2] = {0, 0};
         HGA_HIP(hipMemsetAsync(ctr2, 0, 16, c->stream));
@@ -812,7 +841,12 @@ bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxl
     uint32_t* mid = nullptr;
     uint32_t* big = nullptr;
     unsigned long long nl[2] = {0, 0};
-    if (maxlen > 64u * WIPT) {
+    if (maxlen > 64u * WIPT && lists) {   // listed by the caller (lk_seg_stats)
+        mid = lists;
+        big = lists + nseg;
+        nl[0] = lists_n[0];
+        nl[1] = lists_n[1];
+    } else if (maxlen > 64u * WIPT) {
         mid = static_cast<uint32_t*>(list_buf.ensure(2 * nseg * 4 + 64));
         big = mid + nseg;
         HGA_HIP(hipMemsetAsync(ctr2, 0, 16, c->stream));
@@ -983,10 +1017,13 @@ void lookup_run(hga_ctx* c) {
     auto* ctr = static_cast<unsigned long long*>(L.first_flag.ensure(64));
     HGA_HIP(hipMemsetAsync(ctr, 0, 32, c->stream));
     uint64_t* hptr = static_cast<uint64_t*>(L.hit_ptr.ensure((n + 1) * 8));
+    // reads listed for the per-read sort tiers: mid (> 64 * WIPT hits) then big (> 2048), n entries each
+    uint32_t* lists = static_cast<uint32_t*>(L.big_list.ensure(2 * std::max<uint64_t>(n, 1) * 4 + 64));
     c->launch("lk_post", [&] {
         hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(H + 1, 256)), dim3(256), 0, c->stream, hr, H, n, hptr);
         if (n)
-            hipLaunchKernelGGL(lk_nonempty, dim3(blocks_for(n, 1024)), dim3(1024), 0, c->stream, hptr, n, ctr);
+            hipLaunchKernelGGL(lk_seg_stats, dim3(blocks_for(n, 1024)), dim3(1024), 0, c->stream, hptr, n, ctr, lists,
+                               lists + n, (uint32_t)(64 * WIPT), 2048u);
     });
     c->check_launch("lk_ptr");
     const int rbits = bits_for(std::max<uint64_t>(n, 1));
@@ -994,10 +1031,10 @@ void lookup_run(hga_ctx* c) {
     uint64_t U = 0;
     if (H) {
         // per-read (read, KmerID) sort of the emitted (read << kbits | KmerID, position) pairs
-        unsigned long long mx[2];
-        HGA_HIP(hipMemcpyAsync(mx, ctr, 16, hipMemcpyDeviceToHost, c->stream));
+        unsigned long long mx[4];   // non-empty reads, most hits, the two tier lists' lengths: one sync
+        HGA_HIP(hipMemcpyAsync(mx, ctr, 32, hipMemcpyDeviceToHost, c->stream));
         c->sync();
-        if (!segment_sort(c, hptr, n, mx[1], kbits, sk, sv, L.big_list, ctr + 2, "lk_sort"))
+        if (!segment_sort(c, hptr, n, mx[1], kbits, sk, sv, L.big_list, ctr + 4, "lk_sort", lists, mx + 2))
             radix_sort_u64(c, sk, sv, H, kbits + rbits, L.scratch2);   // a read with > 16384 hits
         uint32_t* skid = static_cast<uint32_t*>(L.s_val2.ensure(H * 4));
         uint64_t* fptr0 = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
@@ -1008,11 +1045,10 @@ void lookup_run(hga_ctx* c) {
         c->check_launch("lk_first_count");
         HGA_HIP(hipMemsetAsync(fptr0 + n, 0, 8, c->stream));
         exclusive_scan_u64(c, fptr0, n + 1, L.scratch3);
-        HGA_HIP(hipMemcpyAsync(&U, fptr0 + n, 8, hipMemcpyDeviceToHost, c->stream));
-        c->sync();
-        uint32_t* fk = static_cast<uint32_t*>(L.first_kid.ensure(std::max<uint64_t>(U, 1) * 4));
-        uint32_t* fp = static_cast<uint32_t*>(L.first_pos.ensure(std::max<uint64_t>(U, 1) * 4));
-        uint32_t* fr = static_cast<uint32_t*>(L.first_read.ensure(std::max<uint64_t>(U, 1) * 4));
+        // U <= H first occurrences: the arrays are sized by H, U itself comes with the final counters
+        uint32_t* fk = static_cast<uint32_t*>(L.first_kid.ensure(H * 4));
+        uint32_t* fp = static_cast<uint32_t*>(L.first_pos.ensure(H * 4));
+        uint32_t* fr = static_cast<uint32_t*>(L.first_read.ensure(H * 4));
         c->launch("lk_post", [&] {
             hipLaunchKernelGGL(lk_first_write, dim3(blocks_for(n, 4)), dim3(256), 0, c->stream, hptr, n, sk, sv,
                                fptr0, kmask, fk, fp, fr);
@@ -1023,7 +1059,6 @@ void lookup_run(hga_ctx* c) {
         uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(H * 4));
         radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
     }
-    L.firsts = U;
     uint64_t* fptr = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
     uint64_t* kptr = static_cast<uint64_t*>(L.kci_ptr.ensure(((uint64_t)L.n_sdk + 1) * 8));
     c->launch("lk_post", [&] {
@@ -1036,7 +1071,9 @@ void lookup_run(hga_ctx* c) {
     c->check_launch("lk_ptr");
     unsigned long long hc[4];
     HGA_HIP(hipMemcpyAsync(hc, ctr, 32, hipMemcpyDeviceToHost, c->stream));
+    if (H) HGA_HIP(hipMemcpyAsync(&U, fptr + n, 8, hipMemcpyDeviceToHost, c->stream));
     c->sync();
+    L.firsts = U;
     L.reads_hit = hc[0];
     L.ran = true;
 }

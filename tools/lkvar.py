@@ -17,7 +17,14 @@ c2 = hga.Ctx(0); c2.lookup_load(19, sdk); c2.lookup_set_reads(bases, offsets, 1)
 c2.profile(True); c2.profile_reset()
 for _ in range(3): c2.lookup_run()
 names = ("lk_count", "lk_emit", "lk_post", "lk_sort", "radix_upsweep", "radix_downsweep", "scan")
-print(json.dumps({"hits": int(c2.lookup_sizes().hits), "k": {n: round(c2.profile_get(n)[0] / 3, 4) for n in names}}))
+k = {n: round(c2.profile_get(n)[0] / 3, 4) for n in names}
+c2.profile(False)
+import time
+c2.sync(); t0 = time.perf_counter()
+for _ in range(10): c2.lookup_run()
+c2.sync(); ms = (time.perf_counter() - t0) / 10 * 1e3
+sz = c2.lookup_sizes()
+print(json.dumps({"ms": round(ms, 3), "hits": int(sz.hits), "firsts": int(sz.firsts), "k": k}))
 ''' % (ROOT, os.path.join(ROOT, "hybrid-genome-assembler_amd"))
 for so in sys.argv[1:]:
     out = subprocess.run([sys.executable, "-c", CODE], env=dict(os.environ, HGA_LIB=so), capture_output=True,
