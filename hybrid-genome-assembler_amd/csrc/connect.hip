@@ -22,6 +22,7 @@
 //   cn_keys / radix sort / cn_decode
 //               composite sort key (CAP-free): (max - score, pivot, candidate).
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -739,6 +740,12 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     if (const char* rc = std::getenv("HGA_CN_RCAP")) rcap = std::max<uint64_t>(1, std::strtoull(rc, nullptr, 10));
     unsigned long long h[4];
     std::vector<unsigned long long> hc(ctr_bytes / 8);
+    // every synchronisation reads all counters (tier counts and the 64 region cursors) at once
+    auto readback = [&] {
+        HGA_HIP(hipMemcpyAsync(hc.data(), ctr, ctr_bytes, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        std::memcpy(h, hc.data(), sizeof(h));
+    };
     std::vector<uint64_t> rpre(CN_R + 1, 0);
     for (int attempt = 0; attempt < 2; ++attempt) {
         const uint64_t cap = rcap * CN_R;
@@ -752,16 +759,14 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
                                ovf, force_block ? 1u : CNW_CAP * 3 / 4);
         });
         c->check_launch("cn_wave");
-        HGA_HIP(hipMemcpyAsync(h, ctr, 32, hipMemcpyDeviceToHost, c->stream));
-        c->sync();
+        readback();
         if (h[2]) {   // pivots with more distinct candidates than a wave table: one workgroup each
             c->launch("cn_local", [&] {
                 hipLaunchKernelGGL(cn_local, dim3((unsigned)h[2]), dim3(CN_T), 0, c->stream, in, out, ovf, ovf2,
                                    ctr + 3, force_global ? 1u : CN_CAP * 3 / 4);
             });
             c->check_launch("cn_local");
-            HGA_HIP(hipMemcpyAsync(h, ctr, 32, hipMemcpyDeviceToHost, c->stream));
-            c->sync();
+            readback();
         }
         if (h[3]) {   // overflow pivots: HBM tables of 2 x (largest pair count), in batches of <= 1 GiB
             auto* mx = ctr + 4;
@@ -789,11 +794,8 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
                 });
                 c->check_launch("cn_global");
             }
-            HGA_HIP(hipMemcpyAsync(h, ctr, 32, hipMemcpyDeviceToHost, c->stream));
-            c->sync();
+            readback();
         }
-        HGA_HIP(hipMemcpyAsync(hc.data(), ctr, ctr_bytes, hipMemcpyDeviceToHost, c->stream));
-        c->sync();
         uint64_t mx_region = 0;
         for (int r = 0; r < CN_R; ++r) {
             const uint64_t cnt = hc[8 + (size_t)r * CN_RSTRIDE];

@@ -499,26 +499,9 @@ __global__ void lk_ptr(const uint32_t* __restrict__ idx, uint64_t H, uint64_t ns
     for (uint64_t s = lo; s <= hi; ++s) ptr[s] = i;
 }
 
-// Number of non-empty CSR segments and the largest segment (one atomic each per 1024 segments).
-__global__ void __launch_bounds__(1024) lk_nonempty(const uint64_t* __restrict__ ptr, uint64_t nseg,
-                                                    unsigned long long* __restrict__ out) {
-    __shared__ uint32_t ws[1024 / 64 + 1];
-    __shared__ unsigned long long smax;
-    const uint64_t s = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-    const uint64_t len = s < nseg ? ptr[s + 1] - ptr[s] : 0;
-    if (threadIdx.x == 0) smax = 0;
-    __syncthreads();
-    if (len) atomicMax(&smax, (unsigned long long)len);
-    uint32_t tot;
-    (void)block_excl_scan<1024>(len ? 1u : 0u, ws, &tot);
-    if (threadIdx.x == 0) {
-        if (tot) atomicAdd(&out[0], (unsigned long long)tot);
-        if (smax) atomicMax(&out[1], smax);
-    }
-}
-
-// lk_nonempty + the reads with more than 512 / 2048 hits listed for the per-read sort tiers (order
-// irrelevant; one list atomic per workgroup): out[0] non-empty reads, out[1] largest, out[2] / out[3]
+// Number of non-empty CSR segments, the largest one, and the segments with more than 512 / 2048 entries
+// listed for the per-segment sort tiers (order irrelevant; one list atomic per workgroup): out[0] non-empty
+// segments, out[1] largest, out[2] / out[3]
 // the two list lengths — all read back with one synchronisation.
 __global__ void __launch_bounds__(1024) lk_seg_stats(const uint64_t* __restrict__ ptr, uint64_t nseg,
                                                      unsigned long long* __restrict__ out, uint32_t* __restrict__ mid,
@@ -824,18 +807,24 @@ inline int bits_for(uint64_t n) {   // bits to hold values in [0, n)
 // Stable per-segment sort of (sk low kbits, sv) by the key, segments hptr[s]..hptr[s+1] of at
 // most maxlen <= 16384 entries (returns false, doing nothing, above that): one wave per segment
 // up to 512 entries, listed segments on 256- and 1024-thread workgroups above.  Leaves
-// sk = s << kbits | key (segments of one entry are not touched: sk must arrive composed).  maxlen ~0: measured here.  `ctr2`: two device counters of scratch.
+// sk = s << kbits | key (segments of one entry are not touched: sk must arrive composed).  maxlen ~0: measured here (with the tier lists).  `ctr2`: two device counters of scratch.
 bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxlen, int kbits, uint64_t* sk,
                   uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label, uint32_t* lists,
                   const unsigned long long* lists_n) {
-    if (maxlen == ~0ull) {   // unknown: the longest segment first
-        unsigned long long h2[2] = {0, 0};
-        HGA_HIP(hipMemsetAsync(ctr2, 0, 16, c->stream));
+    unsigned long long h4[4] = {0, 0, 0, 0};
+    if (maxlen == ~0ull && !lists) {   // unknown: the longest segment and the tier lists, one read-back
+        const size_t lb = (2 * nseg * 4 + 7) & ~(size_t)7;
+        char* lp = static_cast<char*>(list_buf.ensure(lb + 64));
+        lists = reinterpret_cast<uint32_t*>(lp);
+        auto* cnt = reinterpret_cast<unsigned long long*>(lp + lb);
+        HGA_HIP(hipMemsetAsync(cnt, 0, 32, c->stream));
         if (nseg)
-            hipLaunchKernelGGL(lk_nonempty, dim3(blocks_for(nseg, 1024)), dim3(1024), 0, c->stream, hptr, nseg, ctr2);
-        HGA_HIP(hipMemcpyAsync(h2, ctr2, 16, hipMemcpyDeviceToHost, c->stream));
+            hipLaunchKernelGGL(lk_seg_stats, dim3(blocks_for(nseg, 1024)), dim3(1024), 0, c->stream, hptr, nseg, cnt,
+                               lists, lists + nseg, (uint32_t)(64 * WIPT), 2048u);
+        HGA_HIP(hipMemcpyAsync(h4, cnt, 32, hipMemcpyDeviceToHost, c->stream));
         c->sync();
-        maxlen = h2[1];
+        maxlen = h4[1];
+        lists_n = h4 + 2;
     }
     if (maxlen > 16384 || nseg >= (1ull << 31)) return false;
     uint32_t* mid = nullptr;
