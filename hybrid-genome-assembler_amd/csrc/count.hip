@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <type_traits>
 
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
@@ -961,18 +962,28 @@ constexpr uint32_t MAXPROBE_P = 64;     // groups probed before the table counts
 #define HGA_CS_WAVES 4
 #endif
 constexpr uint32_t T_S = HGA_T_S;       // slots (32 KB keys + 32 KB counts)
-constexpr uint32_t GS_S = 4;            // keys per probe group (one ds_read_b128)
+#ifndef HGA_GS_S
+#define HGA_GS_S 4
+#endif
+constexpr uint32_t GS_S = HGA_GS_S;     // keys per probe group (4: one ds_read_b128, 2: one ds_read_b64)
 constexpr uint32_t G_S = T_S / GS_S;
+static_assert(GS_S == 2 || GS_S == 4, "probe groups of 2 or 4 keys");
+using KGrp = std::conditional_t<GS_S == 4, uint4, uint2>;
 
-__device__ __forceinline__ uint4 read_keys_s(const uint32_t* tkey, uint32_t g) {
-    return reinterpret_cast<const uint4*>(tkey)[g];
+__device__ __forceinline__ KGrp read_keys_s(const uint32_t* tkey, uint32_t g) {
+    return reinterpret_cast<const KGrp*>(tkey)[g];
 }
-__device__ __forceinline__ void match_s(const uint4 kg, uint32_t r, int& w, int& e0) {
-    const uint32_t k[4] = {kg.x, kg.y, kg.z, kg.w};
+__device__ __forceinline__ void match_s(const KGrp kg, uint32_t r, int& w, int& e0) {
+    uint32_t k[GS_S];
+    if constexpr (GS_S == 4) {
+        k[0] = kg.x; k[1] = kg.y; k[2] = reinterpret_cast<const uint4&>(kg).z; k[3] = reinterpret_cast<const uint4&>(kg).w;
+    } else {
+        k[0] = kg.x; k[1] = kg.y;
+    }
     w = -1;
     e0 = -1;
 #pragma unroll
-    for (int t = 3; t >= 0; --t) {
+    for (int t = GS_S - 1; t >= 0; --t) {
         w = k[t] == r ? t : w;
         e0 = k[t] == 0xFFFFFFFFu ? t : e0;
     }
@@ -1098,7 +1109,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                         rv[q] = (sk >= lo && sk < hi) ? rv[q] : 0xFFFFFFFFu;
                     }
                 }
-                uint4 kg[PF_P];
+                KGrp kg[PF_P];
 #pragma unroll
                 for (int q = 0; q < PF_P; ++q) kg[q] = read_keys_s(tkey, rv[q] & (G_S - 1));
                 uint32_t claim = 0, miss = 0, slot[PF_P];
