@@ -941,7 +941,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 #define HGA_NT_P 512
 #endif
 #ifndef HGA_PF_P
-#define HGA_PF_P 8
+#define HGA_PF_P 6
 #endif
 constexpr int NT_P = HGA_NT_P;
 constexpr int PF_P = HGA_PF_P;          // binned elements per thread per batch
