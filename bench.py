@@ -380,19 +380,28 @@ def ingest_leg(ga, gb, threads):
         shutil.rmtree(d, ignore_errors=True)
 
 
-def scale_leg(dev, reps=2):
-    """SURVEY.md C4 at one rank of eight: reads of a 2 x 500 Mbp diploid (d = 0.005) at 30x / 8 =
-    3.75x, ART-like 150 bp, 2 files (3.77 Gbases, 3.3 G 19-mer instances) counted on this GPU in one
-    pass (the third split level); the same step as the headline."""
-    L4, cov = 500_000_000, 3.75
+C4_GENOME, C4_COV = 500_000_000, 30.0 / 8
+
+
+def make_c4_shard(rank=0):
+    """SURVEY.md C4 at one rank of eight: ART-like 150 bp reads of a 2 x 500 Mbp diploid (d = 0.005)
+    at 30x / 8 = 3.75x, 2 files (3.77 Gbases, 3.3 G 19-mer instances).  Rank r draws its own reads
+    of the same diploid (seeds 43/44 at rank 0, the N = 1 bench leg and tests/test_scale_gpu.py)."""
     t_gen = time.perf_counter()
-    g4a = hga.gen_genome(L4, 41)
+    g4a = hga.gen_genome(C4_GENOME, 41)
     g4b = hga.gen_haplotype(g4a, 0.005, 0, 42)
-    n4 = int(cov * L4 / READ_LEN)
-    r4a = hga.gen_art(g4a, n4, READ_LEN, 43)
-    r4b = hga.gen_art(g4b, n4, READ_LEN, 44)
+    n4 = int(C4_COV * C4_GENOME / READ_LEN)
+    r4a = hga.gen_art(g4a, n4, READ_LEN, 43 + 2 * rank)
+    r4b = hga.gen_art(g4b, n4, READ_LEN, 44 + 2 * rank)
     del g4a, g4b
-    log(f"C4 rank shard generated in {time.perf_counter() - t_gen:.1f}s: {2 * n4} reads")
+    log(f"[rank {rank}] C4 rank shard generated in {time.perf_counter() - t_gen:.1f}s: {2 * n4} reads")
+    return r4a, r4b
+
+
+def scale_leg(dev, reps=2):
+    """SURVEY.md C4 at one rank of eight (make_c4_shard) counted on this GPU in one pass (DESIGN.md
+    §3: the third split level); the same step as the headline."""
+    r4a, r4b = make_c4_shard(0)
     c4 = hga.Ctx(dev)
     try:
         c4.count_begin(K, 2)

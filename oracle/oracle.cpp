@@ -748,6 +748,89 @@ int64_t or_connections(uint64_t n, const uint64_t* hit_ptr, const uint32_t* sort
     return (int64_t)conns.size();
 }
 
+// or_connections with the pivots split over `threads` threads (contiguous pivot ranges, the same
+// per-pivot count as above), each thread's list sorted in the same order and the sorted lists
+// merged pairwise.  Identical output; for the config-size parity tests (C5 share: 600 K pivots,
+// 115 M connections) where one thread would take minutes.
+int64_t or_connections_mt(uint64_t n, const uint64_t* hit_ptr, const uint32_t* sorted_kid,
+                          const uint64_t* kci_ptr, const uint32_t* kci_read, const uint32_t* read_ids,
+                          const uint32_t* pivots, uint64_t n_piv, uint32_t min_kmers, uint64_t min_score,
+                          int threads, uint32_t** ox, uint32_t** oy, uint64_t** os) {
+    if (threads < 1) threads = 1;
+    std::unordered_map<uint32_t, uint64_t> row_of;
+    for (uint64_t r = 0; r < n; ++r)
+        if (hit_ptr[r + 1] > hit_ptr[r]) row_of[read_ids[r]] = r;
+    std::vector<uint32_t> piv;
+    if (pivots) piv.assign(pivots, pivots + n_piv);
+    else for (uint64_t r = 0; r < n; ++r) piv.push_back(read_ids[r]);
+    struct Conn { uint32_t x, y; uint64_t s; };
+    auto less = [](const Conn& a, const Conn& b) {
+        if (a.s != b.s) return a.s > b.s;
+        if (a.x != b.x) return a.x < b.x;
+        return a.y < b.y;
+    };
+    std::vector<std::vector<Conn>> part(threads);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                const size_t p0 = piv.size() * t / threads, p1 = piv.size() * (t + 1) / threads;
+                auto& out = part[t];
+                std::unordered_map<uint32_t, uint64_t> shared;
+                for (size_t q = p0; q < p1; ++q) {
+                    const uint32_t p = piv[q];
+                    auto it = row_of.find(p);
+                    if (it == row_of.end()) continue;
+                    const uint64_t r = it->second;
+                    if (hit_ptr[r + 1] - hit_ptr[r] < min_kmers) continue;
+                    shared.clear();
+                    for (uint64_t i = hit_ptr[r]; i < hit_ptr[r + 1]; ++i) {
+                        const uint32_t kid = sorted_kid[i];
+                        for (uint64_t j = kci_ptr[kid]; j < kci_ptr[kid + 1]; ++j) shared[kci_read[j]]++;
+                    }
+                    shared.erase(p);
+                    for (auto& kv : shared)
+                        if (kv.second >= min_score) out.push_back({p, kv.first, kv.second});
+                }
+                std::sort(out.begin(), out.end(), less);
+            });
+        for (auto& x : th) x.join();
+    }
+    // pairwise merges, independent pairs in parallel
+    while (part.size() > 1) {
+        std::vector<std::vector<Conn>> next((part.size() + 1) / 2);
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < next.size(); ++i)
+            th.emplace_back([&, i] {
+                if (2 * i + 1 >= part.size()) {
+                    next[i].swap(part[2 * i]);
+                    return;
+                }
+                auto& a = part[2 * i];
+                auto& b = part[2 * i + 1];
+                next[i].resize(a.size() + b.size());
+                std::merge(a.begin(), a.end(), b.begin(), b.end(), next[i].begin(), less);
+                std::vector<Conn>().swap(a);
+                std::vector<Conn>().swap(b);
+            });
+        for (auto& x : th) x.join();
+        part.swap(next);
+    }
+    const auto& c = part[0];
+    uint32_t* X = (uint32_t*)std::malloc(std::max<size_t>(1, c.size() * 4));
+    uint32_t* Y = (uint32_t*)std::malloc(std::max<size_t>(1, c.size() * 4));
+    uint64_t* S = (uint64_t*)std::malloc(std::max<size_t>(1, c.size() * 8));
+    for (size_t i = 0; i < c.size(); ++i) {
+        X[i] = c[i].x;
+        Y[i] = c[i].y;
+        S[i] = c[i].s;
+    }
+    *ox = X;
+    *oy = Y;
+    *os = S;
+    return (int64_t)c.size();
+}
+
 // Multi-threaded lookup-only timing kernel for the cpu_baseline leg: counts SDK hits
 // over all windows of all reads with a std::unordered_set, reads split over threads.
 uint64_t or_lookup_hits_mt(const char* bases, const uint64_t* offsets, uint64_t n, int k,

@@ -73,6 +73,10 @@ def lib():
         L.or_connections.argtypes = [C.c_uint64, _u64p, _u32p, _u64p, _u32p, _u32p, _u32p, C.c_uint64, C.c_uint32,
                                      C.c_uint64, _i32p, C.POINTER(_u32p), C.POINTER(_u32p), C.POINTER(_u64p),
                                      C.POINTER(_u8p)]
+        L.or_connections_mt.restype = C.c_int64
+        L.or_connections_mt.argtypes = [C.c_uint64, _u64p, _u32p, _u64p, _u32p, _u32p, _u32p, C.c_uint64,
+                                        C.c_uint32, C.c_uint64, C.c_int, C.POINTER(_u32p), C.POINTER(_u32p),
+                                        C.POINTER(_u64p)]
         L.or_lookup_hits_mt.restype = C.c_uint64
         L.or_lookup_hits_mt.argtypes = [C.c_char_p, _u64p, C.c_uint64, C.c_int, _u64p, C.c_uint32, C.c_int]
         L.or_murmur3_x86_32.restype = C.c_uint32
@@ -241,6 +245,24 @@ def connections(idx, pivots=None, min_kmers: int = 1, min_score: int = 1, catego
     return _take(px, m, np.uint32), _take(py, m, np.uint32), _take(ps, m, np.uint64), _take(pg, m, np.uint8)
 
 
+def connections_mt(idx, threads: int, pivots=None, min_kmers: int = 1, min_score: int = 1,
+                   first_read_id: int = 1):
+    """connections() (no categories) with the pivots split over `threads` threads: (x, y, score)."""
+    hp = np.ascontiguousarray(idx["hit_ptr"], np.uint64)
+    n = len(hp) - 1
+    sk = np.ascontiguousarray(idx["sorted_kid"], np.uint32)
+    kp = np.ascontiguousarray(idx["kci_ptr"], np.uint64)
+    kr = np.ascontiguousarray(idx["kci_read"], np.uint32)
+    ids = np.arange(first_read_id, first_read_id + n, dtype=np.uint32)
+    pv = None if pivots is None else np.ascontiguousarray(pivots, np.uint32)
+    px, py, ps = _u32p(), _u32p(), _u64p()
+    m = lib().or_connections_mt(n, _p(hp, C.c_uint64), _p(sk, C.c_uint32), _p(kp, C.c_uint64),
+                                _p(kr, C.c_uint32), _p(ids, C.c_uint32), None if pv is None else _p(pv, C.c_uint32),
+                                0 if pv is None else len(pv), min_kmers, min_score, threads,
+                                C.byref(px), C.byref(py), C.byref(ps))
+    return _take(px, m, np.uint32), _take(py, m, np.uint32), _take(ps, m, np.uint64)
+
+
 def lookup_hits_mt(bases: bytes, offsets, k: int, sdk_keys, threads: int) -> int:
     offsets = np.ascontiguousarray(offsets, np.uint64)
     sdk = np.ascontiguousarray(sdk_keys, np.uint64)
@@ -259,6 +281,14 @@ def count_pipeline(streams, k, lower, upper, thresholds=THRESHOLDS, min_count=2)
     hist = specificity(counts, thresholds) if len(keys) else np.zeros((0, 3), np.int64)
     sel, disc = select(keys, counts, lower, upper)
     return {"dumps": dumps, "keys": keys, "counts": counts, "hist": hist, "selected": sel, "n_discr": disc}
+
+
+def count_pipeline_mt(streams, k, lower, upper, threads, thresholds=THRESHOLDS, min_count=2):
+    """count_pipeline's outputs from the multi-threaded count stage (or_count_files_mt)."""
+    keys, counts = count_files_mt(streams, k, min_count, threads)
+    hist = specificity(counts, thresholds) if len(keys) else np.zeros((0, 3), np.int64)
+    sel, disc = select(keys, counts, lower, upper)
+    return {"keys": keys, "counts": counts, "hist": hist, "selected": sel, "n_discr": disc}
 
 
 def murmur3_x86_32(data: bytes, seed: int) -> int:

@@ -167,7 +167,7 @@ def run(rank, world, args, group_ready=False):
         log(f"[rank {rank}] k={k}: {out['per_k'][k]}")
     ctx.close()
     if args.check and rank == 0:
-        verify(args, world, checks)
+        verify(args, world, checks, own=(ga, gb, art, lr_bases, lr_offsets, first_id) if world == 1 else None)
         out["checked_against_oracle"] = True
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -185,12 +185,14 @@ def _fetch_conn(ctx, n):
     return x, y, s
 
 
-def verify(args, world, checks):
-    """Rank 0 regenerates every rank's shards (same seeds) and runs the oracle over all of them."""
+def verify(args, world, checks, own=None):
+    """Rank 0 regenerates every rank's shards (same seeds; at one rank its own data is reused) and
+    runs the oracle over all of them."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     L = int(CHR1 * args.scale)
-    shards = [make_data(L, args.div, args.art_cov, args.lr_cov, r, world) for r in range(world)]
+    shards = [own] if own is not None else \
+        [make_data(L, args.div, args.art_cov, args.lr_cov, r, world) for r in range(world)]
     streams = [b"\n".join(s[2][f].seq for s in shards) for f in range(2)]
     bases = b"".join(s[3] for s in shards)
     offs = [np.zeros(1, np.uint64)]
@@ -199,17 +201,29 @@ def verify(args, world, checks):
         offs.append(s[4][1:] + np.uint64(base))
         base += int(s[4][-1])
     offsets = np.concatenate(offs).astype(np.uint64)
+    del shards
+    th = args.check_threads
     for k, c in checks.items():
-        o = oracle.count_pipeline(streams, k, args.lower, args.upper)
+        t0 = time.perf_counter()
+        if th > 1:   # the multi-threaded restatements (each checked against the plain one in tests/)
+            o = oracle.count_pipeline_mt(streams, k, args.lower, args.upper, th)
+        else:
+            o = oracle.count_pipeline(streams, k, args.lower, args.upper)
         assert np.array_equal(c["hist"], o["hist"]), f"k={k}: histogram"
         assert np.array_equal(c["sdk"], o["selected"]) and c["nd"] == o["n_discr"], f"k={k}: export"
-        idx = oracle.construct_indices(bases, offsets, k, o["selected"], 1)
+        sel = o["selected"]
+        del o
+        idx = oracle.construct_indices(bases, offsets, k, sel, 1, threads=th if th > 1 else 0)
         for name in idx:
             assert np.array_equal(c["idx"][name], idx[name]), f"k={k}: lookup {name}"
-        x, y, s, _ = oracle.connections(idx, min_score=1)
+        if th > 1:
+            x, y, s = oracle.connections_mt(idx, th, min_score=1)
+        else:
+            x, y, s, _ = oracle.connections(idx, min_score=1)
         assert np.array_equal(c["conn"][0], x) and np.array_equal(c["conn"][1], y) and \
             np.array_equal(c["conn"][2], s), f"k={k}: connections"
-        log(f"k={k}: export, index and read graph equal the oracle")
+        log(f"k={k}: export ({len(sel)}), index ({len(idx['hit_kid'])} hits) and read graph ({len(x)} "
+            f"connections) equal the oracle [{time.perf_counter() - t0:.1f}s]")
 
 
 def parse(argv=None):
@@ -222,6 +236,8 @@ def parse(argv=None):
     ap.add_argument("--lower", type=int, default=10)
     ap.add_argument("--upper", type=int, default=25)
     ap.add_argument("--check", action="store_true", help="rank 0 checks every stage against the oracle")
+    ap.add_argument("--check-threads", type=int, default=1,
+                    help="oracle threads for --check (> 1: the multi-threaded restatements)")
     ap.add_argument("--warmup", type=int, default=1, help="1: an untimed pass of the first k first (allocations)")
     return ap.parse_args(argv)
 
