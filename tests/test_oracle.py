@@ -171,3 +171,35 @@ def test_construct_indices_mt_matches_plain(threads):
     assert int(a["hit_ptr"][-1]) > 1000
     for name in a:
         assert np.array_equal(a[name], b[name]), name
+
+
+@pytest.mark.parametrize("threads,use_piv,min_kmers,min_score", [(1, False, 1, 1), (3, False, 1, 2), (8, True, 2, 1),
+                                                                 (64, False, 1, 1)])
+def test_connections_mt_matches_plain(threads, use_piv, min_kmers, min_score):
+    """The pivot-parallel connections oracle (C5 share test) equals the plain one."""
+    rng = np.random.default_rng(33)
+    gnm = bytes(rng.choice(list(b"ACGT"), 5000).tolist())
+    reads = []
+    for _ in range(300):
+        s = int(rng.integers(0, 4800))
+        reads.append(gnm[s:s + int(rng.integers(0, 350))])
+    bases = b"".join(reads)
+    offs = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    c, _ = oracle.kmer_windows(gnm, 13)
+    sdk = np.unique(c)[::5]
+    idx = oracle.construct_indices(bases, offs, 13, sdk, 2)
+    piv = np.arange(300, 1, -3, dtype=np.uint32) if use_piv else None
+    x, y, s, _ = oracle.connections(idx, piv, min_kmers, min_score, first_read_id=2)
+    x2, y2, s2 = oracle.connections_mt(idx, threads, piv, min_kmers, min_score, first_read_id=2)
+    assert len(x) > 100
+    assert np.array_equal(x, x2) and np.array_equal(y, y2) and np.array_equal(s, s2)
+
+
+def test_count_pipeline_mt_matches_plain():
+    rng = random.Random(77)
+    streams = ["\n".join(rand_seq(rng, 150) for _ in range(3000)).encode() for _ in range(2)]
+    streams = [s + b"\n" + s[: len(s) // 3] for s in streams]
+    a = oracle.count_pipeline(streams, 17, 2, 4)
+    b = oracle.count_pipeline_mt(streams, 17, 2, 4, threads=6)
+    for name in ("keys", "counts", "hist", "selected", "n_discr"):
+        assert np.array_equal(a[name], b[name]), name
