@@ -75,22 +75,51 @@ def pmc_traffic(kernel):
     return None
 
 
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) started without torchrun: run N rank processes of this same command
+    (torch.distributed.run, one node, 127.0.0.1) as a child and return its exit code.  Called before
+    anything touches the GPU; the parent only waits."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"bench: --gpus {n} without WORLD_SIZE: starting {n} ranks (torch.distributed.run)")
+    return subprocess.call(cmd, env=dict(os.environ, HGA_BENCH_SPAWNED="1"))
+
+
 class Dist:
     def __init__(self, n):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
+        if n != self.world:   # the ranks that exist must be the ranks asked for
+            log(f"error: --gpus {n} but WORLD_SIZE={self.world} ranks")
+            sys.exit(2)
+        # HGA_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks (the
+        # library's host transport); nccl = RCCL, one rank per GPU
+        backend = os.environ.get("HGA_BENCH_BACKEND", "nccl")
+        self.backend = backend
         # HGA_BENCH_FORCE_DIST=1 (under torchrun): the N>1 code path at one rank — the library's
         # RCCL communicator, the exchange and the global queries — on a one-GPU box
         if self.world > 1 or os.environ.get("HGA_BENCH_FORCE_DIST") == "1":
             import torch
             import torch.distributed as dist
-            # HGA_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks
-            backend = os.environ.get("HGA_BENCH_BACKEND", "nccl")
-            if backend != "nccl":
+            dry = os.environ.get("HGA_BENCH_DRYRUN") == "1"   # launcher test: no GPU call at all
+            if backend == "nccl" and not dry:
+                nd = torch.cuda.device_count()   # does not initialise the GPU
+                if nd < self.world:
+                    log(f"error: {self.world} RCCL ranks need {self.world} GPUs, {nd} visible "
+                        "(HGA_BENCH_BACKEND=gloo shares GPUs)")
+                    sys.exit(2)
+            elif not dry:
                 self.local %= max(1, torch.cuda.device_count())
-            torch.cuda.set_device(self.local)
+            if not dry:
+                torch.cuda.set_device(self.local)
             # the communication libraries may print to fd 1; stdout must carry only the JSON line
             sys.stdout.flush()
             saved = os.dup(1)
@@ -108,8 +137,6 @@ class Dist:
             self.comm_dev = f"cuda:{self.local}" if backend == "nccl" else "cpu"
             self.torch, self.dist = torch, dist
             self.pg = True
-        if n != self.world and self.world > 1:
-            log(f"warning: --gpus {n} but WORLD_SIZE={self.world}")
 
     def barrier(self):
         if self.pg:
@@ -186,6 +213,10 @@ def cpu_baseline(ra, rb, threads, parse_s=None):
         return time.perf_counter() - t0
 
     dt = stage(streams, threads)
+    # every host core this process may run on (BASELINE.md §3 "all host cores"; nproc counts the whole
+    # host, the affinity mask what the box gives this process)
+    n_all = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    dt_all = stage(streams, n_all) if n_all != threads else dt
     sub16 = [s[: s.find(b"\n", len(s) // 16)] for s in streams]
     inst16 = sum(oracle.count_instances(s, K) for s in sub16)
     dt1 = stage(sub16, 1)
@@ -199,7 +230,10 @@ def cpu_baseline(ra, rb, threads, parse_s=None):
                      f"count stage (range-partitioned exact counts, sort + run-length, --bc drop, merge; "
                      f"{threads} threads) + specificity + select[10,25]",
            "seconds": round(dt, 3), "nproc": os.cpu_count(), "cpu_model": cpu_model(),
-           "threads_note": "threads = the GPU box's CPU share for one GPU (16), not nproc, which counts the whole host",
+           "threads_note": "threads = the GPU box's CPU share for one GPU (16); all_cores = every CPU in this "
+                           "process's affinity mask (nproc counts the whole host)",
+           "all_cores": {"value": round(inst / dt_all, 1), "unit": "k-mers/s", "cores": n_all,
+                         "sample": "the whole C2 workload, same stage", "seconds": round(dt_all, 3)},
            "one_core": {"value": round(inst16 / dt1, 1), "unit": "k-mers/s", "cores": 1,
                         "sample": f"first 1/16 of each C2 file ({inst16} windows), same stage", "seconds": round(dt1, 3)},
            "reference_like": {"value": round(inst64 / dtr, 1), "unit": "k-mers/s", "cores": 1,
@@ -274,7 +308,7 @@ def connections_leg(ctx2, D, reps, args):
                         "(id, candidate) pair + 12 B per kept pair",
                         "achieved": round(cn_bytes / (cn_ms * 1e-3) / 1e9, 1) if cn_ms else None,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s"}}
-    if not args.no_cpu and D.rank == 0:
+    if not args.no_cpu and D.rank == 0 and D.world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         n_p = 2000
@@ -315,7 +349,7 @@ def hll_leg(ctx2, D, n_bases, bases, offsets, args):
            "roofline": {"bound": "hbm", "kernel": "hll_scan", "model": "0.5 B per base (packed codes + valid + "
                         "read-start bits)", "achieved": round(0.5 * n_bases / (per_k * 1e-3) / 1e9, 1) if per_k
                         else None, "peak": HBM_PEAK_GBS, "unit": "GB/s"}}
-    if not args.no_cpu and D.rank == 0:
+    if not args.no_cpu and D.rank == 0 and D.world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         n = min(len(offsets) - 1, 8000)
@@ -398,40 +432,87 @@ def make_c4_shard(rank=0):
     return r4a, r4b
 
 
-def scale_leg(dev, reps=2):
-    """SURVEY.md C4 at one rank of eight (make_c4_shard) counted on this GPU in one pass (DESIGN.md
-    §3: the third split level); the same step as the headline."""
-    r4a, r4b = make_c4_shard(0)
-    c4 = hga.Ctx(dev)
+def scale_leg(D, reps=2):
+    """BASELINE configs[3] ("C4": k=19 count of a 1 Gbp diploid at ART 30x over 8 GPUs) on this run's
+    ranks: every rank counts its own C4/8 shard (make_c4_shard(rank): 3.77 Gbases, 3.3 G instances,
+    counted in one pass with the third split level); at N > 1 the shards are then
+    merged by the owner exchange over the library's communicator (hga_count_exchange), so N = 8 is
+    configs[3] itself.  The step is the headline's (count + histogram + export selection); time = max
+    over ranks."""
+    r4a, r4b = make_c4_shard(D.rank)
+    c4 = hga.Ctx(D.local)
     try:
         c4.count_begin(K, 2)
         c4.count_add(0, r4a.seq)
         c4.count_add(1, r4b.seq)
         bases = len(r4a.seq) + len(r4b.seq)
         del r4a, r4b
-        count_step(c4)   # warm-up (allocations)
+        ex4 = None
+        if D.pg:
+            import hga_dist
+            ex4 = hga_dist.OwnerExchange(c4)
+        step = (lambda: dist_count_step(ex4)) if ex4 else (lambda: count_step(c4))
+        step()   # warm-up (allocations)
         c4.profile(True)
         c4.profile_reset()
-        count_step(c4)
+        step()
         names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
+                 "kx_piece_hist", "kx_pack_scatter", "kx_mb_hist", "kx_mb_scatter", "kx_mb_merge", "kx_mb_compact",
                  "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
         ker = {nm: round(c4.profile_get(nm)[0], 3) for nm in names if c4.profile_get(nm)[1]}
         c4.profile(False)
+        D.barrier()
         c4.sync()
         t0 = time.perf_counter()
         for _ in range(reps):
-            n_sel, n_disc = count_step(c4)
+            n_sel, n_disc = step()
         c4.sync()
-        ms = (time.perf_counter() - t0) / reps * 1e3
-        st = c4.count_stats()
-        return {"workload": "C4 rank shard: 1/8 of ART-like 30x reads of a 2 x 500 Mbp diploid (d=0.005), k=19, "
-                            "2 files; step = count_run + spec_hist + select[10,25]",
-                "bases": int(bases), "instances": int(st.instances), "distinct_rows": int(st.distinct_rows),
+        D.barrier()
+        ms = D.max((time.perf_counter() - t0) / reps * 1e3)
+        st = c4.count_stats()   # global after the exchange
+        return {"workload": f"C4 (configs[3]): {D.world} of the 8 rank shards of ART-like 30x reads of a 2 x 500 Mbp "
+                            "diploid (d=0.005), k=19, 2 files per shard; step = count_run + "
+                            + ("hga_count_exchange (owner all-to-all) + " if ex4 else "")
+                            + "spec_hist + select[10,25]",
+                "ranks": D.world, "fraction_of_c4": D.world / 8, "bases_per_rank": int(bases),
+                "instances": int(st.instances), "distinct_rows": int(st.distinct_rows),
                 "buckets": int(st.buckets), "max_split": int(st.max_split), "selected": int(n_sel),
                 "discriminative": int(n_disc), "ms_per_step": round(ms, 2),
-                "k_mers_per_s": round(st.instances / (ms * 1e-3), 1), "kernels_ms": ker}
+                "k_mers_per_s": round(st.instances / (ms * 1e-3), 1), "kernels_ms_rank0": ker}
     finally:
         c4.close()
+
+
+def dist_parity(ctx, D, threads):
+    """N > 1: the exchanged (global) count of the timed step against the oracle over every rank's C2
+    shard — all merged rows, the histogram and the export counts — so each multi-GPU run records
+    the parity of its own transport (RCCL over xGMI by default).  Rank 0 checks; all ranks take part
+    in the collective reads."""
+    keys, counts = ctx.rows()
+    hist = ctx.spec_hist(THRESHOLDS)
+    n_sel, n_disc = ctx.select_device(LOWER, UPPER)
+    out = None
+    if D.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        t0 = time.perf_counter()
+        shards = [make_c2(r)[2:] for r in range(D.world)]
+        streams = [b"\n".join(sh[f].seq for sh in shards) for f in range(2)]
+        del shards
+        ok, oc = oracle.count_files_mt(streams, K, 2, threads)
+        sel, nd = oracle.select(ok, oc, LOWER, UPPER)
+        eq = {"rows": bool(np.array_equal(keys, ok) and np.array_equal(counts, oc)),
+              "histogram": bool(np.array_equal(hist, oracle.specificity(oc, THRESHOLDS))),
+              "export_counts": bool(n_sel == len(sel) and n_disc == nd)}
+        out = {"checked": "global rows, histogram and export counts of the exchanged C2 shards vs the oracle "
+                          f"over all {D.world} ranks' reads ({threads} threads)",
+               "transport": "RCCL (hga_comm_init)" if D.backend == "nccl" else "host transport hook (gloo)",
+               "rows": int(len(ok)), "equal": all(eq.values()), "parts": eq,
+               "seconds": round(time.perf_counter() - t0, 1)}
+        if not out["equal"]:
+            log(f"error: N>1 parity check failed: {eq}")
+    D.barrier()
+    return out
 
 
 def main():
@@ -442,10 +523,18 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lookup", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host FASTQ ingest leg")
-    ap.add_argument("--no-scale", action="store_true", help="skip the C4 rank-shard count leg (N=1 only)")
+    ap.add_argument("--no-scale", action="store_true", help="skip the C4 leg (one C4/8 shard per rank)")
+    ap.add_argument("--no-check", action="store_true", help="N > 1: skip the oracle check of the exchanged count")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("HGA_CPU_THREADS", "16")))
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     D = Dist(args.gpus)
+    if os.environ.get("HGA_BENCH_DRYRUN") == "1":   # launcher test (tests/test_bench_launch.py)
+        if D.rank == 0:
+            print(json.dumps({"dryrun": True, "n_gpus": D.world, "backend": D.backend}), flush=True)
+        D.close()
+        return
     dev = D.local
     t_gen = time.perf_counter()
     ga, gb, ra, rb = make_c2(D.rank)
@@ -528,6 +617,8 @@ def main():
                               "achieved": round(pipe_gbs, 1), "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)},
         "kernels_ms_per_step": {k: round(v["ms_per_step"], 4) for k, v in kernels.items()},
     }
+    if ex and not args.no_check:   # the state of the last timed step: the exchanged global count
+        result["parity"] = dist_parity(ctx, D, min(16 * D.world, os.cpu_count() or 16))
 
     if not args.no_lookup:
         t_gen = time.perf_counter()
@@ -582,17 +673,18 @@ def main():
         result["categorize"]["connections"] = connections_leg(ctx2, D, reps, args)
         result["categorize"]["hll_auto_k"] = hll_leg(ctx2, D, len(bases), bases, offsets, args)
         ctx2.close()
-        if not args.no_cpu and D.rank == 0:
+        if not args.no_cpu and D.rank == 0 and D.world == 1:
             result["categorize"]["cpu_baseline"] = cpu_lookup_baseline(bases, offsets, sdk, args.cpu_threads)
 
     if not args.no_ingest and D.rank == 0 and D.world == 1:
         result["ingest"] = ingest_leg(ga, gb, args.cpu_threads)
-    if not args.no_cpu and D.rank == 0:
+    if not args.no_cpu and D.rank == 0 and D.world == 1:   # CPU baselines: rank 0 at N = 1 only
         parse_s = result.get("ingest", {}).get("parallel", {}).get("jf_stream_s")
         result["cpu_baseline"] = cpu_baseline(ra, rb, args.cpu_threads, parse_s)
-    if not args.no_scale and D.world == 1:
-        result["scale_c4_shard"] = scale_leg(dev)
     ctx.close()
+    del ra, rb
+    if not args.no_scale:
+        result["scale_c4"] = scale_leg(D)
     D.close()
     if D.rank == 0:
         print(json.dumps(result), flush=True)

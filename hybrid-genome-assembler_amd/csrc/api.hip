@@ -145,12 +145,8 @@ hga_status hga_count_get_stats(hga_ctx* c, hga_count_stats* out) {
         uint64_t b = 0;
         for (auto l : s.seq_len) b += l;
         out->bytes = b;
-        if (s.dist) {   // after hga_count_exchange: the whole input over all ranks
-            uint64_t r = s.rows;
-            std::vector<uint64_t> g(c->comm->nranks);
-            hga::comm_allgather(c, &r, 8, g.data());
-            out->distinct_rows = 0;
-            for (auto v : g) out->distinct_rows += v;
+        if (s.dist) {   // after hga_count_exchange: the whole input over all ranks (no collective)
+            out->distinct_rows = s.g_rows;
             out->instances = s.g_instances;
             out->bytes = s.g_bytes;
         }

@@ -33,6 +33,8 @@
         if (r_ != ncclSuccess) throw ::hga::Error(HGA_ERR_COMM, std::string(#call) + ": " + ncclGetErrorString(r_)); \
     } while (0)
 
+static_assert(sizeof(ncclUniqueId) <= HGA_UNIQUE_ID_BYTES, "hga.h HGA_UNIQUE_ID_BYTES must hold an ncclUniqueId");
+
 namespace hga {
 
 namespace {
@@ -45,9 +47,10 @@ struct RcclComm : Comm {
         // HGA_RCCL_SELF (test hook, read per call): the rank's own slice also goes through
         // ncclSend/ncclRecv, so a one-GPU box exercises the grouped point-to-point calls
         const bool self_p2p = std::getenv("HGA_RCCL_SELF") != nullptr;
-        if (sb[rank] && !self_p2p) {
+        if (!self_p2p) {
             HGA_REQUIRE(rb[rank] == sb[rank], HGA_ERR_COMM, "alltoallv: self sizes disagree");
-            HGA_HIP(hipMemcpyAsync(recv[rank], send[rank], sb[rank], hipMemcpyDeviceToDevice, c->stream));
+            if (sb[rank])
+                HGA_HIP(hipMemcpyAsync(recv[rank], send[rank], sb[rank], hipMemcpyDeviceToDevice, c->stream));
         }
         HGA_NCCL(ncclGroupStart());
         for (int p = 0; p < nranks; ++p) {
@@ -239,6 +242,12 @@ void count_exchange(hga_ctx* c, uint32_t min_per_file) {
     proto::count_exchange(e, x, min_per_file, mine, &g);
     s.g_instances = g[0];
     s.g_bytes = g[1];
+    // the global row count once, here, so hga_count_get_stats stays local (not a collective)
+    std::vector<uint64_t> gr(x.nranks);
+    uint64_t r = s.rows;
+    comm_allgather(c, &r, 8, gr.data());
+    s.g_rows = 0;
+    for (auto v : gr) s.g_rows += v;
     s.dist = true;
 }
 

@@ -140,7 +140,7 @@ struct CountState {
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t sel_grid = 0;   // kc_select workgroups: as many as are resident at once (count.hip)
-    uint64_t g_instances = 0, g_bytes = 0;   // over all ranks (set by count_exchange)
+    uint64_t g_instances = 0, g_bytes = 0, g_rows = 0;   // over all ranks (set by count_exchange)
     std::vector<char> tab_host;
     std::vector<double> thr_dev;   // thresholds last uploaded next to the histogram (count_spec_hist)   // last uploaded per-file tables
     // pre-counted dump rows per file (hga_count_add_rows), merged verbatim at the end of count_run

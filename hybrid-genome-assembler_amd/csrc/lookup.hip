@@ -38,6 +38,7 @@ namespace {
 #endif
 constexpr int LK_T = HGA_LK_T;   // lookup scan workgroup
 constexpr int LK_P = 32;                  // window ends per thread (frame of 4 words)
+static_assert(LK_P % 32 == 0, "a thread's windows start on a 32-base word (word_read, lk_scan's emit)");
 constexpr int LK_QN = 256;                // filter-pass queue entries per wave
 constexpr int LK_ST = 2048;               // emit pass: hits per tile staged in LDS (more: direct stores)
 constexpr uint64_t EMPTY_KEY = ~0ull;     // never canonical: min(fwd, rc) of all-T is 0
@@ -458,7 +459,7 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
             const uint64_t gtt = gt0 + (w >> 5);
             const uint64_t e = gtt * LK_P + (w & 31u);
             const uint32_t kk = win_kid[e];
-            uint64_t rr = word_read[gtt];
+            uint64_t rr = word_read[(gtt * LK_P) >> 5];   // word_read is per 32 bases
             uint64_t nx = offs[rr + 1];
             while (nx <= e) nx = offs[++rr + 1];
             const uint32_t pp = (uint32_t)(e + 1 - offs[rr]);

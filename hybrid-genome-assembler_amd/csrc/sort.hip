@@ -417,9 +417,9 @@ __global__ void __launch_bounds__(SC_T) sc_onepass(T* data, uint64_t n, unsigned
         unsigned long long* st = status + tile;
         uint64_t excl = 0;
         if (tile == 0) {
-            __hip_atomic_store(st, SCS_P | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(st, SCS_P | tag | (agg & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(st, SCS_A | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(st, SCS_A | tag | (agg & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             int64_t t = (int64_t)tile - 1;
             while (true) {
                 const uint64_t w = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -433,7 +433,10 @@ __global__ void __launch_bounds__(SC_T) sc_onepass(T* data, uint64_t n, unsigned
                     --t;
                 }   // else: tile t has not published yet, read it again
             }
-            __hip_atomic_store(st, SCS_P | tag | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the value field is 40 bits: a prefix of 2^40 or more wraps in the published word (its flag
+            // and epoch stay intact, so successors never spin on it) — callers scan element counts of
+            // HBM-resident arrays, far below 2^40 (exclusive_scan_u64's contract)
+            __hip_atomic_store(st, SCS_P | tag | ((excl + agg) & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         s_pre = excl;
     }
@@ -662,6 +665,9 @@ void radix_sort_u32_from(hga_ctx* c, const uint32_t* src_k, const uint32_t* src_
                          uint64_t n, int bits, DevBuf& scratch) {
     radix_sort_impl<uint32_t>(c, keys, vals, n, bits > 32 ? 32 : bits, scratch, src_k, src_v);
 }
+// Exclusive scan in place.  Contract: the total stays below 2^40 (the look-back status words carry
+// 40-bit values; a larger total wraps, it never hangs).  Every caller scans counts of elements of
+// HBM-resident arrays (at most a few 10^9).
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch) {
     (void)scratch;   // the single-pass scan keeps its state in the ctx
     excl_scan_impl<uint64_t>(c, data, n);

@@ -1,10 +1,12 @@
 // ranks.h — one hga_ctx per GPU inside one process, for the CLIs' `--gpus N` mode.
 //
-// Rank r runs on device (dev0 + r) mod #devices with its own HIP stream.  When every rank has its own
-// device the ranks share an RCCL communicator over xGMI (hga_comm_unique_id + hga_comm_init, one
-// thread per rank).  When ranks share a device (fewer GPUs than ranks, or HGA_COMM=host) they exchange
+// Rank r runs on device (dev0 + r) mod #devices with its own HIP stream.  By default the ranks exchange
 // through an in-process host transport (hga_comm_init_host): the threads meet at a barrier and copy
-// each other's slices.  Collective library calls are issued by Ranks::each, one thread per rank.
+// each other's slices (verified on hardware: tests/test_cli_gpu.py, --gpus 2/3 equal one GPU).  With
+// HGA_COMM=rccl and every rank on its own device they share an RCCL communicator over xGMI
+// (hga_comm_unique_id + hga_comm_init, one thread per rank) — opt-in until a multi-GPU run of the CLIs
+// has recorded parity (bench.py --gpus N checks the RCCL exchange against the oracle on every N > 1
+// run).  Collective library calls are issued by Ranks::each, one thread per rank.
 #pragma once
 
 #include <barrier>
@@ -69,7 +71,7 @@ class Ranks {
         check(hga_device_count(&nd), "hga_device_count");
         if (nd < 1) throw std::runtime_error("no HIP device");
         const char* cm = std::getenv("HGA_COMM");
-        const bool host = n > nd || (cm && std::string(cm) == "host");
+        const bool host = n > nd || !(cm && std::string(cm) == "rccl");
         ctx.assign(n, nullptr);
         for (int r = 0; r < n; ++r) check(hga_ctx_create(&ctx[r], (dev0 + r) % nd), "hga_ctx_create");
         if (n == 1) return;
