@@ -33,8 +33,9 @@
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
 
-// Timing experiments (tools/build_variants.sh): each disables one part of a kernel; results are
-// wrong with any of them set, the default build has all 0.
+#ifndef HGA_XB1_NOFHIST
+#define HGA_XB1_NOFHIST 0   // timing experiment only (tools/build_variants.sh): 1 = no fine histogram (wrong results)
+#endif
 
 namespace hga {
 namespace {
@@ -259,7 +260,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
             rk[j] = 0;
             if ((wm >> j) & 1u) {
                 rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
-                atomicAdd(&fhist[bucket_of(h, kp)], 1u);
+                if (!HGA_XB1_NOFHIST) atomicAdd(&fhist[bucket_of(h, kp)], 1u);
             }
         }
         inst += __popc(wm);

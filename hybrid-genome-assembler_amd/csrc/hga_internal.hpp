@@ -156,6 +156,7 @@ struct CountState {
 
 struct LookupState {
     bool loaded = false, have_reads = false, ran = false;
+    bool packed_ok = false;   // packed / valid / starts / word_read hold the current reads (lookup_pack)
     int k = 0, km = 0;
     uint32_t n_sdk = 0;
     uint64_t slots = 0, fwords = 0, pk_words = 0;   // slots = table buckets
@@ -276,6 +277,7 @@ void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n);
 void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, uint64_t n,
                       uint32_t first_id);
 void lookup_run(hga_ctx* c);
+void lookup_pack(hga_ctx* c);   // per-base encode of the resident reads (lookup_run, hll_registers)
 void lookup_sizes(hga_ctx* c, hga_lookup_sizes* out);
 void lookup_fetch(hga_ctx* c, const hga_lookup_result* out);
 void hll_registers(hga_ctx* c, int k, int b, uint8_t* regs);

@@ -116,6 +116,7 @@ void hll_registers(hga_ctx* c, int k, int b, uint8_t* regs) {
     HGA_REQUIRE(k >= 1, HGA_ERR_INVALID, "k must be >= 1");
     HGA_REQUIRE(k <= 32, HGA_ERR_INVALID, "Kmer size is too big");   // KmerIterator.cpp:24-26
     HGA_REQUIRE(b >= 4 && b <= HL_MAXB, HGA_ERR_INVALID, "bit width must be in the range [4,14]");
+    if (!L.packed_ok) lookup_pack(c);
     const uint32_t m = 1u << b;
     const uint64_t nb = L.n_bases;
     const uint64_t n_threads = (nb + HL_P - 1) / HL_P;
