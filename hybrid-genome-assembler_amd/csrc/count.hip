@@ -33,6 +33,9 @@
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
 
+#ifndef HGA_B1_BRANCHFREE
+#define HGA_B1_BRANCHFREE 0   // 1: kc_bin1 ranks every window (invalid ones into per-lane dummy counters)
+#endif
 #ifndef HGA_XB1_NOFHIST
 #define HGA_XB1_NOFHIST 0   // timing experiment only (tools/build_variants.sh): 1 = no fine histogram (wrong results)
 #endif
@@ -119,6 +122,12 @@ __device__ __forceinline__ uint64_t frame_canon(const Frame<P>& f, int j, uint64
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+// (the builtin returns int: each half is widened as uint32_t, never sign-extended)
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((uint64_t)hi << 32) | lo;
+}
 
 // Level-1 blocks: every workgroup takes BLK-element blocks per region from one pool with a
 // single atomic (and a new one only when a block fills), so a tile's region runs are
@@ -134,9 +143,9 @@ constexpr uint32_t BLK = TP_B;   // >= a tile, so a tile's run spans at most two
 // 4 level-1 pool exhausted), [3] blocks used, [4] instances.
 // Block e always starts at e * BLK in the pool.  Workgroup w's first block of region r is
 // entry w * nb1 + r (no atomic); spill blocks are numbered from W * nb1 up (gstat[3]).
-__device__ __forceinline__ uint32_t new_block(unsigned long long* gstat, Blk* table, uint64_t table_cap,
-                                              uint32_t tag, unsigned long long& start) {
-    const unsigned long long e = atomicAdd(&gstat[3], 1ull);
+// Block e (reserved from gstat[3] by the caller) for the run tagged `tag`.
+__device__ __forceinline__ uint32_t claim_block(unsigned long long e, unsigned long long* gstat, Blk* table,
+                                                uint64_t table_cap, uint32_t tag, unsigned long long& start) {
     if (e >= table_cap) {
         atomicOr(&gstat[2], 4ull);
         start = table_cap * (unsigned long long)BLK;   // writes into this block are dropped
@@ -163,14 +172,17 @@ struct BinFile {
 #ifndef HGA_B1_WAVES
 #define HGA_B1_WAVES 1
 #endif
-template <class E1>
+// K > 0: k known at compile time (the usual k of a run): the window mask, the run-of-k validity
+// doubling and the mix's mask and shift fold to constants — with a runtime k those uniform values
+// spill out of the SGPR file (v_readlane per use) and runs_of is a chain of uniform selects.
+template <class E1, int K = 0>
 __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __restrict__ files, uint32_t F,
                                                 uint64_t st_pos, KP kp,
                                                 Blk* __restrict__ table, uint64_t table_cap,
                                                 uint64_t pool_cap, E1* __restrict__ out1,
                                                 uint32_t* __restrict__ wcnt, uint32_t* __restrict__ nblk,
                                                 unsigned long long* __restrict__ gstat) {
-    __shared__ uint32_t cnt1[NB1_MAX];
+    __shared__ uint32_t cnt1[NB1_MAX + (HGA_B1_BRANCHFREE ? 64 : 0)];
     __shared__ uint32_t off1[NB1_MAX + 1];
     __shared__ unsigned long long bstart[NB1_MAX];   // current block of each region
     __shared__ uint32_t bfill[NB1_MAX];              // elements already in it
@@ -178,8 +190,8 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
     __shared__ uint32_t nchain[NB1_MAX];             // blocks this workgroup used per region
     __shared__ unsigned long long base_a[NB1_MAX], base_b[NB1_MAX];
     __shared__ uint32_t take_a[NB1_MAX];
-    __shared__ uint32_t fhist[MAX_NB];
-    __shared__ E1 stage[TP_B];
+    __shared__ uint32_t fhist[MAX_NB + (HGA_B1_BRANCHFREE ? 64 : 0)];
+    __shared__ E1 stage[TP_B + 64];   // + one dummy slot per lane for invalid windows
     __shared__ uint32_t ws[NT_B / 64 + 1];
     // packed words [t0/16 - 2, t0/16 + 512) of this tile and the next (code | valid << 32)
     __shared__ uint64_t lpw[2][TP_B / 16 + 2];
@@ -248,19 +260,34 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
             load_raw(t0 + 2 * TP_B, nraw, nhalo);
         }
         buf ^= 1;
-        const uint64_t v64 = build_frame<P_B, false>(fr, kp.k, f);
-        const uint32_t wm = (uint32_t)(runs_of(v64, kp.k) >> 32);   // bit j: window at p0+j valid
+        const int kk = K ? K : kp.k;
+        const uint64_t v64 = build_frame<P_B, false>(fr, kk, f);
+        const uint32_t wm = (uint32_t)(runs_of(v64, kk) >> 32);   // bit j: window at p0+j valid
         uint32_t dd[P_B], rk[P_B];
         E1 ee[P_B];
+        const uint64_t wmask = K ? (K >= 32 ? ~0ull : ((1ull << (2 * K)) - 1)) : kp.mask;
+        Mix mx = kp.mix;
+        if (K) {
+            mx.mask = wmask;
+            mx.s = (uint32_t)(2 * K + 1) / 2;
+            mx.c1 = 0x9E3779B97F4A7C15ull;   // make_mix's constant
+        }
 #pragma unroll
         for (int j = 0; j < P_B; ++j) {
-            const uint64_t h = mix_fwd(frame_canon<P_B>(f, j, kp.mask), kp.mix);
+            const uint64_t h = mix_fwd(frame_canon<P_B>(f, j, wmask), mx);
             dd[j] = region_of(h, kp);
             ee[j] = (E1)(h & kp.r1mask);
-            rk[j] = 0;
-            if ((wm >> j) & 1u) {
-                rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
-                if (!HGA_XB1_NOFHIST) atomicAdd(&fhist[bucket_of(h, kp)], 1u);
+            if (HGA_B1_BRANCHFREE) {   // invalid windows count into this lane's dummy counters
+                const bool ok = (wm >> j) & 1u;
+                const uint32_t r = atomicAdd(&cnt1[ok ? dd[j] : NB1_MAX + (uint32_t)(tid & 63)], 1u);
+                if (!HGA_XB1_NOFHIST) atomicAdd(&fhist[ok ? bucket_of(h, kp) : MAX_NB + (uint32_t)(tid & 63)], 1u);
+                rk[j] = ok ? r : ~0u;
+            } else {
+                rk[j] = ~0u;   // invalid window: staged into this lane's dummy slot (no mask kept live)
+                if ((wm >> j) & 1u) {
+                    rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
+                    if (!HGA_XB1_NOFHIST) atomicAdd(&fhist[bucket_of(h, kp)], 1u);
+                }
             }
         }
         inst += __popc(wm);
@@ -268,19 +295,32 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
         if (tid < 64) {   // one wave: scan the <= 64 region counts, place them in the blocks
             const uint32_t c = tid < (int)nb1 ? cnt1[tid] : 0u;
             const uint32_t inc = wave_incl_scan(c, tid);
+            const uint32_t room = tid < (int)nb1 ? BLK - bfill[tid] : 0u;
+            const bool spill = tid < (int)nb1 && c > room;   // the run spills into a fresh block
             if (tid < (int)nb1) {
                 off1[tid] = inc - c;
                 cnt1[tid] = 0;
-                const uint32_t room = BLK - bfill[tid];
                 base_a[tid] = bstart[tid] + bfill[tid];
-                if (c <= room) {
+                if (!spill) {
                     take_a[tid] = c;
                     bfill[tid] += c;
-                } else {   // the run spills into a fresh block
+                }
+            }
+            // ONE returning atomic per workgroup and tile for all spilling runs: regions fill in
+            // lockstep, so at a C4 shard every lane of every workgroup spills in the same tiles (one
+            // atomic per lane queued 32 K same-address atomics, ~0.37 ms at ~88/us, per round)
+            const uint64_t sm = __ballot(spill);
+            if (sm) {
+                const int l0 = __builtin_ctzll(sm);
+                unsigned long long e0 = 0;
+                if (tid == l0) e0 = atomicAdd(&gstat[3], (unsigned long long)__popcll(sm));
+                e0 = __shfl(e0, l0, 64);
+                if (spill) {
                     take_a[tid] = room;
                     if (bent[tid] != 0xFFFFFFFFu) table[bent[tid]].used = BLK;
                     unsigned long long st;
-                    bent[tid] = new_block(gstat, table, table_cap, tag0 | tid, st);
+                    bent[tid] = claim_block(e0 + (unsigned long long)__popcll(sm & ((1ull << tid) - 1ull)), gstat,
+                                            table, table_cap, tag0 | tid, st);
                     ++nchain[tid];
                     bstart[tid] = st;
                     base_b[tid] = st;
@@ -290,17 +330,38 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
             if (tid == 63) off1[nb1] = inc;
         }
         lds_barrier();
+        {   // all 16 run offsets read first (no wait per element), then the writes
+            uint32_t o1[P_B];
 #pragma unroll
-        for (int j = 0; j < P_B; ++j)
-            if ((wm >> j) & 1u) stage[off1[dd[j]] + rk[j]] = ee[j];
+            for (int j = 0; j < P_B; ++j) o1[j] = off1[dd[j]];
+#pragma unroll
+            for (int j = 0; j < P_B; ++j)
+                stage[rk[j] != ~0u ? o1[j] + rk[j] : (uint32_t)TP_B + (uint32_t)(tid & 63)] = ee[j];
+        }
         lds_barrier();
         // flush: one wave per region run (region-uniform bases, lanes on consecutive elements)
+        // (run values made wave-uniform: scalar base addresses, 32-bit lane offsets, no per-element
+        // 64-bit select / bound check)
+        const uint32_t lane = (uint32_t)(tid & 63);
         for (uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6); d < nb1; d += NT_B / 64) {
-            const uint32_t o = off1[d], len = off1[d + 1] - o, ta = take_a[d];
-            const unsigned long long ba = base_a[d], bb = base_b[d];
-            for (uint32_t jj = (uint32_t)(tid & 63); jj < len; jj += 64) {
-                const unsigned long long g = jj < ta ? ba + jj : bb + (jj - ta);
-                if (g < pool_cap) out1[g] = stage[o + jj];
+            const uint32_t o = __builtin_amdgcn_readfirstlane(off1[d]);
+            const uint32_t len = __builtin_amdgcn_readfirstlane(off1[d + 1]) - o;
+            const uint32_t ta = __builtin_amdgcn_readfirstlane(take_a[d]);
+            const uint32_t na = len < ta ? len : ta;
+            const uint64_t ba = readfirstlane64(base_a[d]);
+            if (ba < pool_cap) {   // a block past the pool (table exhausted, error bit set) drops its writes
+                E1* __restrict__ dst = out1 + ba;
+                const uint32_t lim = (uint32_t)(pool_cap - ba < na ? pool_cap - ba : na);
+                for (uint32_t jj = lane; jj < lim; jj += 64) dst[jj] = stage[o + jj];
+            }
+            if (len > na) {   // the part past a full block, into the fresh one
+                const uint64_t bb = readfirstlane64(base_b[d]);
+                if (bb < pool_cap) {
+                    E1* __restrict__ dst = out1 + bb;
+                    const uint32_t n2 = len - na;
+                    const uint32_t lim = (uint32_t)(pool_cap - bb < n2 ? pool_cap - bb : n2);
+                    for (uint32_t jj = lane; jj < lim; jj += 64) dst[jj] = stage[o + na + jj];
+                }
             }
         }
         lds_barrier();
@@ -1746,6 +1807,13 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     // super-tiles: ~2 per CU over all files (one resident wave of bin1 workgroups, so each
     // (workgroup, region) fills about one level-1 block), whole tiles
     uint64_t st_pos = total_bytes / ((uint64_t)c->num_cu * HGA_B1_PER_CU) + 1;
+    // far larger inputs (a C4 rank shard: 7.4 M bases per super-tile, each region's run a chain of
+    // ~12 blocks) take more, smaller super-tiles instead, sized so that each (workgroup, region) still
+    // fits one block: every re-bin block then writes to precomputed offsets (a chained block reserves
+    // its digit runs with a returning device atomic per digit) and bin1 spills almost never
+    const uint64_t st_cap = (uint64_t)BLK * nb1 * 15 / 16;   // bases; instances <= bases
+    const char* sole_env = std::getenv("HGA_B1_SOLE");
+    if ((!sole_env || std::atoi(sole_env) != 0) && st_pos > st_cap + st_cap / 2) st_pos = st_cap;
     st_pos = std::max<uint64_t>(ST_ALIGN, (st_pos + ST_ALIGN - 1) / ST_ALIGN * ST_ALIGN);
     std::vector<uint32_t> n_st(F, 0);
     std::vector<BinFile> bf(F);
@@ -1799,12 +1867,17 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     // B1: level-1 binning of every file into pool blocks + per-workgroup fine histograms
     if (W) {
         c->launch("kc_bin1", [&] {
-            if (e1_32)
-                hipLaunchKernelGGL(kc_bin1<uint32_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
-                                   table_cap, pool_cap, static_cast<uint32_t*>(binned1), wcnt, nblk, gstat);
-            else
-                hipLaunchKernelGGL(kc_bin1<uint64_t>, dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table,
-                                   table_cap, pool_cap, static_cast<uint64_t*>(binned1), wcnt, nblk, gstat);
+#define HGA_BIN1(E1T, KK)                                                                                   \
+    hipLaunchKernelGGL((kc_bin1<E1T, KK>), dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table, table_cap, \
+                       pool_cap, static_cast<E1T*>(binned1), wcnt, nblk, gstat)
+            // compile-time k for the k of the configs (C1-C4: 19; C5: 15, 17, 19, 21)
+            if (e1_32 && kp.k == 19) HGA_BIN1(uint32_t, 19);
+            else if (e1_32 && kp.k == 17) HGA_BIN1(uint32_t, 17);
+            else if (e1_32 && kp.k == 15) HGA_BIN1(uint32_t, 15);
+            else if (e1_32) HGA_BIN1(uint32_t, 0);
+            else if (kp.k == 21) HGA_BIN1(uint64_t, 21);
+            else HGA_BIN1(uint64_t, 0);
+#undef HGA_BIN1
         });
         c->check_launch("kc_bin1");
     }

@@ -10,10 +10,13 @@ CODE = r'''
 import sys, json
 sys.path[:0] = [%r, %r]
 import bench
-r = bench.scale_leg(0)
-print(json.dumps({"ms": r["ms_per_step"], "sel": [r["selected"], r["discriminative"]], "k": r["kernels_ms"]}))
+r = bench.scale_leg(bench.Dist(1))
+print(json.dumps({"ms": r["ms_per_step"], "sel": [r["selected"], r["discriminative"]], "k": r["kernels_ms_rank0"]}))
 ''' % (ROOT, os.path.join(ROOT, "hybrid-genome-assembler_amd"))
-for so in sys.argv[1:]:
-    out = subprocess.run([sys.executable, "-c", CODE], env=dict(os.environ, HGA_LIB=so), capture_output=True,
-                         text=True, timeout=400)
-    print(os.path.basename(so), (out.stdout.strip().splitlines() or [out.stderr[-400:]])[-1], flush=True)
+for arg in sys.argv[1:]:   # lib.so or lib.so:VAR=value,VAR2=value
+    so, _, envs = arg.partition(":")
+    env = dict(os.environ, HGA_LIB=so)
+    for kv in filter(None, envs.split(",")):
+        env[kv.split("=")[0]] = kv.split("=", 1)[1]
+    out = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, timeout=400)
+    print(os.path.basename(arg), (out.stdout.strip().splitlines() or [out.stderr[-400:]])[-1], flush=True)
