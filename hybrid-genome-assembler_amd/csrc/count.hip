@@ -270,23 +270,29 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
         if (K) {
             mx.mask = wmask;
             mx.s = (uint32_t)(2 * K + 1) / 2;
-            mx.c1 = 0x9E3779B97F4A7C15ull;   // make_mix's constant
+            mx.c1 = kMixC1;   // make_mix's constant
         }
 #pragma unroll
         for (int j = 0; j < P_B; ++j) {
             const uint64_t h = mix_fwd(frame_canon<P_B>(f, j, wmask), mx);
-            dd[j] = region_of(h, kp);
-            ee[j] = (E1)(h & kp.r1mask);
+            // (k < 32: h < 4^k, so a shift by the full width 2k already gives region / bucket 0)
+            dd[j] = K && K < 32 ? (uint32_t)(h >> kp.r1bits) : region_of(h, kp);
+            // (u32 elements of a k with 2k - MAX_FB1 >= 32: r1bits == 32, the truncation is the mask)
+            constexpr bool trunc = K && sizeof(E1) == 4 && 2 * K - MAX_FB1 >= 32;
+            ee[j] = trunc ? (E1)h : (E1)(h & kp.r1mask);
             if (HGA_B1_BRANCHFREE) {   // invalid windows count into this lane's dummy counters
                 const bool ok = (wm >> j) & 1u;
                 const uint32_t r = atomicAdd(&cnt1[ok ? dd[j] : NB1_MAX + (uint32_t)(tid & 63)], 1u);
-                if (!HGA_XB1_NOFHIST) atomicAdd(&fhist[ok ? bucket_of(h, kp) : MAX_NB + (uint32_t)(tid & 63)], 1u);
+                if (!HGA_XB1_NOFHIST)
+                    atomicAdd(&fhist[ok ? (K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp))
+                                        : MAX_NB + (uint32_t)(tid & 63)], 1u);
                 rk[j] = ok ? r : ~0u;
             } else {
                 rk[j] = ~0u;   // invalid window: staged into this lane's dummy slot (no mask kept live)
                 if ((wm >> j) & 1u) {
                     rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
-                    if (!HGA_XB1_NOFHIST) atomicAdd(&fhist[bucket_of(h, kp)], 1u);
+                    if (!HGA_XB1_NOFHIST)
+                        atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp)], 1u);
                 }
             }
         }

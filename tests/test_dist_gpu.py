@@ -195,7 +195,7 @@ def _mix_inv(h, k):
     n = 2 * k
     mask = np.uint64((1 << n) - 1)
     s = np.uint64((n + 1) // 2)
-    c1 = 0x9E3779B97F4A7C15
+    c1 = 0x9E3779C07F4A7C15   # kmer_dev.hpp kMixC1
     c1i = pow(c1, -1, 1 << 64)
     h = h ^ (h >> s)
     return (h * np.uint64(c1i)) & mask
