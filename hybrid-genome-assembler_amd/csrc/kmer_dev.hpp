@@ -220,14 +220,14 @@ __device__ __forceinline__ void pack_bytes(const uint4 v, uint32_t& code, uint32
     for (int i = 0; i < 4; ++i) {
         const uint32_t u = REF ? ws[i] : (ws[i] & 0xDFDFDFDFu);
         uint32_t c4 = ((u >> 1) ^ (u >> 2)) & 0x03030303u;
-        uint32_t f = 0;
-#pragma unroll
-        for (uint32_t X : {0x41u, 0x43u, 0x47u, 0x54u}) {
-            const uint32_t t = u ^ (X * 0x01010101u);
-            f |= ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;   // bit 7: byte == X
-        }
+        // the base letter each byte's code stands for ('A' 'C' 'G' 'T' as bytes 0..3 of the table,
+        // one v_perm_b32 picks them by code): a byte is a base iff it equals its own letter, since
+        // every other byte value differs from all four
+        const uint32_t want = __builtin_amdgcn_perm(0u, 0x54474341u, c4);
+        const uint32_t d = u ^ want;
+        const uint32_t f = ~(((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;   // bit 7: byte is a base
         const uint32_t m = f >> 7;                        // bits 0, 8, 16, 24
-        c4 &= m * 3u;
+        if (REF) c4 &= m * 3u;   // KmerIterator: a non-base contributes code 0 (counting ignores it)
         const uint32_t r = __builtin_bswap32(c4);         // first base in the top byte
         const uint32_t t = (r | (r >> 6)) & 0x000F000Fu;
         code |= ((t | (t >> 12)) & 0xFFu) << (24 - 8 * i);
