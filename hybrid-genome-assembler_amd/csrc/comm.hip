@@ -6,16 +6,17 @@
 // (hga_comm_init_host: gloo, MPI, sockets, threads).  The protocol is the same either way:
 //   every rank: hga_count_run(ctx, 1) on its shard of every file (no per-file drop before the sum)
 //   hga_count_exchange(ctx, min):
-//     rows range-partitioned by canonical code on equal-mass splitters (owner o holds
-//     [spl[o-1], spl[o])), packed one u64 per row piece (exchange.hip kx_piece_hist/kx_pack_scatter),
-//     piece counts all-gathered, one all-to-all-v of the pieces, owner merge + `--bc` drop
-//     (kx_mb_*, run_jellyfish.sh:3-6).  Rows too wide to pack go as (key, counts[F]) rows.
+//     rows packed one u64 per row piece and ordered by hash bucket (owner o holds a range of the
+//     counting mix's top bits; exchange.hip kx_xb_hist / kx_xb_scatter), piece counts all-gathered,
+//     one all-to-all-v of the pieces and one of the per-bucket counts, owner merge of every sender's
+//     runs + `--bc` drop (kx_xb_merge, run_jellyfish.sh:3-6).  Rows too wide to pack go as
+//     (key, counts[F]) rows to code-range owners.
 //   Afterwards the count queries of the ctx answer for the whole input, identically on every rank:
 //     spec_hist  owners' (threshold, total, count) triples gathered and summed per bin
 //                (JellyfishOccurrenceReader.cpp:88-108 over all k-mers);
-//     select*    owners' sorted exports concatenated in rank order = ascending (:110-135);
+//     select*    owners' sorted exports merged by key = ascending (:110-135);
 //     select_device  keys stay on their owner, (n, n_discriminative) summed;
-//     rows/dump  owners' rows concatenated in rank order (:63-86; run_jellyfish.sh:5-6).
+//     rows/dump  owners' sorted rows merged by key (:63-86; run_jellyfish.sh:5-6).
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -212,10 +213,13 @@ struct DevEngine {
     int pack_bits() { return count_pack_bits(c); }
     void* send_buf(uint64_t bytes) { return c->count.xsend.ensure(bytes + 64); }
     void* recv_buf(uint64_t bytes) { return c->count.xrecv.ensure(bytes + 64); }
-    uint64_t partition_packed(const uint64_t* spl, uint32_t P, uint64_t* out, uint64_t cap, uint64_t* per) {
-        return count_partition_packed(c, spl, P, out, cap, per, false);
+    int xb_pack(uint32_t P, uint64_t* per) { return count_xb_pack(c, P, per); }
+    const void* xb_pieces() const { return c->count.xsend.p; }
+    const void* xb_dir() const { return c->count.xdir.p; }
+    void xb_merge(const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from, uint32_t P,
+                  uint32_t me, uint32_t min) {
+        count_xb_merge(c, in, n_from, dir_in, r_from, P, me, min);
     }
-    void merge_packed(const uint64_t* in, uint64_t n, uint32_t min) { count_merge_packed(c, in, n, min); }
     void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per) {
         count_partition(c, spl, P, keys, counts, per);
     }
@@ -276,8 +280,7 @@ void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::v
     std::vector<uint8_t> f(s.n_sel);
     count_fetch_selected(c, k.data(), f.data());
     CtxXport x(c);
-    keys = proto::concat(x, k);
-    flags = proto::concat(x, f);
+    proto::merge_sorted(x, k, f, 1, keys, flags);
 }
 
 void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
@@ -285,8 +288,7 @@ void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::v
     std::vector<uint32_t> v;
     count_rows(c, file, k, v);
     CtxXport x(c);
-    keys = proto::concat(x, k);
-    counts = proto::concat(x, v);
+    proto::merge_sorted(x, k, v, file < 0 ? c->count.n_files : 1, keys, counts);
 }
 
 // ---- sharded categorization ------------------------------------------------------------------

@@ -505,67 +505,69 @@ __global__ void __launch_bounds__(MB_NT) kx_mb_scatter(const uint64_t* __restric
 // kept rows staged in LDS and written coalesced into the bucket's own piece range of wkey /
 // wcnt (rows <= pieces), kept[b] = its rows.  No device-wide cursor: same-address device atomics
 // serialise, one per workgroup would bound the kernel.  gstat[1] |= 1 when a table filled (the
-// host reruns with pmul doubled).
+// host reruns with pmul doubled).  `ld(i)` returns the bucket's i-th piece, i < m; `a` is the
+// bucket's first slot in wkey / wcnt.  HASHED: the pieces carry the counting mix of the key (the
+// hash-bucket exchange), whose low bits are the slot; the rows get the key back (mix_inv).
 template <int T, int FMAX>
-__global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ bstart,
-                                                     PackFmt pf, uint64_t kmask, int mb,
-                                                     uint32_t min_c, uint32_t pmul, uint64_t* __restrict__ wkey,
-                                                     uint32_t* __restrict__ wcnt, uint64_t n,
-                                                     uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
+struct MergeLds {
+    unsigned long long tkey[T];
+    uint32_t tcnt[FMAX * T];
+    uint32_t tsat[(FMAX * T + 31) / 32];   // bit f * T + slot: that sum passed 2^32 - 1
+    uint32_t ws[MG_NT / 64 + 1];
+    uint32_t s_ovf;
+};
+template <int T, int FMAX, bool HASHED, class Load>
+__device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX>& L, const Load& ld, uint64_t m, uint64_t a, uint32_t b,
+                                             const PackFmt& pf, const Mix& mx, uint64_t kmask, uint32_t min_c, uint32_t pmul,
+                                             uint64_t* __restrict__ wkey, uint32_t* __restrict__ wcnt, uint64_t n,
+                                             uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
     static_assert(T % MG_NT == 0 && T / MG_NT <= 32, "each thread owns T / MG_NT <= 32 slots");
-    __shared__ unsigned long long tkey[T];
-    __shared__ uint32_t tcnt[FMAX * T];
-    __shared__ uint32_t tsat[(FMAX * T + 31) / 32];   // bit f * T + slot: that sum passed 2^32 - 1
-    __shared__ uint32_t ws[MG_NT / 64 + 1];
-    __shared__ uint32_t s_ovf;
     const int tid = threadIdx.x;
     uint64_t rb = 0;   // rows written so far (uniform)
-    const uint32_t b = blockIdx.x;
-    const uint64_t a = bstart[b], e = bstart[b + 1];
     const uint32_t F = pf.F;
-    uint32_t P = (uint32_t)(((e - a) * 4 + 3 * T - 1) / (3 * T));   // <= 3/4 load per pass
+    uint32_t P = (uint32_t)((m * 4 + 3 * T - 1) / (3 * T));   // <= 3/4 load per pass
     P = pmul ? (P ? P : 1u) * pmul : 1u;   // pmul 0: one pass whatever the size (test hook)
     P = P < 256u ? P : 256u;
-    if (tid == 0) s_ovf = 0;
+    if (tid == 0) L.s_ovf = 0;
     for (uint32_t p = 0; p < P; ++p) {
-        for (uint32_t j = tid; j < T; j += MG_NT) tkey[j] = MG_EMPTY;
-        for (uint32_t j = tid; j < F * T; j += MG_NT) tcnt[j] = 0;
-        for (uint32_t j = tid; j < (FMAX * T + 31) / 32; j += MG_NT) tsat[j] = 0;
+        for (uint32_t j = tid; j < T; j += MG_NT) L.tkey[j] = MG_EMPTY;
+        for (uint32_t j = tid; j < F * T; j += MG_NT) L.tcnt[j] = 0;
+        for (uint32_t j = tid; j < (FMAX * T + 31) / 32; j += MG_NT) L.tsat[j] = 0;
         __syncthreads();
-        for (uint64_t i0 = a; i0 < e; i0 += (uint64_t)MG_NT * MG_R) {
+        for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)MG_NT * MG_R) {
             uint64_t v[MG_R];
 #pragma unroll
             for (int q = 0; q < MG_R; ++q) {   // all loads issued before the table work
                 const uint64_t i = i0 + (uint64_t)q * MG_NT + tid;
-                v[q] = i < e ? sk[i] : 0ull;
+                v[q] = i < m ? ld(i) : 0ull;
             }
 #pragma unroll
             for (int q = 0; q < MG_R; ++q) {
-                if (i0 + (uint64_t)q * MG_NT + tid >= e) continue;
-                const uint64_t key = v[q] & kmask, g = fmix64(key);
-                if (P > 1 && (((uint32_t)(g >> 56) * P) >> 8) != p) continue;   // this pass's share
-                uint32_t slot = (uint32_t)g & (T - 1);
+                if (i0 + (uint64_t)q * MG_NT + tid >= m) continue;
+                const uint64_t key = v[q] & kmask;
+                if (P > 1 && (((uint32_t)(fmix64(key) >> 56) * P) >> 8) != p) continue;   // this pass's share
+                uint32_t slot = (uint32_t)(HASHED ? key : fmix64(key)) & (T - 1);
                 uint32_t t = 0;
                 for (; t < T; ++t) {
-                    const unsigned long long old = atomicCAS(&tkey[slot], MG_EMPTY, (unsigned long long)key);
+                    const unsigned long long old = atomicCAS(&L.tkey[slot], MG_EMPTY, (unsigned long long)key);
                     if (old == MG_EMPTY || old == key) break;
                     slot = (slot + 1) & (T - 1);
                 }
                 if (t == T) {
-                    s_ovf = 1;
+                    L.s_ovf = 1;
                     continue;
                 }
                 for (uint32_t f = 0; f < F; ++f) {
                     const uint32_t c = (uint32_t)((v[q] >> (pf.kb + (int)f * pf.cb)) & pf.cmax);
                     if (c) {   // counts saturate at 2^32 - 1 like count_merge's (a wrapping add is flagged)
-                        const uint32_t old = atomicAdd(&tcnt[f * T + slot], c);
-                        if (old + c < old) atomicOr(&tsat[(f * T + slot) >> 5], 1u << ((f * T + slot) & 31));
+                        const uint32_t old = atomicAdd(&L.tcnt[f * T + slot], c);
+                        if (old + c < old) atomicOr(&L.tsat[(f * T + slot) >> 5], 1u << ((f * T + slot) & 31));
                     }
                 }
             }
         }
         __syncthreads();
-        if (s_ovf) {
+        if (L.s_ovf) {
             if (tid == 0) {
                 atomicOr(&gstat[1], 1ull);
                 kept[b] = 0;   // the compaction that follows this attempt stays in bounds
@@ -579,45 +581,59 @@ __global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict_
             const uint32_t s = j * MG_NT + tid;
             bool any = false;
             for (uint32_t f = 0; f < F; ++f) {
-                uint32_t c = tcnt[f * T + s];
-                if ((tsat[(f * T + s) >> 5] >> ((f * T + s) & 31)) & 1u) c = 0xFFFFFFFFu;
+                uint32_t c = L.tcnt[f * T + s];
+                if ((L.tsat[(f * T + s) >> 5] >> ((f * T + s) & 31)) & 1u) c = 0xFFFFFFFFu;
                 c = c >= min_c ? c : 0u;
-                tcnt[f * T + s] = c;
+                L.tcnt[f * T + s] = c;
                 any |= c != 0u;
             }
-            if (tkey[s] != MG_EMPTY && any) keep |= 1u << j;
+            if (L.tkey[s] != MG_EMPTY && any) keep |= 1u << j;
         }
         uint32_t tot;
-        const uint32_t ex = block_excl_scan<MG_NT>((uint32_t)__popc(keep), ws, &tot);
+        const uint32_t ex = block_excl_scan<MG_NT>((uint32_t)__popc(keep), L.ws, &tot);
         // compaction in place: every source is read into registers before the barrier
         unsigned long long kk[ES];
         uint32_t cc[ES * FMAX];
 #pragma unroll
         for (int j = 0; j < ES; ++j) {
-            kk[j] = tkey[j * MG_NT + tid];
+            kk[j] = L.tkey[j * MG_NT + tid];
 #pragma unroll
-            for (int f = 0; f < FMAX; ++f) cc[j * FMAX + f] = f < (int)F ? tcnt[f * T + j * MG_NT + tid] : 0u;
+            for (int f = 0; f < FMAX; ++f) cc[j * FMAX + f] = f < (int)F ? L.tcnt[f * T + j * MG_NT + tid] : 0u;
         }
         __syncthreads();
         uint32_t o = ex;
 #pragma unroll
         for (int j = 0; j < ES; ++j)
             if ((keep >> j) & 1u) {
-                tkey[o] = kk[j];
+                L.tkey[o] = kk[j];
 #pragma unroll
                 for (int f = 0; f < FMAX; ++f)
-                    if (f < (int)F) tcnt[f * T + o] = cc[j * FMAX + f];
+                    if (f < (int)F) L.tcnt[f * T + o] = cc[j * FMAX + f];
                 ++o;
             }
         __syncthreads();
         for (uint32_t j = tid; j < tot; j += MG_NT) {
-            wkey[a + rb + j] = tkey[j];
-            for (uint32_t f = 0; f < F; ++f) wcnt[(uint64_t)f * n + a + rb + j] = tcnt[f * T + j];
+            wkey[a + rb + j] = HASHED ? mix_inv(L.tkey[j], mx) : (uint64_t)L.tkey[j];
+            for (uint32_t f = 0; f < F; ++f) wcnt[(uint64_t)f * n + a + rb + j] = L.tcnt[f * T + j];
         }
         rb += tot;
         __syncthreads();
     }
     if (tid == 0) kept[b] = rb;
+}
+
+template <int T, int FMAX>
+__global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ bstart,
+                                                     PackFmt pf, uint64_t kmask, int mb,
+                                                     uint32_t min_c, uint32_t pmul, uint64_t* __restrict__ wkey,
+                                                     uint32_t* __restrict__ wcnt, uint64_t n,
+                                                     uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
+    __shared__ MergeLds<T, FMAX> L;
+    (void)mb;
+    const uint32_t b = blockIdx.x;
+    const uint64_t a = bstart[b], e = bstart[b + 1];
+    merge_bucket<T, FMAX, false>(L, [&](uint64_t i) { return sk[a + i]; }, e - a, a, b, pf, Mix{}, kmask, min_c, pmul,
+                                 wkey, wcnt, n, kept, gstat);
 }
 
 // Rows of bucket b from its piece range to the scanned row offset off[b] (one workgroup per bucket).
@@ -631,6 +647,202 @@ __global__ void __launch_bounds__(256) kx_mb_compact(const uint64_t* __restrict_
         rkey[o + j] = wkey[a + j];
         for (uint32_t f = 0; f < F; ++f) rcnt[(uint64_t)f * cap + o + j] = wcnt[(uint64_t)f * n + a + j];
     }
+}
+
+// ---------------------------------------------------------------- hash-bucket exchange
+// hga_count_exchange's packed form (exchange_protocol.hpp): owners hold ranges of the counting mix's
+// top bits (kmer_dev.hpp Mix, the same on every rank).  The sender bins its pieces by the top R bits
+// (kx_xb_hist: per-bucket totals, one device atomic per tile and nonzero bucket; a scan;
+// kx_xb_scatter: ranks in LDS, one device atomic per tile and bucket reserves the tile's run), so
+// every owner's pieces leave as one bucket-ordered range and its directory as its slice of the
+// per-bucket counts.  The owner sums each of its buckets, at the coarsest resolution any sender
+// used, straight from the senders' runs (kx_xb_units sizes them, kx_xb_merge sums them): no
+// re-binning on the owner.
+constexpr int XB_MAXR = 14;        // sender resolution: LDS counters per tile
+constexpr int XB_NT = 1024;
+constexpr int XB_R = 8;            // rows per thread per tile
+constexpr uint64_t XB_TILE = (uint64_t)XB_NT * XB_R;
+constexpr uint32_t XB_MAXP = 1024; // senders (= KX_MAX_OWN)
+
+// A tile's rows: the counting mix of each key (the pieces carry it: the owner's buckets and table
+// slots are its bits), the packed single piece and the largest count.
+struct XbRows {
+    uint64_t h[XB_R], pk[XB_R];
+    uint32_t big[XB_R];
+};
+__device__ __forceinline__ void xb_load(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ cnt,
+                                        uint64_t cap, uint64_t rows, uint64_t t0, const PackFmt& pf, const Mix& mx,
+                                        XbRows& x) {
+#pragma unroll
+    for (int r = 0; r < XB_R; ++r) {
+        const uint64_t i = t0 + (uint64_t)r * XB_NT + threadIdx.x;
+        x.h[r] = i < rows ? keys[i] : 0ull;
+        x.big[r] = 0;
+    }
+#pragma unroll
+    for (int r = 0; r < XB_R; ++r) x.h[r] = mix_fwd(x.h[r], mx);
+#pragma unroll
+    for (int r = 0; r < XB_R; ++r) x.pk[r] = x.h[r];
+    for (uint32_t f = 0; f < pf.F; ++f) {
+        uint32_t c[XB_R];
+#pragma unroll
+        for (int r = 0; r < XB_R; ++r) {
+            const uint64_t i = t0 + (uint64_t)r * XB_NT + threadIdx.x;
+            c[r] = i < rows ? cnt[(uint64_t)f * cap + i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < XB_R; ++r) {
+            x.big[r] = c[r] > x.big[r] ? c[r] : x.big[r];
+            x.pk[r] |= (uint64_t)c[r] << (pf.kb + (int)f * pf.cb);   // the single piece (valid when big <= cmax)
+        }
+    }
+}
+__device__ __forceinline__ uint32_t xb_pieces_of(uint32_t big, const PackFmt& pf) {
+    return big <= pf.cmax ? 1u : (uint32_t)(((uint64_t)big + pf.cmax - 1) / pf.cmax);
+}
+__device__ __forceinline__ uint32_t xb_bucket(uint64_t h, const Mix& mx, int R) {
+    return (uint32_t)(h >> (mx.n - (uint32_t)R));
+}
+
+__global__ void __launch_bounds__(XB_NT) kx_xb_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ cnt,
+                                                    uint64_t cap, uint64_t rows, PackFmt pf, Mix mx, int R,
+                                                    unsigned long long* __restrict__ tot) {
+    __shared__ uint32_t h[1 << XB_MAXR];
+    const uint32_t nb = 1u << R;
+    for (uint32_t b = threadIdx.x; b < nb; b += XB_NT) h[b] = 0;
+    const uint64_t t0 = (uint64_t)blockIdx.x * XB_TILE;
+    XbRows x;
+    xb_load(keys, cnt, cap, rows, t0, pf, mx, x);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < XB_R; ++r)
+        if (t0 + (uint64_t)r * XB_NT + threadIdx.x < rows)
+            atomicAdd(&h[xb_bucket(x.h[r], mx, R)], xb_pieces_of(x.big[r], pf));
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += XB_NT)
+        if (h[b]) atomicAdd(&tot[b], (unsigned long long)h[b]);
+}
+
+// Pieces to their buckets: ranks within the tile in LDS, one device atomic per nonzero bucket on
+// `cursor` (initialised to the bucket starts) reserves the tile's run; a row whose count passes the
+// piece width writes its pieces one after the other.
+__global__ void __launch_bounds__(XB_NT) kx_xb_scatter(const uint64_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ cnt, uint64_t cap, uint64_t rows,
+                                                       PackFmt pf, Mix mx, int R,
+                                                       unsigned long long* __restrict__ cursor,
+                                                       uint64_t* __restrict__ out) {
+    __shared__ uint32_t c[1 << XB_MAXR];
+    __shared__ uint32_t st[1 << XB_MAXR];   // pieces < 2^32 per rank (count_xb_pack)
+    const uint32_t nb = 1u << R;
+    for (uint32_t b = threadIdx.x; b < nb; b += XB_NT) c[b] = 0;
+    const uint64_t t0 = (uint64_t)blockIdx.x * XB_TILE;
+    XbRows x;
+    xb_load(keys, cnt, cap, rows, t0, pf, mx, x);
+    __syncthreads();
+    uint32_t bk[XB_R], at[XB_R];
+#pragma unroll
+    for (int r = 0; r < XB_R; ++r) {
+        const bool live = t0 + (uint64_t)r * XB_NT + threadIdx.x < rows;
+        bk[r] = live ? xb_bucket(x.h[r], mx, R) : 0u;
+        at[r] = live ? atomicAdd(&c[bk[r]], xb_pieces_of(x.big[r], pf)) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += XB_NT)
+        if (c[b]) st[b] = (uint32_t)atomicAdd(&cursor[b], (unsigned long long)c[b]);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < XB_R; ++r) {
+        const uint64_t i = t0 + (uint64_t)r * XB_NT + threadIdx.x;
+        if (i >= rows) continue;
+        uint64_t pos = (uint64_t)st[bk[r]] + at[r];
+        if (x.big[r] <= pf.cmax) {
+            out[pos] = x.pk[r];
+            continue;
+        }
+        uint64_t left[8];   // F <= 8 on this path
+        for (uint32_t f = 0; f < pf.F; ++f) left[f] = cnt[(uint64_t)f * cap + i];
+        for (uint32_t p = 0, np = xb_pieces_of(x.big[r], pf); p < np; ++p) {
+            uint64_t v = x.h[r];
+            for (uint32_t f = 0; f < pf.F; ++f) {
+                const uint64_t q = left[f] < pf.cmax ? left[f] : pf.cmax;
+                left[f] -= q;
+                v |= q << (pf.kb + (int)f * pf.cb);
+            }
+            out[pos++] = v;
+        }
+    }
+}
+
+// Per-owner piece totals from the scanned bucket starts S (2^R + 1 entries).
+__global__ void kx_xb_owner_tot(const uint64_t* __restrict__ S, uint32_t P, int eb0, int R, uint64_t* __restrict__ per) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= P) return;
+    auto first = [&](uint32_t q) { return ((((uint64_t)q << eb0) + P - 1) / P) << (R - eb0); };
+    per[o] = S[first(o + 1)] - S[first(o)];
+}
+
+// Owner side.  S = exclusive scan of the received directories (sender-major, sender p's buckets
+// from entry src[p].off at resolution rmin + src[p].d): bucket u of this owner at the coarsest
+// resolution rmin is sender p's entries [u << d, (u + 1) << d), pieces S[off + (u << d)] ..
+// S[off + ((u + 1) << d)] of the received buffer (senders in rank order, like the directories).
+struct XbSrc {
+    uint64_t off;
+    uint32_t d, pad;
+};
+__global__ void kx_xb_units(const uint64_t* __restrict__ S, const XbSrc* __restrict__ src, uint32_t P, uint64_t units,
+                            uint64_t* __restrict__ ut) {
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u > units) return;
+    uint64_t t = 0;
+    if (u < units)
+        for (uint32_t p = 0; p < P; ++p) {
+            const XbSrc s = src[p];
+            t += S[s.off + ((u + 1) << s.d)] - S[s.off + (u << s.d)];
+        }
+    ut[u] = t;   // ut[units] = 0: the scan's total
+}
+
+template <int T, int FMAX>
+__global__ void __launch_bounds__(MG_NT) kx_xb_merge(const uint64_t* __restrict__ in, const uint64_t* __restrict__ S,
+                                                     const XbSrc* __restrict__ src, uint32_t P,
+                                                     const uint64_t* __restrict__ ubase, PackFmt pf, Mix mx, uint64_t kmask,
+                                                     uint32_t min_c, uint32_t pmul, uint64_t* __restrict__ wkey,
+                                                     uint32_t* __restrict__ wcnt, uint64_t n,
+                                                     uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
+    __shared__ MergeLds<T, FMAX> L;
+    __shared__ uint64_t rst[XB_MAXP];        // sender p's run start in `in`
+    __shared__ uint32_t rpre[XB_MAXP + 1];   // run lengths, exclusive prefix (a bucket holds < 2^32 pieces)
+    const uint32_t u = blockIdx.x;
+    const int tid = threadIdx.x;
+    for (uint32_t p = tid; p < P; p += MG_NT) {
+        const XbSrc s = src[p];
+        const uint64_t a = S[s.off + ((uint64_t)u << s.d)];
+        rst[p] = a;
+        rpre[p + 1] = (uint32_t)(S[s.off + ((uint64_t)(u + 1) << s.d)] - a);
+    }
+    __syncthreads();
+    if (tid < 64) {   // prefix over the senders, 64 at a time
+        uint32_t carry = 0;
+        for (uint32_t p0 = 0; p0 < P; p0 += 64) {
+            const uint32_t p = p0 + tid;
+            const uint32_t v = p < P ? rpre[p + 1] : 0u;
+            const uint32_t inc = wave_incl_scan(v, tid);
+            if (p < P) rpre[p + 1] = carry + inc;
+            carry += __shfl(inc, 63, 64);
+        }
+        if (tid == 0) rpre[0] = 0;
+    }
+    __syncthreads();
+    const uint64_t m = rpre[P];
+    auto ld = [&](uint64_t i) {   // i-th piece of the bucket: sender run by binary search
+        uint32_t lo = 0, hi = P;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (rpre[mid] <= i) lo = mid; else hi = mid;
+        }
+        return in[rst[lo] + (i - rpre[lo])];
+    };
+    merge_bucket<T, FMAX, true>(L, ld, m, ubase[u], u, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
 }
 
 }  // namespace
@@ -777,6 +989,154 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
             if (!hs[1]) break;
         }
         s.rows = hs[0];
+    }
+    s.min_per_file = min_c;
+    s.ran = true;
+    s.dist = false;
+    s.n_sel = 0;
+}
+
+// ---- hash-bucket exchange (hga_count_exchange, exchange_protocol.hpp) ---------------------------
+// Sender: this rank's rows as pieces in bucket order in `xsend`, the per-bucket counts in `xdir`,
+// pieces per owner in per_owner[P]; returns the bucket resolution R (about 1024 pieces per owner
+// bucket if every rank holds as many rows as this one, within [EB0, min(2k, XB_MAXR)]).
+int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner) {
+    auto& s = c->count;
+    count_settle(c);
+    HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    HGA_REQUIRE(P >= 1 && P <= XB_MAXP, HGA_ERR_INVALID, "at most 1024 ranks");
+    const int cb = count_pack_bits(c);
+    HGA_REQUIRE(cb > 0, HGA_ERR_INVALID, "rows of this k / file count do not pack into 64 bits");
+    const PackFmt pf{2 * s.k, cb, s.n_files, (1ull << cb) - 1};
+    const Mix mx = make_mix(s.k);
+    const int eb0 = std::min(10, 2 * s.k);
+    const int rmax = std::min(2 * s.k, XB_MAXR);
+    const uint64_t rows = s.rows;
+    int R = eb0;
+    while (R < rmax && ((uint64_t)1024 << R) < rows * P) ++R;
+    if (const char* e = std::getenv("HGA_XB_R")) R = std::max(eb0, std::min(rmax, std::atoi(e)));   // test hook
+    const uint64_t nb = 1ull << R;
+    char* w = static_cast<char*>(s.xch.ensure((3 * nb + 2) * 8 + 8 * (uint64_t)P + 64));
+    auto* tot = reinterpret_cast<unsigned long long*>(w);   // nb + 1: scanned = bucket starts
+    auto* cursor = tot + nb + 1;
+    uint64_t* per_d = reinterpret_cast<uint64_t*>(cursor + nb);
+    uint64_t* dir = static_cast<uint64_t*>(s.xdir.ensure(nb * 8 + 64));
+    HGA_HIP(hipMemsetAsync(tot, 0, (nb + 1) * 8, c->stream));
+    const uint64_t n_tiles = kx_blocks(rows, XB_TILE);
+    if (rows)
+        c->launch("kx_xb_hist", [&] {
+            hipLaunchKernelGGL(kx_xb_hist, dim3(n_tiles), dim3(XB_NT), 0, c->stream, s.rows_key.as<uint64_t>(),
+                               s.rows_cnt.as<uint32_t>(), s.rows_cap, rows, pf, mx, R, tot);
+        });
+    c->check_launch("kx_xb_hist");
+    HGA_HIP(hipMemcpyAsync(dir, tot, nb * 8, hipMemcpyDeviceToDevice, c->stream));
+    exclusive_scan_u64(c, reinterpret_cast<uint64_t*>(tot), nb + 1, s.scratch);
+    c->launch("kx_xb_pack", [&] {
+        hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream,
+                           reinterpret_cast<const uint64_t*>(tot), P, eb0, R, per_d);
+    });
+    c->check_launch("kx_xb_owner_tot");
+    HGA_HIP(hipMemcpyAsync(per_owner, per_d, 8 * (uint64_t)P, hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+    uint64_t total = 0;
+    for (uint32_t o = 0; o < P; ++o) total += per_owner[o];
+    HGA_REQUIRE(total < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per rank");
+    uint64_t* out = static_cast<uint64_t*>(s.xsend.ensure(std::max<uint64_t>(total, 1) * 8 + 64));
+    if (rows) {
+        HGA_HIP(hipMemcpyAsync(cursor, tot, nb * 8, hipMemcpyDeviceToDevice, c->stream));
+        c->launch("kx_xb_scatter", [&] {
+            hipLaunchKernelGGL(kx_xb_scatter, dim3(n_tiles), dim3(XB_NT), 0, c->stream, s.rows_key.as<uint64_t>(),
+                               s.rows_cnt.as<uint32_t>(), s.rows_cap, rows, pf, mx, R, cursor, out);
+        });
+        c->check_launch("kx_xb_scatter");
+    }
+    return R;
+}
+
+// Owner: every sender's runs of this owner's buckets -> merged ctx rows (drop at min_c per file).
+void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from,
+                    uint32_t P, uint32_t me, uint32_t min_c) {
+    auto& s = c->count;
+    count_settle(c);
+    HGA_REQUIRE(min_c >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
+    const int cb = count_pack_bits(c);
+    const PackFmt pf{2 * s.k, cb, s.n_files, (1ull << cb) - 1};
+    const uint64_t kmask = pf.kb >= 64 ? ~0ull : ((1ull << pf.kb) - 1);
+    const uint32_t F = s.n_files;
+    const Mix mx = make_mix(s.k);
+    const int eb0 = std::min(10, 2 * s.k);
+    auto first = [&](uint32_t o, int R) { return ((((uint64_t)o << eb0) + P - 1) / P) << (R - eb0); };
+    int rmin = 64;
+    for (uint32_t p = 0; p < P; ++p) {
+        HGA_REQUIRE(r_from[p] >= eb0 && r_from[p] <= 2 * s.k, HGA_ERR_COMM, "exchange: bad bucket resolution");
+        rmin = std::min(rmin, r_from[p]);
+    }
+    std::vector<XbSrc> src(P);
+    uint64_t n = 0, nd = 0;
+    for (uint32_t p = 0; p < P; ++p) {
+        src[p] = XbSrc{nd, (uint32_t)(r_from[p] - rmin), 0};
+        nd += first(me + 1, r_from[p]) - first(me, r_from[p]);
+        n += n_from[p];
+    }
+    HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per merge");
+    const uint64_t units = first(me + 1, rmin) - first(me, rmin);
+    const uint64_t cap = (std::max<uint64_t>(n, 1) + 3) & ~3ull;   // x4: 16-B row groups (kc_spec_hist)
+    s.rows_key.ensure(cap * 8);
+    s.rows_cnt.ensure(cap * 4 * F);
+    s.rows = 0;
+    s.rows_cap = cap;
+    // S (nd + 1) | ut = unit starts (units + 1) | kept (units + 1) | gstat 2 | wkey n | wcnt F n
+    char* w = static_cast<char*>(s.xch2.ensure((nd + 1 + 2 * (units + 1) + 2 + n) * 8 + 4ull * F * n + 64));
+    uint64_t* S = reinterpret_cast<uint64_t*>(w);
+    uint64_t* ut = S + nd + 1;
+    uint64_t* kept = ut + units + 1;
+    auto* gstat = reinterpret_cast<unsigned long long*>(kept + units + 1);
+    uint64_t* wkey = reinterpret_cast<uint64_t*>(gstat + 2);
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(wkey + n);
+    XbSrc* d_src = static_cast<XbSrc*>(s.xsrc.ensure(sizeof(XbSrc) * P + 64));
+    HGA_HIP(hipMemcpyAsync(d_src, src.data(), sizeof(XbSrc) * P, hipMemcpyHostToDevice, c->stream));
+    if (nd) HGA_HIP(hipMemcpyAsync(S, dir_in, nd * 8, hipMemcpyDeviceToDevice, c->stream));
+    HGA_HIP(hipMemsetAsync(S + nd, 0, 8, c->stream));
+    exclusive_scan_u64(c, S, nd + 1, s.scratch);
+    c->launch("kx_xb_units", [&] {
+        hipLaunchKernelGGL(kx_xb_units, dim3(kx_blocks(units + 1, 256)), dim3(256), 0, c->stream, S, d_src, P, units,
+                           ut);
+    });
+    c->check_launch("kx_xb_units");
+    exclusive_scan_u64(c, ut, units + 1, s.scratch);
+    unsigned long long* hs = static_cast<unsigned long long*>(c->pinned.ensure(16));
+    if (n) {
+        // one host round trip per attempt: the overflow flag and the row total come back together
+        for (uint32_t pmul = std::getenv("HGA_MB_ONE_PASS") ? 0u : 1u;; pmul = pmul ? pmul * 2 : 1u) {
+            HGA_REQUIRE(pmul <= 256, HGA_ERR_OOM, "owner merge: a bucket does not fit its LDS table");
+            HGA_HIP(hipMemsetAsync(gstat, 0, 16, c->stream));
+            c->launch("kx_xb_merge", [&] {
+                if (F <= 2)
+                    hipLaunchKernelGGL((kx_xb_merge<2048, 2>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P,
+                                       ut, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
+                else if (F <= 4)
+                    hipLaunchKernelGGL((kx_xb_merge<1024, 4>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P,
+                                       ut, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
+                else
+                    hipLaunchKernelGGL((kx_xb_merge<1024, 8>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P,
+                                       ut, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
+            });
+            c->check_launch("kx_xb_merge");
+            HGA_HIP(hipMemsetAsync(kept + units, 0, 8, c->stream));
+            exclusive_scan_u64(c, kept, units + 1, s.scratch);
+            c->launch("kx_mb_compact", [&] {
+                hipLaunchKernelGGL(kx_mb_compact, dim3(units), dim3(256), 0, c->stream, wkey, wcnt, n, F, ut, kept,
+                                   s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap);
+            });
+            c->check_launch("kx_mb_compact");
+            HGA_HIP(hipMemcpyAsync(hs, kept + units, 8, hipMemcpyDeviceToHost, c->stream));
+            HGA_HIP(hipMemcpyAsync(hs + 1, gstat + 1, 8, hipMemcpyDeviceToHost, c->stream));
+            c->sync();
+            if (!hs[1]) break;
+        }
+        s.rows = hs[0];
+    } else {
+        c->sync();
     }
     s.min_per_file = min_c;
     s.ran = true;

@@ -4,18 +4,26 @@
 // run the same code.  Plain C++17, no HIP.
 //
 //   every rank has counted its shard with min 1 (no per-file drop before the global sum);
-//   owner o holds canonical codes [spl[o-1], spl[o]) on equal-mass splitters;
-//   rows go to their owner as packed u64 pieces (or wide (key, counts[F]) rows), sizes first;
+//   packed rows (one u64 piece per row, the default): owners hold HASH ranges — the engine orders
+//   its pieces by a bijective hash of the key (the same on every rank) and counts them per hash
+//   bucket at a resolution of R bits (R may differ between ranks); bucket cells of the top EB0
+//   bits are split evenly over the owners; one all-to-all-v moves the pieces, a second the
+//   per-bucket counts (the owner's directory of every sender's runs), and the owner sums each of
+//   its buckets from all senders' runs without re-binning;
+//   wide rows ((key, counts[F]) when rows do not pack): owner o holds canonical codes
+//   [spl[o-1], spl[o]) on equal-mass splitters;
 //   the owner sums equal keys and drops counts < min per file (jellyfish --bc, run_jellyfish.sh:3-6);
 //   histogram triples of all owners are summed per (threshold, total) bin in std::map order
-//   (JellyfishOccurrenceReader.cpp:88-108); exports and rows concatenate in rank order, which is
-//   ascending code order (:63-86, :110-135).
+//   (JellyfishOccurrenceReader.cpp:88-108); exports and rows are the owners' sorted slices merged by
+//   key, i.e. ascending code order (:63-86, :110-135).
 #pragma once
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <queue>
 #include <utility>
 #include <vector>
 
@@ -47,14 +55,33 @@ inline std::vector<uint64_t> owner_splitters(int k, int P) {
     return out;
 }
 
+// Hash-bucket ownership of the packed exchange.  A rank's directory resolution R (bits of the hash,
+// R >= EB0) is its own choice; cell c of the top EB0 bits belongs to owner floor(c P / 2^EB0), so a
+// bucket at any resolution lies in one owner, and owner o's buckets at resolution R are the
+// contiguous range [cell_lo(o) << (R - EB0), cell_lo(o + 1) << (R - EB0)).  EB0 = 10 covers up to
+// 1024 owners (KX_MAX_OWN).
+inline int xb_base_bits(int k) { return std::min(10, 2 * k); }
+inline uint64_t xb_cell_lo(int o, int P, int eb0) {   // smallest cell c with floor(c P / 2^eb0) >= o
+    return (((uint64_t)o << eb0) + (uint64_t)P - 1) / (uint64_t)P;
+}
+inline uint64_t xb_first(int o, int P, int eb0, int R) { return xb_cell_lo(o, P, eb0) << (R - eb0); }
+inline uint32_t xb_owner_of_cell(uint64_t c, int P, int eb0) { return (uint32_t)((c * (uint64_t)P) >> eb0); }
+
 // Engine E (the rank's rows after a local count with min 1):
 //   int k(); uint32_t n_files(); uint64_t rows(); int pack_bits();
 //   void* send_buf(uint64_t bytes); void* recv_buf(uint64_t bytes);     (engine memory, kept by E)
-//   uint64_t partition_packed(const uint64_t* spl, uint32_t P, uint64_t* out, uint64_t cap, uint64_t* per);
-//       (returns the piece total; writes nothing when it exceeds cap)
-//   void merge_packed(const uint64_t* pieces, uint64_t n, uint32_t min);
-//   void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per);
-//   void merge(const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min);
+//   packed (hash-bucket owners):
+//     int xb_pack(uint32_t P, uint64_t* per_owner);
+//         orders the pieces by bucket (owner-major) in engine memory xb_pieces() and counts them per
+//         bucket in xb_dir() (u64, 2^R entries); returns R; per_owner[o] = pieces for owner o
+//     const void* xb_pieces(); const void* xb_dir();
+//     void xb_merge(const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from,
+//                   uint32_t P, uint32_t me, uint32_t min);
+//         in = every sender's pieces for this owner (sender order, n_from[p] each); dir_in = every
+//         sender's counts of this owner's buckets at its resolution r_from[p] (sender order)
+//   wide (code-range owners):
+//     void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per);
+//     void merge(const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min);
 //   void sync();
 // Returns the pieces / rows this owner received.  `extra` (same length on every rank) rides in the
 // piece-count all-gather; *extra_sum receives its element-wise sums over the ranks (one collective
@@ -62,42 +89,50 @@ inline std::vector<uint64_t> owner_splitters(int k, int P) {
 template <class E>
 uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file, const std::vector<uint64_t>& extra = {},
                         std::vector<uint64_t>* extra_sum = nullptr) {
-    const int P = x.nranks;
-    const size_t X = extra.size(), W = (size_t)P + X;
-    const std::vector<uint64_t> spl = owner_splitters(e.k(), P);
+    const int P = x.nranks, me = x.rank;
+    const size_t X = extra.size(), W = (size_t)P + 1 + X;
     std::vector<uint64_t> per(W), all((size_t)P * W), rn(P), sb(P), rb(P);
-    for (size_t i = 0; i < X; ++i) per[P + i] = extra[i];
+    for (size_t i = 0; i < X; ++i) per[P + 1 + i] = extra[i];
     auto recv_counts = [&] {
         x.allgather(per.data(), 8 * (uint64_t)W, all.data());
         uint64_t n = 0;
-        for (int p = 0; p < P; ++p) n += (rn[p] = all[(size_t)p * W + x.rank]);
+        for (int p = 0; p < P; ++p) n += (rn[p] = all[(size_t)p * W + me]);
         if (extra_sum) {
             extra_sum->assign(X, 0);
             for (int p = 0; p < P; ++p)
-                for (size_t i = 0; i < X; ++i) (*extra_sum)[i] += all[(size_t)p * W + P + i];
+                for (size_t i = 0; i < X; ++i) (*extra_sum)[i] += all[(size_t)p * W + P + 1 + i];
         }
         return n;
     };
     if (e.pack_bits() > 0) {   // one u64 piece per row (a count past the piece width: several pieces)
-        const uint64_t rows = e.rows();
-        uint64_t cap = rows + rows / 64 + 1024;
-        uint64_t* out = static_cast<uint64_t*>(e.send_buf(cap * 8));
-        uint64_t total = e.partition_packed(spl.data(), (uint32_t)P, out, cap, per.data());
-        if (total > cap) {
-            cap = total;
-            out = static_cast<uint64_t*>(e.send_buf(cap * 8));
-            total = e.partition_packed(spl.data(), (uint32_t)P, out, cap, per.data());
-        }
+        const int eb0 = xb_base_bits(e.k());
+        const int R = e.xb_pack((uint32_t)P, per.data());
+        per[P] = (uint64_t)R;
         const uint64_t n = recv_counts();
-        uint64_t* in = static_cast<uint64_t*>(e.recv_buf((n ? n : 1) * 8));
+        std::vector<int> rf(P);
+        uint64_t nd = 0;   // directory entries this owner receives
+        for (int p = 0; p < P; ++p) {
+            rf[p] = (int)all[(size_t)p * W + P];
+            nd += xb_first(me + 1, P, eb0, rf[p]) - xb_first(me, P, eb0, rf[p]);
+        }
+        // engine receive memory: the pieces, then the directories (8-byte aligned)
+        char* in = static_cast<char*>(e.recv_buf((n + nd + 1) * 8));
+        uint64_t* dir_in = reinterpret_cast<uint64_t*>(in + n * 8);
         for (int p = 0; p < P; ++p) {
             sb[p] = per[p] * 8;
             rb[p] = rn[p] * 8;
         }
-        x.alltoallv_eng(out, sb.data(), in, rb.data());
-        e.merge_packed(in, n, min_per_file);
+        x.alltoallv_eng(e.xb_pieces(), sb.data(), in, rb.data());
+        for (int p = 0; p < P; ++p) {
+            sb[p] = 8 * (xb_first(p + 1, P, eb0, R) - xb_first(p, P, eb0, R));
+            rb[p] = 8 * (xb_first(me + 1, P, eb0, rf[p]) - xb_first(me, P, eb0, rf[p]));
+        }
+        x.alltoallv_eng(e.xb_dir(), sb.data(), dir_in, rb.data());
+        e.xb_merge(reinterpret_cast<const uint64_t*>(in), rn.data(), dir_in, rf.data(), (uint32_t)P, (uint32_t)me,
+                   min_per_file);
         return n;
     }
+    const std::vector<uint64_t> spl = owner_splitters(e.k(), P);
     // wide rows: keys u64 then counts u32[F] row-major, one all-to-all each
     const uint32_t F = e.n_files();
     const uint64_t rows = e.rows(), rcap = rows ? rows : 1;
@@ -182,6 +217,42 @@ std::vector<T> concat(Xport& x, const std::vector<T>& mine) {
         out.insert(out.end(), v, v + pt.size() / sizeof(T));
     }
     return out;
+}
+
+// Every rank's ascending keys (with vw values of type V per key) merged into one ascending list:
+// the owners' slices of exports and rows (hash-bucket owners interleave in code order; code-range
+// owners come out concatenated in rank order).  Equal keys keep rank order.
+template <class V>
+void merge_sorted(Xport& x, const std::vector<uint64_t>& keys, const std::vector<V>& vals, size_t vw,
+                  std::vector<uint64_t>& out_keys, std::vector<V>& out_vals) {
+    const auto pk = x.allgatherv(keys.data(), keys.size() * 8);
+    const auto pv = x.allgatherv(vals.data(), vals.size() * sizeof(V));
+    const int P = x.nranks;
+    std::vector<const uint64_t*> k(P);
+    std::vector<const V*> v(P);
+    std::vector<size_t> n(P), at(P, 0);
+    size_t tot = 0;
+    for (int p = 0; p < P; ++p) {
+        k[p] = reinterpret_cast<const uint64_t*>(pk[p].data());
+        v[p] = reinterpret_cast<const V*>(pv[p].data());
+        tot += (n[p] = pk[p].size() / 8);
+    }
+    out_keys.clear();
+    out_vals.clear();
+    out_keys.reserve(tot);
+    out_vals.reserve(tot * vw);
+    using Head = std::pair<uint64_t, int>;   // (key, rank): smallest key first, ties by rank
+    std::priority_queue<Head, std::vector<Head>, std::greater<Head>> q;
+    for (int p = 0; p < P; ++p)
+        if (n[p]) q.push({k[p][0], p});
+    while (!q.empty()) {
+        const int p = q.top().second;
+        q.pop();
+        const size_t i = at[p]++;
+        out_keys.push_back(k[p][i]);
+        out_vals.insert(out_vals.end(), v[p] + i * vw, v[p] + (i + 1) * vw);
+        if (at[p] < n[p]) q.push({k[p][at[p]], p});
+    }
 }
 
 // ---- sharded categorization -------------------------------------------

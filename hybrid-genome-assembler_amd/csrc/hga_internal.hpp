@@ -136,7 +136,7 @@ struct CountState {
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
         sel_keys, sel_tmp, sel_wtmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, blist,
-        binned3, file_start3, xsend, xrecv;
+        binned3, file_start3, xsend, xrecv, xdir, xsrc;
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t sel_grid = 0;   // kc_select workgroups: as many as are resident at once (count.hip)
@@ -257,6 +257,12 @@ int count_pack_bits(hga_ctx* c);
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,
                                 uint64_t cap_out, uint64_t* pieces_per_owner, bool sync_out = true);
 void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t min_c);
+// hash-bucket exchange (exchange.hip; protocol in exchange_protocol.hpp): the sender's pieces in
+// bucket order in `xsend` and its per-bucket counts in `xdir` (returns the resolution R), and the
+// owner's merge of every sender's runs of its buckets
+int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner);
+void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in,
+                    const int* r_from, uint32_t P, uint32_t me, uint32_t min_c);
 
 // comm.hip: multi-GPU counting (hga_comm_*, hga_count_exchange) and the global query answers
 void comm_init_rccl(hga_ctx* c, const void* id, int rank, int nranks);

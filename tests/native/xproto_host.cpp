@@ -70,13 +70,24 @@ int jf_code(unsigned char c) {
     }
 }
 
+// the device's bucket hash (kmer_dev.hpp Mix), restated: multiply by an odd constant mod 4^k, then
+// xor the top half into the bottom half
+uint64_t mix_host(uint64_t x, int k) {
+    const int n = 2 * k;
+    const uint64_t mask = n >= 64 ? ~0ull : (1ull << n) - 1;
+    x = (x * 0x9E3779C07F4A7C15ull) & mask;
+    return x ^ (x >> ((n + 1) / 2));
+}
+
 struct HostEngine {
     int k_ = 0;
     uint32_t F = 0;
+    int rank_ = 0;
     bool allow_pack = true;
     std::vector<uint64_t> keys;                 // ascending
     std::vector<std::vector<uint32_t>> counts;  // per row, F counts
     std::vector<char> sbuf, rbuf;
+    std::vector<uint64_t> xbp, xbd;             // pieces in bucket order, per-bucket counts
 
     int k() const { return k_; }
     uint32_t n_files() const { return F; }
@@ -108,13 +119,17 @@ struct HostEngine {
             counts.push_back(c);
         }
     }
-    uint64_t partition_packed(const uint64_t* spl, uint32_t P, uint64_t* out, uint64_t cap, uint64_t* per) {
+    // pieces of every row, by hash bucket at resolution R; R differs between ranks on purpose (the
+    // owners merge at the coarsest one)
+    int xb_pack(uint32_t P, uint64_t* per) {
+        const int eb0 = hga::proto::xb_base_bits(k_);
+        const int R = std::min(2 * k_, eb0 + rank_ % 3);
         const int cb = pack_bits();
         const uint64_t cmax = (1ull << cb) - 1;
-        std::vector<std::vector<uint64_t>> by(P);
+        std::vector<std::pair<uint64_t, uint64_t>> t;   // (bucket, piece)
         for (size_t i = 0; i < keys.size(); ++i) {
+            const uint64_t b = mix_host(keys[i], k_) >> (2 * k_ - R);
             std::vector<uint64_t> left(counts[i].begin(), counts[i].end());
-            auto& o = by[owner(spl, P, keys[i])];
             while (true) {
                 uint64_t v = keys[i];
                 bool more = false;
@@ -124,25 +139,62 @@ struct HostEngine {
                     more |= left[f] != 0;
                     v |= c << (2 * k_ + f * cb);
                 }
-                o.push_back(v);
+                t.push_back({b, v});
                 if (!more) break;
             }
         }
-        uint64_t tot = 0;
-        for (uint32_t p = 0; p < P; ++p) tot += (per[p] = by[p].size());
-        if (tot > cap) return tot;
-        for (auto& v : by)
-            for (auto x : v) *out++ = x;
-        return tot;
+        std::stable_sort(t.begin(), t.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+        xbd.assign(1ull << R, 0);
+        xbp.clear();
+        for (auto& e : t) {
+            xbd[e.first]++;
+            xbp.push_back(e.second);
+        }
+        xbp.push_back(0);   // never empty
+        for (uint32_t o = 0; o < P; ++o) {
+            per[o] = 0;
+            for (uint64_t j = hga::proto::xb_first(o, P, eb0, R); j < hga::proto::xb_first(o + 1, P, eb0, R); ++j)
+                per[o] += xbd[j];
+        }
+        return R;
     }
-    void merge_packed(const uint64_t* in, uint64_t n, uint32_t min) {
+    const void* xb_pieces() const { return xbp.data(); }
+    const void* xb_dir() const { return xbd.data(); }
+    // every bucket of the coarsest resolution from all senders' runs; checks that each run holds only
+    // keys of its bucket and that the runs cover every received piece
+    void xb_merge(const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from, uint32_t P,
+                  uint32_t me, uint32_t min) {
+        const int eb0 = hga::proto::xb_base_bits(k_);
         const int cb = pack_bits();
         const uint64_t kmask = 2 * k_ >= 64 ? ~0ull : (1ull << (2 * k_)) - 1, cmax = (1ull << cb) - 1;
-        std::map<uint64_t, std::vector<uint64_t>> m;
-        for (uint64_t i = 0; i < n; ++i) {
-            auto& c = m.try_emplace(in[i] & kmask, std::vector<uint64_t>(F, 0)).first->second;
-            for (uint32_t f = 0; f < F; ++f) c[f] += (in[i] >> (2 * k_ + f * cb)) & cmax;
+        int rmin = 64;
+        for (uint32_t p = 0; p < P; ++p) rmin = std::min(rmin, r_from[p]);
+        std::vector<std::vector<uint64_t>> pre(P);   // per sender: piece offset of each of its buckets
+        std::vector<const uint64_t*> src(P);
+        uint64_t po = 0, dof = 0;
+        for (uint32_t p = 0; p < P; ++p) {
+            const uint64_t ne = hga::proto::xb_first(me + 1, P, eb0, r_from[p]) - hga::proto::xb_first(me, P, eb0, r_from[p]);
+            pre[p].assign(ne + 1, 0);
+            for (uint64_t j = 0; j < ne; ++j) pre[p][j + 1] = pre[p][j] + dir_in[dof + j];
+            if (pre[p][ne] != n_from[p]) throw std::runtime_error("directory does not cover the pieces");
+            src[p] = in + po;
+            po += n_from[p];
+            dof += ne;
         }
+        const uint64_t u0 = hga::proto::xb_first(me, P, eb0, rmin), u1 = hga::proto::xb_first(me + 1, P, eb0, rmin);
+        std::map<uint64_t, std::vector<uint64_t>> m;
+        uint64_t seen = 0;
+        for (uint64_t u = 0; u < u1 - u0; ++u)
+            for (uint32_t p = 0; p < P; ++p) {
+                const int d = r_from[p] - rmin;
+                for (uint64_t i = pre[p][u << d]; i < pre[p][(u + 1) << d]; ++i, ++seen) {
+                    const uint64_t key = src[p][i] & kmask;
+                    if ((mix_host(key, k_) >> (2 * k_ - rmin)) != u0 + u) throw std::runtime_error("piece in a foreign bucket");
+                    auto& c = m.try_emplace(key, std::vector<uint64_t>(F, 0)).first->second;
+                    for (uint32_t f = 0; f < F; ++f) c[f] += (src[p][i] >> (2 * k_ + f * cb)) & cmax;
+                }
+            }
+        if (seen != po) throw std::runtime_error("pieces outside every bucket");
         set_rows(m, min);
     }
     void partition(const uint64_t* spl, uint32_t P, uint64_t* ko, uint32_t* co, uint64_t* per) {
@@ -190,6 +242,7 @@ void* xt_create(int k, int n_files, int rank, int nranks, const hga_transport* t
     r->e.k_ = k;
     r->e.F = (uint32_t)n_files;
     r->e.allow_pack = allow_pack != 0;
+    r->e.rank_ = rank;
     r->x.rank = rank;
     r->x.nranks = nranks;
     r->x.t = *t;
@@ -257,7 +310,7 @@ int64_t xt_hist_merge(void* h, const int64_t* local, int64_t n_triples, int64_t*
     return (int64_t)g.size() / 3;
 }
 
-// global export: keys ascending (owners in rank order), flags; *n_discr over all owners
+// global export: keys ascending (the owners' slices merged), flags; *n_discr over all owners
 int64_t xt_select(void* h, int64_t lower, int64_t upper, uint64_t** keys, uint8_t** flags, uint64_t* n_discr) {
     auto* r = static_cast<Rank*>(h);
     std::vector<uint64_t> k;
@@ -273,8 +326,9 @@ int64_t xt_select(void* h, int64_t lower, int64_t upper, uint64_t** keys, uint8_
             d += nz == 1;
         }
     }
-    const auto gk = hga::proto::concat(r->x, k);
-    const auto gf = hga::proto::concat(r->x, f);
+    std::vector<uint64_t> gk;
+    std::vector<uint8_t> gf;
+    hga::proto::merge_sorted(r->x, k, f, 1, gk, gf);
     *n_discr = hga::proto::sum_u64(r->x, {d})[0];
     *keys = dup(gk);
     *flags = dup(gf);
@@ -286,8 +340,9 @@ int64_t xt_rows(void* h, uint64_t** keys, uint32_t** counts) {
     auto* r = static_cast<Rank*>(h);
     std::vector<uint32_t> c;
     for (auto& v : r->e.counts) c.insert(c.end(), v.begin(), v.end());
-    const auto gk = hga::proto::concat(r->x, r->e.keys);
-    const auto gc = hga::proto::concat(r->x, c);
+    std::vector<uint64_t> gk;
+    std::vector<uint32_t> gc;
+    hga::proto::merge_sorted(r->x, r->e.keys, c, r->e.F, gk, gc);
     *keys = dup(gk);
     *counts = dup(gc);
     return (int64_t)gk.size();

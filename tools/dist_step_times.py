@@ -39,4 +39,14 @@ for it in range(14):
     whole.append(time.perf_counter() - t00)
 print({n: round(float(np.median(v[4:])) * 1e3, 3) for n, v in acc.items()},
       "step ms", round(float(np.median(whole[4:])) * 1e3, 3), flush=True)
+# per-kernel device time of the exchange (event-timed launches, 5 steps)
+names = ["kx_xb_hist", "kx_xb_pack", "kx_xb_scatter", "kx_xb_units", "kx_xb_merge", "kx_mb_compact", "scan"]
+ctx.profile(True)
+ctx.profile_reset()
+for it in range(5):
+    for n, f in calls:
+        f()
+ctx.sync()
+print({n: round(ctx.profile_get(n)[0] / 5, 4) for n in names},
+      "(ms per step)", flush=True)
 ctx.close()
