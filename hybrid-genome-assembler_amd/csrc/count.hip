@@ -1082,12 +1082,27 @@ __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t
     return false;
 }
 
+// Exchange emission (hga_count_exchange's hash buckets, exchange.hip count_xb_pack): with a
+// communicator attached, count_run(ctx, 1) also writes every bucket's rows as packed pieces that
+// carry the mix h of the key (h in the low 2k bits, file f's count in bits [2k + f cb, ...), a count
+// past 2^cb - 1 split over several pieces) into `slab` from the bucket's first binned position
+// (pieces <= instances), grouped by the next x bits of h in ascending order (sub-ranges of a split
+// bucket are emitted in ascending order too), and each (bucket, sub-bin)'s piece count into
+// dir[(b << x) + sub].  The owner side then needs no hashing and the sender no binning pass.
+struct XbEmit {
+    uint64_t* slab;   // nullptr: off
+    uint64_t* dir;
+    uint32_t x, cb, kb, cmax;
+};
+constexpr uint32_t XE_MAXSUB = 64;
+static_assert(sizeof(XbEmit) <= 32, "CountState::xemit_host holds one XbEmit");
+
 __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t* __restrict__ binned,
                                                       const uint64_t* __restrict__ fs, uint32_t F,
                                                       uint32_t min_count, KP kp, uint64_t* __restrict__ out_key,
                                                       uint32_t* __restrict__ out_cnt, uint64_t cap,
                                                       unsigned long long* __restrict__ gstat,
-                                                      uint32_t* __restrict__ blist) {
+                                                      uint32_t* __restrict__ blist, const XbEmit* __restrict__ xep) {
     __shared__ __attribute__((aligned(16))) uint32_t tkey[T_S];
     __shared__ __attribute__((aligned(16))) uint32_t tcnt[T_S + 64];   // + per-lane dummies (branch-free hits)
     __shared__ uint32_t qbuf[NT_P / 64][QN_P];
@@ -1095,6 +1110,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
     __shared__ uint32_t stk_lo[40], stk_hi[40];
     __shared__ uint32_t ws[NT_P / 64 + 1];
     __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_xe[XE_MAXSUB], s_xpre[XE_MAXSUB], s_xtot[XE_MAXSUB], s_xw;   // exchange emission
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     uint32_t* myq = qbuf[tid >> 6];
@@ -1114,7 +1130,9 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         stk_hi[0] = full_hi;
         s_sp = 1;
         s_ranges = 0;
+        s_xw = 0;
     }
+    if (tid < (int)XE_MAXSUB) s_xe[tid] = s_xtot[tid] = 0;
     __syncthreads();
     while (true) {
         const uint32_t sp = s_sp;
@@ -1291,10 +1309,10 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
             }
         __syncthreads();
         const uint64_t base = s_base;
+        const uint64_t hb = kp.fb ? ((uint64_t)b << rbits) : 0ull;
         if (base + tot > cap) {
             if (tid == 0 && tot) atomicOr(&gstat[2], 2ull);
         } else {
-            const uint64_t hb = kp.fb ? ((uint64_t)b << rbits) : 0ull;
             for (uint32_t j = tid; j < tot; j += NT_P) {
                 const uint32_t c = tcnt[j];
                 out_key[base + j] = mix_inv(hb | tkey[j], kp.mix);
@@ -1306,8 +1324,50 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                 }
             }
         }
+        if (xep) {   // uniform: the exchange pieces of these rows, by sub-bin, after the earlier ranges'
+            const XbEmit xe = *xep;
+            for (uint32_t j = tid; j < tot; j += NT_P) {   // pieces per sub-bin
+                const uint32_t c = tcnt[j];
+                const uint32_t big = F == 1 ? c : max(c & 0xFFFFu, c >> 16);
+                atomicAdd(&s_xe[xe.x ? tkey[j] >> (rbits - xe.x) : 0u], big <= xe.cmax ? 1u : (big + xe.cmax - 1) / xe.cmax);
+            }
+            __syncthreads();
+            if (tid < 64) {   // sub-bin cursors after the pieces already written for this bucket
+                const uint32_t nsub = 1u << xe.x;
+                const uint32_t v = (uint32_t)tid < nsub ? s_xe[tid] : 0u;
+                const uint32_t inc = wave_incl_scan(v, tid);
+                const uint32_t w0 = s_xw;
+                s_xpre[tid] = w0 + inc - v;
+                if ((uint32_t)tid < nsub) {
+                    s_xtot[tid] += v;
+                    s_xe[tid] = 0;
+                }
+                if (tid == 63) s_xw = w0 + inc;
+            }
+            __syncthreads();
+            uint64_t* __restrict__ slab = xe.slab + f[0];
+            for (uint32_t j = tid; j < tot; j += NT_P) {
+                const uint32_t c = tcnt[j], r = tkey[j];
+                const uint64_t h = hb | r;
+                uint32_t c0 = F == 1 ? c : c & 0xFFFFu, c1 = F == 1 ? 0u : c >> 16;
+                const uint32_t big = max(c0, c1);
+                const uint32_t np = big <= xe.cmax ? 1u : (big + xe.cmax - 1) / xe.cmax;
+                uint64_t at = atomicAdd(&s_xpre[xe.x ? r >> (rbits - xe.x) : 0u], np);
+                if (np == 1) {
+                    slab[at] = h | ((uint64_t)c0 << xe.kb) | ((uint64_t)c1 << (xe.kb + xe.cb));
+                    continue;
+                }
+                while (c0 | c1) {   // a count past the piece width: several pieces of one row
+                    const uint32_t q0 = min(c0, xe.cmax), q1 = min(c1, xe.cmax);
+                    slab[at++] = h | ((uint64_t)q0 << xe.kb) | ((uint64_t)q1 << (xe.kb + xe.cb));
+                    c0 -= q0;
+                    c1 -= q1;
+                }
+            }
+        }
         __syncthreads();
     }
+    if (xep && (uint32_t)tid < (1u << xep->x)) xep->dir[((uint64_t)b << xep->x) + tid] = s_xtot[tid];
     if (tid == 0) atomicMax(&gstat[1], (unsigned long long)s_ranges);
 }
 
@@ -1952,13 +2012,48 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
         s.buckets = kp.nb;
     }
     const uint32_t nbc = kp.nb;   // count buckets
+    // exchange emission (kc_count_s XbEmit): a communicator is attached and this is the exchange's
+    // local count (min 1) of packable rows; sub-bins x = ceil(log2 P) + 2 bits below the count bucket
+    // (about 1024 pieces per owner bucket at C2-sized shards), at least the owners' EB0 bits in all
+    XbEmit xe{};
+    const XbEmit* d_xe = nullptr;   // the emission parameters in device memory (kernel SGPRs are full)
+    s.xb_on = false;
+    if (c->comm && min_per_file == 1 && packed && e32 && !std::getenv("HGA_XB_GENERIC")) {
+        const uint32_t P = (uint32_t)c->comm->nranks;
+        const int cbits = F <= 8 ? std::min<int>(32, (64 - (int)nbits) / (int)F) : 0;
+        const uint32_t eb0 = std::min<uint32_t>(10, nbits);
+        uint32_t x = 2;
+        while ((1u << (x - 2)) < P) ++x;
+        if (kp.fb + x < eb0) x = eb0 - kp.fb;
+        if (cbits >= 4 && (1u << x) <= XE_MAXSUB && x <= kp.rbits) {
+            const uint64_t slab_n = fb3 ? (total_bytes + total_bytes / 4 + (uint64_t)nbc * SLACK_3 + 64) : total_bytes;
+            xe.slab = static_cast<uint64_t*>(s.xslab.ensure(std::max<uint64_t>(slab_n, 1) * 8));
+            xe.dir = static_cast<uint64_t*>(s.xdir.ensure(((uint64_t)nbc << x) * 8 + 64));
+            xe.x = x;
+            xe.cb = (uint32_t)cbits;
+            xe.kb = nbits;
+            xe.cmax = (uint32_t)((1ull << cbits) - 1);
+            s.xb_on = true;
+            s.xb_P = P;
+            s.xb_x = x;
+            s.xb_R = (int)(kp.fb + x);
+            s.xb_nbc = nbc;
+            s.xb_fs = fs;
+            XbEmit* d = static_cast<XbEmit*>(s.xemit.ensure(sizeof(XbEmit)));
+            if (std::memcmp(&s.xemit_host, &xe, sizeof(XbEmit)) != 0) {   // uploaded when it changes
+                HGA_HIP(hipMemcpy(d, &xe, sizeof(XbEmit), hipMemcpyHostToDevice));
+                std::memcpy(&s.xemit_host, &xe, sizeof(XbEmit));
+            }
+            d_xe = d;
+        }
+    }
     // C: per-bucket count
     if (packed && e32) {
         uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nbc * 4));
         c->launch("kc_count", [&] {
             hipLaunchKernelGGL(kc_count_s, dim3(nbc), dim3(NT_P), 0, c->stream,
                                static_cast<const uint32_t*>(binned), fs, F, min_per_file, kp, s.rows_key.as<uint64_t>(),
-                               s.rows_cnt.as<uint32_t>(), cap, gstat, blist);
+                               s.rows_cnt.as<uint32_t>(), cap, gstat, blist, d_xe);
             // buckets with a per-file run >= 65536 (listed in blist, count in gstat[5])
             hipLaunchKernelGGL(kc_count<uint32_t>, dim3(std::min<uint32_t>(nbc, (uint32_t)c->num_cu)), dim3(NT_C), 0,
                                c->stream, static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
@@ -1987,6 +2082,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     s.pending = true;
     bool dumps = false;
     for (auto& v : s.dump_keys) dumps = dumps || !v.empty();
+    if (dumps) s.xb_on = false;   // the pieces would miss the cached rows
     if (dumps) count_settle(c);   // the cached rows are merged on the host side now
 }
 
@@ -2009,6 +2105,7 @@ void count_settle(hga_ctx* c, const unsigned long long* h) {
     s.rows = h[0];
     s.max_split = (uint32_t)h[1];
     s.instances = h[4];
+    s.listed = h[5];
     merge_dump_rows(c);
 }
 

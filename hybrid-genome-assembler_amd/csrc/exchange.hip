@@ -191,6 +191,7 @@ void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint6
     s.rows_cnt.ensure(cap * 4 * F);
     s.rows = 0;
     s.rows_cap = cap;
+    s.xb_on = false;
     if (n) {
         HGA_REQUIRE(keys && counts, HGA_ERR_INVALID, "input buffers required");
         char* w = static_cast<char*>(s.xch2.ensure(n * 8 + n * 4 + (n + 1) * 8 + 64));
@@ -400,7 +401,6 @@ constexpr uint64_t MB_TILE = (uint64_t)MB_NT * MB_R;
 constexpr int MB_MAXB = 14;                    // <= 16384 buckets
 constexpr int MG_NT = 512;
 constexpr int MG_R = 8;                        // pieces per thread in flight
-constexpr uint64_t MG_EMPTY = ~0ull;           // keys are < 2^60 on this path
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {   // MurmurHash3's 64-bit finaliser
     k ^= k >> 33;
@@ -506,22 +506,26 @@ __global__ void __launch_bounds__(MB_NT) kx_mb_scatter(const uint64_t* __restric
 // wcnt (rows <= pieces), kept[b] = its rows.  No device-wide cursor: same-address device atomics
 // serialise, one per workgroup would bound the kernel.  gstat[1] |= 1 when a table filled (the
 // host reruns with pmul doubled).  `ld(i)` returns the bucket's i-th piece, i < m; `a` is the
-// bucket's first slot in wkey / wcnt.  HASHED: the pieces carry the counting mix of the key (the
-// hash-bucket exchange), whose low bits are the slot; the rows get the key back (mix_inv).
-template <int T, int FMAX>
+// bucket's first slot in wkey / wcnt.  HASHED: the pieces carry the counting mix h of the key (the
+// hash-bucket exchange), whose low bits are the slot; the table holds h & kmask (KT = u32 when the
+// bucket's own bits leave <= 31 others: hbase holds the rest) and the rows get the key back
+// (mix_inv(hbase | key)).
+template <int T, int FMAX, class KT = unsigned long long>
 struct MergeLds {
-    unsigned long long tkey[T];
+    KT tkey[T];
     uint32_t tcnt[FMAX * T];
     uint32_t tsat[(FMAX * T + 31) / 32];   // bit f * T + slot: that sum passed 2^32 - 1
     uint32_t ws[MG_NT / 64 + 1];
     uint32_t s_ovf;
 };
-template <int T, int FMAX, bool HASHED, class Load>
-__device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX>& L, const Load& ld, uint64_t m, uint64_t a, uint32_t b,
-                                             const PackFmt& pf, const Mix& mx, uint64_t kmask, uint32_t min_c, uint32_t pmul,
+template <int T, int FMAX, bool HASHED, class KT, class Load>
+__device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX, KT>& L, const Load& ld, uint64_t m, uint64_t a, uint32_t b,
+                                             const PackFmt& pf, const Mix& mx, uint64_t kmask, uint64_t hbase,
+                                             uint32_t min_c, uint32_t pmul,
                                              uint64_t* __restrict__ wkey, uint32_t* __restrict__ wcnt, uint64_t n,
                                              uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
     static_assert(T % MG_NT == 0 && T / MG_NT <= 32, "each thread owns T / MG_NT <= 32 slots");
+    constexpr KT EMPTY = (KT)~(KT)0;
     const int tid = threadIdx.x;
     uint64_t rb = 0;   // rows written so far (uniform)
     const uint32_t F = pf.F;
@@ -530,7 +534,7 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX>& L, const Load& l
     P = P < 256u ? P : 256u;
     if (tid == 0) L.s_ovf = 0;
     for (uint32_t p = 0; p < P; ++p) {
-        for (uint32_t j = tid; j < T; j += MG_NT) L.tkey[j] = MG_EMPTY;
+        for (uint32_t j = tid; j < T; j += MG_NT) L.tkey[j] = EMPTY;
         for (uint32_t j = tid; j < F * T; j += MG_NT) L.tcnt[j] = 0;
         for (uint32_t j = tid; j < (FMAX * T + 31) / 32; j += MG_NT) L.tsat[j] = 0;
         __syncthreads();
@@ -544,13 +548,13 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX>& L, const Load& l
 #pragma unroll
             for (int q = 0; q < MG_R; ++q) {
                 if (i0 + (uint64_t)q * MG_NT + tid >= m) continue;
-                const uint64_t key = v[q] & kmask;
+                const KT key = (KT)(v[q] & kmask);
                 if (P > 1 && (((uint32_t)(fmix64(key) >> 56) * P) >> 8) != p) continue;   // this pass's share
-                uint32_t slot = (uint32_t)(HASHED ? key : fmix64(key)) & (T - 1);
+                uint32_t slot = (uint32_t)(HASHED ? (uint64_t)key : fmix64(key)) & (T - 1);
                 uint32_t t = 0;
                 for (; t < T; ++t) {
-                    const unsigned long long old = atomicCAS(&L.tkey[slot], MG_EMPTY, (unsigned long long)key);
-                    if (old == MG_EMPTY || old == key) break;
+                    const KT old = atomicCAS(&L.tkey[slot], EMPTY, key);
+                    if (old == EMPTY || old == key) break;
                     slot = (slot + 1) & (T - 1);
                 }
                 if (t == T) {
@@ -587,12 +591,12 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX>& L, const Load& l
                 L.tcnt[f * T + s] = c;
                 any |= c != 0u;
             }
-            if (L.tkey[s] != MG_EMPTY && any) keep |= 1u << j;
+            if (L.tkey[s] != EMPTY && any) keep |= 1u << j;
         }
         uint32_t tot;
         const uint32_t ex = block_excl_scan<MG_NT>((uint32_t)__popc(keep), L.ws, &tot);
         // compaction in place: every source is read into registers before the barrier
-        unsigned long long kk[ES];
+        KT kk[ES];
         uint32_t cc[ES * FMAX];
 #pragma unroll
         for (int j = 0; j < ES; ++j) {
@@ -613,7 +617,7 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX>& L, const Load& l
             }
         __syncthreads();
         for (uint32_t j = tid; j < tot; j += MG_NT) {
-            wkey[a + rb + j] = HASHED ? mix_inv(L.tkey[j], mx) : (uint64_t)L.tkey[j];
+            wkey[a + rb + j] = HASHED ? mix_inv(hbase | (uint64_t)L.tkey[j], mx) : (uint64_t)L.tkey[j];
             for (uint32_t f = 0; f < F; ++f) wcnt[(uint64_t)f * n + a + rb + j] = L.tcnt[f * T + j];
         }
         rb += tot;
@@ -632,8 +636,8 @@ __global__ void __launch_bounds__(MG_NT) kx_mb_merge(const uint64_t* __restrict_
     (void)mb;
     const uint32_t b = blockIdx.x;
     const uint64_t a = bstart[b], e = bstart[b + 1];
-    merge_bucket<T, FMAX, false>(L, [&](uint64_t i) { return sk[a + i]; }, e - a, a, b, pf, Mix{}, kmask, min_c, pmul,
-                                 wkey, wcnt, n, kept, gstat);
+    merge_bucket<T, FMAX, false>(L, [&](uint64_t i) { return sk[a + i]; }, e - a, a, b, pf, Mix{}, kmask, 0ull, min_c,
+                                 pmul, wkey, wcnt, n, kept, gstat);
 }
 
 // Rows of bucket b from its piece range to the scanned row offset off[b] (one workgroup per bucket).
@@ -773,6 +777,17 @@ __global__ void __launch_bounds__(XB_NT) kx_xb_scatter(const uint64_t* __restric
     }
 }
 
+// Pieces of the count kernel's exchange emission (count.hip XbEmit) from each count bucket's slab
+// range to its place in the send buffer (S = scanned per-(bucket, sub-bin) counts, 2^x per bucket).
+__global__ void __launch_bounds__(256) kx_xb_gather(const uint64_t* __restrict__ slab, const uint64_t* __restrict__ fs,
+                                                    uint32_t F, uint32_t x, const uint64_t* __restrict__ S,
+                                                    uint64_t* __restrict__ out) {
+    const uint64_t b = blockIdx.x;
+    const uint64_t a = S[b << x], m = S[(b + 1) << x] - a;
+    const uint64_t* __restrict__ src = slab + fs[b * (F + 1)];
+    for (uint64_t j = threadIdx.x; j < m; j += 256) out[a + j] = src[j];
+}
+
 // Per-owner piece totals from the scanned bucket starts S (2^R + 1 entries).
 __global__ void kx_xb_owner_tot(const uint64_t* __restrict__ S, uint32_t P, int eb0, int R, uint64_t* __restrict__ per) {
     const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
@@ -802,16 +817,19 @@ __global__ void kx_xb_units(const uint64_t* __restrict__ S, const XbSrc* __restr
     ut[u] = t;   // ut[units] = 0: the scan's total
 }
 
-template <int T, int FMAX>
+// KT u32: the table keeps the low `lowbits` (<= 31) bits of h, the unit index the rest; MAXP: senders
+// whose runs fit the LDS run table.
+template <int T, int FMAX, class KT, uint32_t MAXP>
 __global__ void __launch_bounds__(MG_NT) kx_xb_merge(const uint64_t* __restrict__ in, const uint64_t* __restrict__ S,
                                                      const XbSrc* __restrict__ src, uint32_t P,
                                                      const uint64_t* __restrict__ ubase, PackFmt pf, Mix mx, uint64_t kmask,
+                                                     uint64_t u_first, uint32_t lowbits,
                                                      uint32_t min_c, uint32_t pmul, uint64_t* __restrict__ wkey,
                                                      uint32_t* __restrict__ wcnt, uint64_t n,
                                                      uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
-    __shared__ MergeLds<T, FMAX> L;
-    __shared__ uint64_t rst[XB_MAXP];        // sender p's run start in `in`
-    __shared__ uint32_t rpre[XB_MAXP + 1];   // run lengths, exclusive prefix (a bucket holds < 2^32 pieces)
+    __shared__ MergeLds<T, FMAX, KT> L;
+    __shared__ uint64_t rst[MAXP];        // sender p's run start in `in`
+    __shared__ uint32_t rpre[MAXP + 1];   // run lengths, exclusive prefix (a bucket holds < 2^32 pieces)
     const uint32_t u = blockIdx.x;
     const int tid = threadIdx.x;
     for (uint32_t p = tid; p < P; p += MG_NT) {
@@ -842,7 +860,9 @@ __global__ void __launch_bounds__(MG_NT) kx_xb_merge(const uint64_t* __restrict_
         }
         return in[rst[lo] + (i - rpre[lo])];
     };
-    merge_bucket<T, FMAX, true>(L, ld, m, ubase[u], u, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
+    const uint64_t hbase = sizeof(KT) == 4 ? (u_first + u) << lowbits : 0ull;
+    merge_bucket<T, FMAX, true>(L, ld, m, ubase[u], u, pf, mx, sizeof(KT) == 4 ? (1ull << lowbits) - 1 : kmask, hbase,
+                                min_c, pmul, wkey, wcnt, n, kept, gstat);
 }
 
 }  // namespace
@@ -926,6 +946,7 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
     s.rows_cnt.ensure(cap * 4 * F);
     s.rows = 0;
     s.rows_cap = cap;
+    s.xb_on = false;
     if (n) {
         HGA_REQUIRE(pieces, HGA_ERR_INVALID, "input buffer required");
         // table slots per bucket (u64 key + F u32 counts): 32 KB for F <= 2, so four workgroups share a CU
@@ -1012,6 +1033,32 @@ int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner) {
     const int eb0 = std::min(10, 2 * s.k);
     const int rmax = std::min(2 * s.k, XB_MAXR);
     const uint64_t rows = s.rows;
+    if (s.xb_on && s.xb_P == P && !s.listed) {   // the count kernel already grouped the pieces
+        const int R = s.xb_R;
+        const uint64_t nb = 1ull << R;
+        char* w = static_cast<char*>(s.xch.ensure((nb + 1) * 8 + 8 * (uint64_t)P + 64));
+        uint64_t* S = reinterpret_cast<uint64_t*>(w);
+        uint64_t* per_d = S + nb + 1;
+        HGA_HIP(hipMemcpyAsync(S, s.xdir.p, nb * 8, hipMemcpyDeviceToDevice, c->stream));
+        HGA_HIP(hipMemsetAsync(S + nb, 0, 8, c->stream));
+        exclusive_scan_u64(c, S, nb + 1, s.scratch);
+        c->launch("kx_xb_pack", [&] {
+            hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream, S, P, eb0, R, per_d);
+        });
+        c->check_launch("kx_xb_owner_tot");
+        HGA_HIP(hipMemcpyAsync(per_owner, per_d, 8 * (uint64_t)P, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        uint64_t total = 0;
+        for (uint32_t o = 0; o < P; ++o) total += per_owner[o];
+        HGA_REQUIRE(total < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per rank");
+        uint64_t* out = static_cast<uint64_t*>(s.xsend.ensure(std::max<uint64_t>(total, 1) * 8 + 64));
+        c->launch("kx_xb_gather", [&] {
+            hipLaunchKernelGGL(kx_xb_gather, dim3(s.xb_nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(), s.xb_fs,
+                               s.n_files, s.xb_x, S, out);
+        });
+        c->check_launch("kx_xb_gather");
+        return R;
+    }
     int R = eb0;
     while (R < rmax && ((uint64_t)1024 << R) < rows * P) ++R;
     if (const char* e = std::getenv("HGA_XB_R")) R = std::max(eb0, std::min(rmax, std::atoi(e)));   // test hook
@@ -1080,11 +1127,15 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, cons
     }
     HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per merge");
     const uint64_t units = first(me + 1, rmin) - first(me, rmin);
+    const uint64_t u_first = first(me, rmin);
+    const uint32_t lowbits = 2u * (uint32_t)s.k - (uint32_t)rmin;
+    const bool small = lowbits <= 31 && !std::getenv("HGA_XB_WIDE");   // u32 table keys (HGA_XB_WIDE: test hook)
     const uint64_t cap = (std::max<uint64_t>(n, 1) + 3) & ~3ull;   // x4: 16-B row groups (kc_spec_hist)
     s.rows_key.ensure(cap * 8);
     s.rows_cnt.ensure(cap * 4 * F);
     s.rows = 0;
     s.rows_cap = cap;
+    s.xb_on = false;
     // S (nd + 1) | ut = unit starts (units + 1) | kept (units + 1) | gstat 2 | wkey n | wcnt F n
     char* w = static_cast<char*>(s.xch2.ensure((nd + 1 + 2 * (units + 1) + 2 + n) * 8 + 4ull * F * n + 64));
     uint64_t* S = reinterpret_cast<uint64_t*>(w);
@@ -1111,15 +1162,16 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, cons
             HGA_REQUIRE(pmul <= 256, HGA_ERR_OOM, "owner merge: a bucket does not fit its LDS table");
             HGA_HIP(hipMemsetAsync(gstat, 0, 16, c->stream));
             c->launch("kx_xb_merge", [&] {
-                if (F <= 2)
-                    hipLaunchKernelGGL((kx_xb_merge<2048, 2>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P,
-                                       ut, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
-                else if (F <= 4)
-                    hipLaunchKernelGGL((kx_xb_merge<1024, 4>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P,
-                                       ut, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
-                else
-                    hipLaunchKernelGGL((kx_xb_merge<1024, 8>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P,
-                                       ut, pf, mx, kmask, min_c, pmul, wkey, wcnt, n, kept, gstat);
+#define HGA_XBM(TT, FM, KT, MP)                                                                             \
+    hipLaunchKernelGGL((kx_xb_merge<TT, FM, KT, MP>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P, ut, pf, mx, \
+                       kmask, u_first, lowbits, min_c, pmul, wkey, wcnt, n, kept, gstat)
+                if (F <= 2 && small && P <= 64) HGA_XBM(2048, 2, uint32_t, 64);
+                else if (F <= 2 && small) HGA_XBM(2048, 2, uint32_t, XB_MAXP);
+                else if (F <= 2 && P <= 64) HGA_XBM(2048, 2, unsigned long long, 64);
+                else if (F <= 2) HGA_XBM(2048, 2, unsigned long long, XB_MAXP);
+                else if (F <= 4) HGA_XBM(1024, 4, unsigned long long, XB_MAXP);
+                else HGA_XBM(1024, 8, unsigned long long, XB_MAXP);
+#undef HGA_XBM
             });
             c->check_launch("kx_xb_merge");
             HGA_HIP(hipMemsetAsync(kept + units, 0, 8, c->stream));

@@ -136,7 +136,8 @@ struct CountState {
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
         sel_keys, sel_tmp, sel_wtmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, blist,
-        binned3, file_start3, xsend, xrecv, xdir, xsrc;
+        binned3, file_start3, xsend, xrecv, xdir, xsrc, xslab, xemit;
+    char xemit_host[32] = {};   // the XbEmit last uploaded to xemit (count.hip)
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t sel_grid = 0;   // kc_select workgroups: as many as are resident at once (count.hip)
@@ -147,6 +148,13 @@ struct CountState {
     std::vector<std::vector<uint64_t>> dump_keys;
     std::vector<std::vector<uint32_t>> dump_cnt;
     uint32_t buckets = 0, fb = 0, max_split = 1;
+    uint64_t listed = 0;   // buckets kc_count_s left to the generic kernel (per-file run >= 65536)
+    // exchange emission of the last count_run (kc_count_s XbEmit): pieces in xslab by count bucket,
+    // counts per (bucket, sub-bin) in xdir at resolution xb_R = fb + xb_x, for xb_P ranks
+    bool xb_on = false;
+    uint32_t xb_P = 0, xb_x = 0, xb_nbc = 0;
+    int xb_R = 0;
+    const uint64_t* xb_fs = nullptr;
     bool pending = false;   // count_run's counters not read back yet (count_settle)
     bool dist = false;      // rows are this rank's owner range after hga_count_exchange
     ~CountState() {

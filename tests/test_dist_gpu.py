@@ -93,11 +93,11 @@ def test_partition_merge_min_counts_and_empty_owner():
     assert np.array_equal(keys, rk) and np.array_equal(counts, rc)
 
 
-def _worker(rank, world, port, out_path, k, xb_r=None, big=False):
+def _worker(rank, world, port, out_path, k, envs=None, big=False):
     import os
     import torch.distributed as dist
-    if xb_r:   # this rank's bucket resolution (exchange.hip count_xb_pack test hook)
-        os.environ["HGA_XB_R"] = str(xb_r[rank])
+    if envs:   # this rank's exchange test hooks (count.hip / exchange.hip)
+        os.environ.update(envs[rank])
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     ctx = hga.Ctx(0)
     try:
@@ -121,14 +121,25 @@ def _worker(rank, world, port, out_path, k, xb_r=None, big=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k,xb_r,big,one_pass", [
-    (2, 13, None, False, False), (3, 27, None, False, False),
-    (2, 13, (10, 12), False, False), (3, 19, (12, 10, 11), False, False),   # senders at different resolutions
-    (1, 19, (10,), True, False), (1, 19, (10,), True, True)])               # multi-pass / overflowing buckets
-def test_count_exchange_processes(tmp_path, monkeypatch, world, k, xb_r, big, one_pass):
-    """The hash-bucket exchange (exchange.hip kx_xb_*): owners merge every sender's runs of their
-    buckets at the coarsest resolution any sender used; `big` puts about 2 K pieces in each of the
-    1024 buckets of one rank (2.1 M rows), so the owner merge takes two passes per bucket (and with
+GEN = {"HGA_XB_GENERIC": "1"}           # sender bins its rows itself (kx_xb_hist / kx_xb_scatter)
+WIDE = {"HGA_XB_WIDE": "1"}             # owner table with u64 keys
+
+
+def _gen(r):
+    return {"HGA_XB_GENERIC": "1", "HGA_XB_R": str(r)}
+
+
+@pytest.mark.parametrize("world,k,envs,big,one_pass", [
+    (2, 13, None, False, False), (3, 27, None, False, False), (3, 19, (WIDE,) * 3, False, False),
+    (2, 13, (_gen(10), _gen(12)), False, False),                  # senders at different resolutions
+    (3, 19, ({}, _gen(10), _gen(13)), False, False),              # count-kernel emission next to generic senders
+    (2, 19, None, True, False), (2, 19, (GEN, GEN), True, False),
+    (1, 19, (_gen(10),), True, False), (1, 19, (_gen(10),), True, True)])   # multi-pass / overflowing buckets
+def test_count_exchange_processes(tmp_path, monkeypatch, world, k, envs, big, one_pass):
+    """The hash-bucket exchange (exchange.hip kx_xb_*): senders' pieces grouped by the count kernel
+    (count.hip XbEmit) or binned by the sender (GEN), owners merge every sender's runs of their
+    buckets at the coarsest resolution any sender used; `big` (2.1 M rows at min 1) at 1024 owner
+    buckets puts about 2 K pieces in each, so the owner merge takes two passes per bucket (and with
     HGA_MB_ONE_PASS a first attempt in one pass overflows its table and is retried)."""
     import torch.multiprocessing as mp
     if one_pass:
@@ -138,7 +149,7 @@ def test_count_exchange_processes(tmp_path, monkeypatch, world, k, xb_r, big, on
     port = s.getsockname()[1]
     s.close()
     out = str(tmp_path / "d")
-    mp.start_processes(_worker, args=(world, port, out, k, xb_r, big), nprocs=world, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, out, k, envs, big), nprocs=world, start_method="spawn")
     streams = make_streams(seed=3, n_reads=100000, L=1500000) if big else make_streams()
     ref = oracle.count_pipeline(streams, k, 3, 40)
     inst = sum(oracle.count_instances(x, k) for x in streams)

@@ -40,7 +40,8 @@ for it in range(14):
 print({n: round(float(np.median(v[4:])) * 1e3, 3) for n, v in acc.items()},
       "step ms", round(float(np.median(whole[4:])) * 1e3, 3), flush=True)
 # per-kernel device time of the exchange (event-timed launches, 5 steps)
-names = ["kx_xb_hist", "kx_xb_pack", "kx_xb_scatter", "kx_xb_units", "kx_xb_merge", "kx_mb_compact", "scan"]
+names = ["kc_count", "kx_xb_hist", "kx_xb_pack", "kx_xb_scatter", "kx_xb_gather", "kx_xb_units", "kx_xb_merge",
+         "kx_mb_compact", "scan"]
 ctx.profile(True)
 ctx.profile_reset()
 for it in range(5):
