@@ -1326,14 +1326,27 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         }
         if (xep) {   // uniform: the exchange pieces of these rows, by sub-bin, after the earlier ranges'
             const XbEmit xe = *xep;
-            for (uint32_t j = tid; j < tot; j += NT_P) {   // pieces per sub-bin
-                const uint32_t c = tcnt[j];
+            const uint32_t nsub = 1u << xe.x;
+            // wave-aggregated sub-bin adds (few sub-bins: per-lane LDS adds would serialise); a wave
+            // with a row past the piece width adds per lane (its row takes several pieces)
+            auto sub_add = [&](uint32_t* ctr, uint32_t j, bool ret) {
+                const bool live = j < tot;
+                const uint32_t c = live ? tcnt[j] : 0u, r = live ? tkey[j] : 0u;
                 const uint32_t big = F == 1 ? c : max(c & 0xFFFFu, c >> 16);
-                atomicAdd(&s_xe[xe.x ? tkey[j] >> (rbits - xe.x) : 0u], big <= xe.cmax ? 1u : (big + xe.cmax - 1) / xe.cmax);
-            }
+                const uint32_t np = big <= xe.cmax ? 1u : (big + xe.cmax - 1) / xe.cmax;
+                const uint32_t sb = xe.x ? r >> (rbits - xe.x) : 0u;
+                uint32_t at = 0;
+                if (__ballot(live && np > 1)) {
+                    if (live) at = atomicAdd(&ctr[sb], np);
+                } else {
+                    at = wave_key_add<uint32_t>(ctr, sb, live, nsub, (int)xe.x);
+                }
+                (void)ret;
+                return at;
+            };
+            for (uint32_t j0 = 0; j0 < tot; j0 += NT_P) (void)sub_add(s_xe, j0 + tid, false);
             __syncthreads();
             if (tid < 64) {   // sub-bin cursors after the pieces already written for this bucket
-                const uint32_t nsub = 1u << xe.x;
                 const uint32_t v = (uint32_t)tid < nsub ? s_xe[tid] : 0u;
                 const uint32_t inc = wave_incl_scan(v, tid);
                 const uint32_t w0 = s_xw;
@@ -1346,14 +1359,14 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
             }
             __syncthreads();
             uint64_t* __restrict__ slab = xe.slab + f[0];
-            for (uint32_t j = tid; j < tot; j += NT_P) {
+            for (uint32_t j0 = 0; j0 < tot; j0 += NT_P) {
+                const uint32_t j = j0 + tid;
+                uint64_t at = sub_add(s_xpre, j, true);
+                if (j >= tot) continue;
                 const uint32_t c = tcnt[j], r = tkey[j];
                 const uint64_t h = hb | r;
                 uint32_t c0 = F == 1 ? c : c & 0xFFFFu, c1 = F == 1 ? 0u : c >> 16;
-                const uint32_t big = max(c0, c1);
-                const uint32_t np = big <= xe.cmax ? 1u : (big + xe.cmax - 1) / xe.cmax;
-                uint64_t at = atomicAdd(&s_xpre[xe.x ? r >> (rbits - xe.x) : 0u], np);
-                if (np == 1) {
+                if (max(c0, c1) <= xe.cmax) {
                     slab[at] = h | ((uint64_t)c0 << xe.kb) | ((uint64_t)c1 << (xe.kb + xe.cb));
                     continue;
                 }

@@ -252,26 +252,11 @@ __device__ __forceinline__ uint64_t pieces_of(const uint32_t* __restrict__ cnt, 
     return ((uint64_t)big + pf.cmax - 1) / pf.cmax;
 }
 
-// Wave-aggregated owner counters (rows go to random owners, so per-lane adds on n_own <= 64
-// counters would serialise): the owner ids' bit planes are balloted once, lane j builds owner
-// j's lane mask from them and makes that owner's one LDS add, every live lane gets its
-// position (in lane order) from its owner's mask.  nbits = ceil(log2(n_own)) <= 6.
+// Wave-aggregated owner counters (kmer_dev.hpp wave_key_add): rows go to random owners, per-lane
+// adds on n_own <= 64 counters would serialise.
 __device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long* ctr, uint32_t o, bool live,
                                                              uint32_t n_own, int nbits) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t L = __ballot(live);
-    uint64_t m = L, mo = L;
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-        if (b >= nbits) break;
-        const uint64_t B = __ballot(live && ((o >> b) & 1u));
-        m &= ((o >> b) & 1u) ? B : ~B;
-        mo &= ((lane >> b) & 1u) ? B : ~B;
-    }
-    unsigned long long base = 0;
-    if (lane < n_own && mo) base = atomicAdd(&ctr[lane], (unsigned long long)__popcll(mo));
-    base = __shfl(base, (int)(o & 63u), 64);
-    return base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    return wave_key_add<unsigned long long>(ctr, o, live, n_own, nbits);
 }
 __device__ __forceinline__ int owner_bits(uint32_t n_own) {
     int b = 0;
@@ -399,8 +384,14 @@ constexpr int MB_NT = 1024;
 constexpr int MB_R = 16;                       // pieces per thread per tile
 constexpr uint64_t MB_TILE = (uint64_t)MB_NT * MB_R;
 constexpr int MB_MAXB = 14;                    // <= 16384 buckets
-constexpr int MG_NT = 512;
-constexpr int MG_R = 8;                        // pieces per thread in flight
+#ifndef HGA_MG_NT
+#define HGA_MG_NT 256   // 256-thread merge workgroups: 0.208 -> 0.157 ms at C2 (more of them resident)
+#endif
+#ifndef HGA_MG_R
+#define HGA_MG_R 4
+#endif
+constexpr int MG_NT = HGA_MG_NT;
+constexpr int MG_R = HGA_MG_R;                 // pieces per thread in flight
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {   // MurmurHash3's 64-bit finaliser
     k ^= k >> 33;
@@ -578,50 +569,42 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX, KT>& L, const Loa
             }
             return;   // uniform: every thread read s_ovf after the barrier
         }
-        constexpr int ES = T / MG_NT;   // slots j * MG_NT + tid: lanes on consecutive banks
+        // each thread owns ES consecutive slots and writes its kept rows straight to their place
+        // (one block scan; rows stay in slot order, no LDS round trip)
+        constexpr int ES = T / MG_NT;
+        KT kk[ES];
+        uint32_t cc[ES * FMAX];
         uint32_t keep = 0;
 #pragma unroll
         for (int j = 0; j < ES; ++j) {
-            const uint32_t s = j * MG_NT + tid;
+            const uint32_t s = tid * ES + j;
+            kk[j] = L.tkey[s];
             bool any = false;
-            for (uint32_t f = 0; f < F; ++f) {
+#pragma unroll
+            for (int f = 0; f < FMAX; ++f) {
+                if (f >= (int)F) break;
                 uint32_t c = L.tcnt[f * T + s];
                 if ((L.tsat[(f * T + s) >> 5] >> ((f * T + s) & 31)) & 1u) c = 0xFFFFFFFFu;
                 c = c >= min_c ? c : 0u;
-                L.tcnt[f * T + s] = c;
+                cc[j * FMAX + f] = c;
                 any |= c != 0u;
             }
-            if (L.tkey[s] != EMPTY && any) keep |= 1u << j;
+            if (kk[j] != EMPTY && any) keep |= 1u << j;
         }
         uint32_t tot;
         const uint32_t ex = block_excl_scan<MG_NT>((uint32_t)__popc(keep), L.ws, &tot);
-        // compaction in place: every source is read into registers before the barrier
-        KT kk[ES];
-        uint32_t cc[ES * FMAX];
-#pragma unroll
-        for (int j = 0; j < ES; ++j) {
-            kk[j] = L.tkey[j * MG_NT + tid];
-#pragma unroll
-            for (int f = 0; f < FMAX; ++f) cc[j * FMAX + f] = f < (int)F ? L.tcnt[f * T + j * MG_NT + tid] : 0u;
-        }
-        __syncthreads();
-        uint32_t o = ex;
+        uint64_t o = a + rb + ex;
 #pragma unroll
         for (int j = 0; j < ES; ++j)
             if ((keep >> j) & 1u) {
-                L.tkey[o] = kk[j];
+                wkey[o] = HASHED ? mix_inv(hbase | (uint64_t)kk[j], mx) : (uint64_t)kk[j];
 #pragma unroll
                 for (int f = 0; f < FMAX; ++f)
-                    if (f < (int)F) L.tcnt[f * T + o] = cc[j * FMAX + f];
+                    if (f < (int)F) wcnt[(uint64_t)f * n + o] = cc[j * FMAX + f];
                 ++o;
             }
-        __syncthreads();
-        for (uint32_t j = tid; j < tot; j += MG_NT) {
-            wkey[a + rb + j] = HASHED ? mix_inv(hbase | (uint64_t)L.tkey[j], mx) : (uint64_t)L.tkey[j];
-            for (uint32_t f = 0; f < F; ++f) wcnt[(uint64_t)f * n + a + rb + j] = L.tcnt[f * T + j];
-        }
         rb += tot;
-        __syncthreads();
+        __syncthreads();   // the next pass clears the table
     }
     if (tid == 0) kept[b] = rb;
 }
@@ -804,17 +787,18 @@ struct XbSrc {
     uint64_t off;
     uint32_t d, pad;
 };
+// ut[u] = the pieces of this owner's buckets before u, over all senders (no scan: each sender's
+// share is a difference of S).
 __global__ void kx_xb_units(const uint64_t* __restrict__ S, const XbSrc* __restrict__ src, uint32_t P, uint64_t units,
                             uint64_t* __restrict__ ut) {
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u > units) return;
     uint64_t t = 0;
-    if (u < units)
-        for (uint32_t p = 0; p < P; ++p) {
-            const XbSrc s = src[p];
-            t += S[s.off + ((u + 1) << s.d)] - S[s.off + (u << s.d)];
-        }
-    ut[u] = t;   // ut[units] = 0: the scan's total
+    for (uint32_t p = 0; p < P; ++p) {
+        const XbSrc s = src[p];
+        t += S[s.off + (u << s.d)] - S[s.off];
+    }
+    ut[u] = t;
 }
 
 // KT u32: the table keeps the low `lowbits` (<= 31) bits of h, the unit index the rest; MAXP: senders
@@ -1154,7 +1138,6 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, cons
                            ut);
     });
     c->check_launch("kx_xb_units");
-    exclusive_scan_u64(c, ut, units + 1, s.scratch);
     unsigned long long* hs = static_cast<unsigned long long*>(c->pinned.ensure(16));
     if (n) {
         // one host round trip per attempt: the overflow flag and the row total come back together

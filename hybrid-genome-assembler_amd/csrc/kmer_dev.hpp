@@ -292,6 +292,28 @@ __device__ __forceinline__ uint32_t wave_excl_scan_small(uint32_t v, uint32_t* t
     return ex;
 }
 
+// Wave-aggregated counter add for keys with few distinct values (o < n_own <= 64, nbits =
+// ceil(log2 n_own) <= 6): the key's bit planes are balloted once, lane j builds key j's lane mask
+// and makes that key's one LDS add, every live lane gets its position (in lane order) from its
+// key's mask.  Per-lane adds on so few counters would serialise on the same LDS addresses.
+template <class C>
+__device__ __forceinline__ C wave_key_add(C* ctr, uint32_t o, bool live, uint32_t n_own, int nbits) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t L = __ballot(live);
+    uint64_t m = L, mo = L;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        if (b >= nbits) break;
+        const uint64_t B = __ballot(live && ((o >> b) & 1u));
+        m &= ((o >> b) & 1u) ? B : ~B;
+        mo &= ((lane >> b) & 1u) ? B : ~B;
+    }
+    C base = 0;
+    if (lane < n_own && mo) base = atomicAdd(&ctr[lane], (C)__popcll(mo));
+    base = __shfl(base, (int)(o & 63u), 64);
+    return base + (C)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Block-wide exclusive scan of one value per thread; NT threads (multiple of 64,
 // <= 1024).  `ws` is LDS scratch of >= NT/64 + 1 words.  Returns the exclusive
 // prefix; *total receives the block sum.  Contains __syncthreads().
