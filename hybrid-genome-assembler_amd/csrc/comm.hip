@@ -98,15 +98,19 @@ void comm_allgather(hga_ctx* c, const void* mine, uint64_t bytes, void* all) {
         m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
         return;
     }
+    // staged through pinned host memory both ways (true asynchronous copies, no pageable staging)
     char* ds = static_cast<char*>(m.stage.ensure(bytes * (P + 1) + 16));
-    HGA_HIP(hipMemcpyAsync(ds, mine, bytes, hipMemcpyHostToDevice, c->stream));
+    char* hs = static_cast<char*>(m.hstage.ensure(bytes * (P + 1) + 16));
+    std::memcpy(hs, mine, bytes);
+    HGA_HIP(hipMemcpyAsync(ds, hs, bytes, hipMemcpyHostToDevice, c->stream));
     for (int p = 0; p < P; ++p) {
         sp[p] = ds;
         rp[p] = ds + bytes * (p + 1);
     }
     m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
-    HGA_HIP(hipMemcpyAsync(all, ds + bytes, bytes * P, hipMemcpyDeviceToHost, c->stream));
+    HGA_HIP(hipMemcpyAsync(hs + bytes, ds + bytes, bytes * P, hipMemcpyDeviceToHost, c->stream));
     c->sync();
+    std::memcpy(all, hs + bytes, bytes * P);
 }
 
 // Variable-size all-gather of host bytes, in rank order.
@@ -148,37 +152,50 @@ std::vector<std::vector<char>> comm_allgatherv(hga_ctx* c, const void* mine, uin
     return out;
 }
 
-// All-to-all-v of DEVICE buffers whose per-peer slices are contiguous in rank order.
-void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) {
+// All-to-all-v of DEVICE buffers whose per-peer slices are contiguous in rank order; keep_self
+// false: the rank's own slice is not moved (rb[rank] must be 0).
+void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb_in, void* recv, const uint64_t* rb,
+                        bool keep_self) {
     Comm& m = need_comm(c);
     const int P = m.nranks;
     std::vector<const void*> sp(P);
     std::vector<void*> rp(P);
+    std::vector<uint64_t> sbv(sb_in, sb_in + P);
     uint64_t so = 0, ro = 0, st = 0, rt = 0;
+    for (int p = 0; p < P; ++p) {
+        sp[p] = static_cast<const char*>(send) + so;
+        so += sbv[p];
+    }
+    if (!keep_self) {
+        HGA_REQUIRE(rb[m.rank] == 0, HGA_ERR_COMM, "alltoallv: own slice kept in place but received");
+        sbv[m.rank] = 0;
+    }
+    const uint64_t* sb = sbv.data();
     for (int p = 0; p < P; ++p) {
         st += sb[p];
         rt += rb[p];
     }
     if (m.on_device()) {
         for (int p = 0; p < P; ++p) {
-            sp[p] = static_cast<const char*>(send) + so;
             rp[p] = static_cast<char*>(recv) + ro;
-            so += sb[p];
             ro += rb[p];
         }
         m.alltoallv(c, sp.data(), sb, rp.data(), rb);
         return;
     }
-    // host-staged: device -> host, the caller's transport, host -> device
-    std::vector<char> hs(st), hr(rt);
-    if (st) HGA_HIP(hipMemcpyAsync(hs.data(), send, st, hipMemcpyDeviceToHost, c->stream));
+    // host-staged: device -> host, the caller's transport, host -> device (the send buffer whole:
+    // a kept-in-place own slice sits between the others)
+    std::vector<char> hs(so), hr(rt);
+    if (so) HGA_HIP(hipMemcpyAsync(hs.data(), send, so, hipMemcpyDeviceToHost, c->stream));
     c->sync();
+    so = 0;
     for (int p = 0; p < P; ++p) {
         sp[p] = hs.data() + so;
         rp[p] = hr.data() + ro;
-        so += sb[p];
+        so += sb_in[p];
         ro += rb[p];
     }
+    (void)st;
     m.alltoallv(c, sp.data(), sb, rp.data(), rb);
     if (rt) HGA_HIP(hipMemcpyAsync(recv, hr.data(), rt, hipMemcpyHostToDevice, c->stream));
     c->sync();
@@ -199,8 +216,8 @@ struct CtxXport : proto::Xport {
     std::vector<std::vector<char>> allgatherv(const void* mine, uint64_t bytes) override {
         return comm_allgatherv(c, mine, bytes);
     }
-    void alltoallv_eng(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
-        comm_alltoallv_dev(c, send, sb, recv, rb);
+    void alltoallv_eng(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb, bool keep_self) override {
+        comm_alltoallv_dev(c, send, sb, recv, rb, keep_self);
     }
 };
 
@@ -216,9 +233,9 @@ struct DevEngine {
     int xb_pack(uint32_t P, uint64_t* per) { return count_xb_pack(c, P, per); }
     const void* xb_pieces() const { return c->count.xsend.p; }
     const void* xb_dir() const { return c->count.xdir.p; }
-    void xb_merge(const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from, uint32_t P,
-                  uint32_t me, uint32_t min) {
-        count_xb_merge(c, in, n_from, dir_in, r_from, P, me, min);
+    void xb_merge(const uint64_t* in, const uint64_t* self, const uint64_t* n_from, const uint64_t* dir_in,
+                  const int* r_from, uint32_t P, uint32_t me, uint32_t min) {
+        count_xb_merge(c, in, self, n_from, dir_in, r_from, P, me, min);
     }
     void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per) {
         count_partition(c, spl, P, keys, counts, per);

@@ -1089,13 +1089,16 @@ __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t
 // (pieces <= instances), grouped by the next x bits of h in ascending order (sub-ranges of a split
 // bucket are emitted in ascending order too), and each (bucket, sub-bin)'s piece count into
 // dir[(b << x) + sub].  The owner side then needs no hashing and the sender no binning pass.
+// The dense rows are not written then: each bucket reserves its row range once (rbase[b]) and
+// kc_xb_dense fills it from the pieces if a local query needs the rows (count_dense).
 struct XbEmit {
     uint64_t* slab;   // nullptr: off
     uint64_t* dir;
+    uint64_t* rbase;
     uint32_t x, cb, kb, cmax;
 };
 constexpr uint32_t XE_MAXSUB = 64;
-static_assert(sizeof(XbEmit) <= 32, "CountState::xemit_host holds one XbEmit");
+static_assert(sizeof(XbEmit) <= 64, "CountState::xemit_host holds one XbEmit");
 
 __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t* __restrict__ binned,
                                                       const uint64_t* __restrict__ fs, uint32_t F,
@@ -1110,7 +1113,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
     __shared__ uint32_t stk_lo[40], stk_hi[40];
     __shared__ uint32_t ws[NT_P / 64 + 1];
     __shared__ unsigned long long s_base;
-    __shared__ uint32_t s_xe[XE_MAXSUB], s_xpre[XE_MAXSUB], s_xtot[XE_MAXSUB], s_xw;   // exchange emission
+    __shared__ uint32_t s_xe[XE_MAXSUB], s_xpre[XE_MAXSUB], s_xtot[XE_MAXSUB], s_xw, s_xrows;   // exchange emission
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     uint32_t* myq = qbuf[tid >> 6];
@@ -1119,6 +1122,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
     for (uint32_t ff = 0; ff < F; ++ff)
         if (f[ff + 1] - f[ff] >= 65536u && F > 1) {   // a count could pass 16 bits: kc_count takes it
             if (tid == 0) blist[atomicAdd(&gstat[5], 1ull)] = b;
+            if (xep && (uint32_t)tid < (1u << xep->x)) xep->dir[((uint64_t)b << xep->x) + tid] = 0;   // no pieces here
             return;
         }
     const uint32_t rbits = kp.rbits;
@@ -1131,6 +1135,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         s_sp = 1;
         s_ranges = 0;
         s_xw = 0;
+        s_xrows = 0;
     }
     if (tid < (int)XE_MAXSUB) s_xe[tid] = s_xtot[tid] = 0;
     __syncthreads();
@@ -1295,7 +1300,8 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         uint32_t tot;
         const uint32_t ex = block_excl_scan<NT_P>((uint32_t)__popc(keep), ws, &tot);
         if (tid == 0) {
-            s_base = tot ? atomicAdd(&gstat[0], (unsigned long long)tot) : 0ull;
+            s_base = tot && !xep ? atomicAdd(&gstat[0], (unsigned long long)tot) : 0ull;   // emission: once, at the end
+            s_xrows += tot;
             ++s_ranges;
         }
         __syncthreads();   // every slot read: the table becomes the staging area
@@ -1310,7 +1316,8 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         __syncthreads();
         const uint64_t base = s_base;
         const uint64_t hb = kp.fb ? ((uint64_t)b << rbits) : 0ull;
-        if (base + tot > cap) {
+        if (xep) {   // no dense rows: kc_xb_dense writes them from the pieces if a local query needs them
+        } else if (base + tot > cap) {
             if (tid == 0 && tot) atomicOr(&gstat[2], 2ull);
         } else {
             for (uint32_t j = tid; j < tot; j += NT_P) {
@@ -1381,7 +1388,48 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         __syncthreads();
     }
     if (xep && (uint32_t)tid < (1u << xep->x)) xep->dir[((uint64_t)b << xep->x) + tid] = s_xtot[tid];
+    if (xep && tid == 0) {   // the bucket's dense row range, reserved once
+        const uint64_t base = s_xrows ? atomicAdd(&gstat[0], (unsigned long long)s_xrows) : 0ull;
+        if (base + s_xrows > cap) atomicOr(&gstat[2], 2ull);
+        xep->rbase[b] = base;
+    }
     if (tid == 0) atomicMax(&gstat[1], (unsigned long long)s_ranges);
+}
+
+// Dense rows of the buckets kc_count_s emitted as exchange pieces only (XbEmit): one workgroup per
+// bucket walks its slab run (pieces of one row are adjacent: a count past the piece width), sums
+// each row's pieces and writes the row into the bucket's reserved range rbase[b].
+__global__ void __launch_bounds__(256) kc_xb_dense(const uint64_t* __restrict__ slab, const uint64_t* __restrict__ fs,
+                                                   uint32_t F, const XbEmit* __restrict__ xep, Mix mx,
+                                                   uint64_t* __restrict__ out_key, uint32_t* __restrict__ out_cnt,
+                                                   uint64_t cap) {
+    __shared__ uint32_t ws[256 / 64 + 1];
+    const XbEmit xe = *xep;
+    const uint64_t b = blockIdx.x;
+    uint64_t m = 0;
+    for (uint32_t j = 0; j < (1u << xe.x); ++j) m += xe.dir[(b << xe.x) + j];
+    const uint64_t* __restrict__ src = slab + fs[b * (F + 1)];
+    const uint64_t kmask = xe.kb >= 64 ? ~0ull : (1ull << xe.kb) - 1, cmax = xe.cmax;
+    uint64_t o = xe.rbase[b];
+    for (uint64_t i0 = 0; i0 < m; i0 += 256) {   // uniform trip count
+        const uint64_t i = i0 + threadIdx.x;
+        const uint64_t h = i < m ? src[i] & kmask : 0ull;
+        const bool head = i < m && (i == 0 || (src[i - 1] & kmask) != h);
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<256>(head ? 1u : 0u, ws, &tot);
+        if (head) {
+            uint64_t c0 = 0, c1 = 0;
+            for (uint64_t q = i; q < m && (src[q] & kmask) == h; ++q) {
+                const uint64_t v = src[q];
+                c0 += (v >> xe.kb) & cmax;
+                if (F > 1) c1 += (v >> (xe.kb + xe.cb)) & cmax;
+            }
+            out_key[o + ex] = mix_inv(h, mx);
+            out_cnt[o + ex] = (uint32_t)c0;
+            if (F > 1) out_cnt[cap + o + ex] = (uint32_t)c1;
+        }
+        o += tot;
+    }
 }
 
 // ---------------------------------------------------------------- histogram / select
@@ -2031,7 +2079,10 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     XbEmit xe{};
     const XbEmit* d_xe = nullptr;   // the emission parameters in device memory (kernel SGPRs are full)
     s.xb_on = false;
-    if (c->comm && min_per_file == 1 && packed && e32 && !std::getenv("HGA_XB_GENERIC")) {
+    bool dumps = false;
+    for (auto& v : s.dump_keys) dumps = dumps || !v.empty();
+    s.dense_pending = false;
+    if (c->comm && min_per_file == 1 && packed && e32 && !dumps && !std::getenv("HGA_XB_GENERIC")) {
         const uint32_t P = (uint32_t)c->comm->nranks;
         const int cbits = F <= 8 ? std::min<int>(32, (64 - (int)nbits) / (int)F) : 0;
         const uint32_t eb0 = std::min<uint32_t>(10, nbits);
@@ -2042,6 +2093,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
             const uint64_t slab_n = fb3 ? (total_bytes + total_bytes / 4 + (uint64_t)nbc * SLACK_3 + 64) : total_bytes;
             xe.slab = static_cast<uint64_t*>(s.xslab.ensure(std::max<uint64_t>(slab_n, 1) * 8));
             xe.dir = static_cast<uint64_t*>(s.xdir.ensure(((uint64_t)nbc << x) * 8 + 64));
+            xe.rbase = static_cast<uint64_t*>(s.xrbase.ensure((uint64_t)nbc * 8 + 64));
             xe.x = x;
             xe.cb = (uint32_t)cbits;
             xe.kb = nbits;
@@ -2058,6 +2110,9 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
                 std::memcpy(&s.xemit_host, &xe, sizeof(XbEmit));
             }
             d_xe = d;
+            s.dense_pending = true;
+            s.xb_dev = d;
+            s.xb_cap = cap;
         }
     }
     // C: per-bucket count
@@ -2093,9 +2148,6 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     s.dist = false;
     s.n_sel = 0;
     s.pending = true;
-    bool dumps = false;
-    for (auto& v : s.dump_keys) dumps = dumps || !v.empty();
-    if (dumps) s.xb_on = false;   // the pieces would miss the cached rows
     if (dumps) count_settle(c);   // the cached rows are merged on the host side now
 }
 
@@ -2120,6 +2172,21 @@ void count_settle(hga_ctx* c, const unsigned long long* h) {
     s.instances = h[4];
     s.listed = h[5];
     merge_dump_rows(c);
+}
+
+// The dense rows of an exchange-emitting count (kc_count_s XbEmit writes pieces only), for the
+// local queries; enqueued on the stream, no host round trip.
+void count_dense(hga_ctx* c) {
+    auto& s = c->count;
+    if (!s.dense_pending) return;
+    s.dense_pending = false;
+    if (!s.xb_nbc) return;
+    c->launch("kc_xb_dense", [&] {
+        hipLaunchKernelGGL(kc_xb_dense, dim3(s.xb_nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(), s.xb_fs,
+                           s.n_files, static_cast<const XbEmit*>(s.xb_dev), make_mix(s.k), s.rows_key.as<uint64_t>(),
+                           s.rows_cnt.as<uint32_t>(), s.xb_cap);
+    });
+    c->check_launch("kc_xb_dense");
 }
 
 // Pre-counted rows of a file whose `<reads>_<k>-mers_sorted` cache exists
@@ -2183,6 +2250,7 @@ void merge_dump_rows(hga_ctx* c) {
 void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::vector<int64_t>& out) {
     auto& s = c->count;
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
     std::vector<double> thr(thr_in, thr_in + n_thr_in);   // std::set<double> semantics
     std::sort(thr.begin(), thr.end());
     thr.erase(std::unique(thr.begin(), thr.end()), thr.end());
@@ -2280,6 +2348,7 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     auto& s = c->count;
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
     const uint64_t cap = std::max<uint64_t>(s.rows, 1);
     char* sb = static_cast<char*>(s.sel_keys.ensure(cap * 12 + 256));
     uint64_t* out = reinterpret_cast<uint64_t*>(sb);
@@ -2387,6 +2456,7 @@ void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<u
     auto& s = c->count;
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
     HGA_REQUIRE(file < (int)s.n_files, HGA_ERR_INVALID, "file index out of range");
     const uint64_t rows = s.rows;
     const uint32_t F = s.n_files;

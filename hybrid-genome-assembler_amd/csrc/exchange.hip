@@ -144,6 +144,7 @@ void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint
     auto& s = c->count;
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
     HGA_REQUIRE(n_own >= 1 && n_own <= KX_MAX_OWN, HGA_ERR_INVALID, "n_owners must be in [1, 1024]");
     for (uint32_t o = 1; o + 1 < n_own; ++o)
         HGA_REQUIRE(splitters[o - 1] <= splitters[o], HGA_ERR_INVALID, "splitters must be ascending");
@@ -192,6 +193,7 @@ void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint6
     s.rows = 0;
     s.rows_cap = cap;
     s.xb_on = false;
+    s.dense_pending = false;
     if (n) {
         HGA_REQUIRE(keys && counts, HGA_ERR_INVALID, "input buffers required");
         char* w = static_cast<char*>(s.xch2.ensure(n * 8 + n * 4 + (n + 1) * 8 + 64));
@@ -781,11 +783,13 @@ __global__ void kx_xb_owner_tot(const uint64_t* __restrict__ S, uint32_t P, int 
 
 // Owner side.  S = exclusive scan of the received directories (sender-major, sender p's buckets
 // from entry src[p].off at resolution rmin + src[p].d): bucket u of this owner at the coarsest
-// resolution rmin is sender p's entries [u << d, (u + 1) << d), pieces S[off + (u << d)] ..
-// S[off + ((u + 1) << d)] of the received buffer (senders in rank order, like the directories).
+// resolution rmin is sender p's entries [u << d, (u + 1) << d), its pieces base + S[off + (u << d)]
+// - S[off] .. base + S[off + ((u + 1) << d)] - S[off] (base: the received buffer's segment of p,
+// or this rank's own slice of its send buffer).
 struct XbSrc {
     uint64_t off;
     uint32_t d, pad;
+    const uint64_t* base;
 };
 // ut[u] = the pieces of this owner's buckets before u, over all senders (no scan: each sender's
 // share is a difference of S).
@@ -812,14 +816,14 @@ __global__ void __launch_bounds__(MG_NT) kx_xb_merge(const uint64_t* __restrict_
                                                      uint32_t* __restrict__ wcnt, uint64_t n,
                                                      uint64_t* __restrict__ kept, unsigned long long* __restrict__ gstat) {
     __shared__ MergeLds<T, FMAX, KT> L;
-    __shared__ uint64_t rst[MAXP];        // sender p's run start in `in`
+    __shared__ uint64_t rst[MAXP];        // address of sender p's run
     __shared__ uint32_t rpre[MAXP + 1];   // run lengths, exclusive prefix (a bucket holds < 2^32 pieces)
     const uint32_t u = blockIdx.x;
     const int tid = threadIdx.x;
     for (uint32_t p = tid; p < P; p += MG_NT) {
         const XbSrc s = src[p];
         const uint64_t a = S[s.off + ((uint64_t)u << s.d)];
-        rst[p] = a;
+        rst[p] = reinterpret_cast<uint64_t>(s.base + (a - S[s.off]));
         rpre[p + 1] = (uint32_t)(S[s.off + ((uint64_t)(u + 1) << s.d)] - a);
     }
     __syncthreads();
@@ -842,7 +846,7 @@ __global__ void __launch_bounds__(MG_NT) kx_xb_merge(const uint64_t* __restrict_
             const uint32_t mid = (lo + hi) >> 1;
             if (rpre[mid] <= i) lo = mid; else hi = mid;
         }
-        return in[rst[lo] + (i - rpre[lo])];
+        return reinterpret_cast<const uint64_t*>(rst[lo])[i - rpre[lo]];
     };
     const uint64_t hbase = sizeof(KT) == 4 ? (u_first + u) << lowbits : 0ull;
     merge_bucket<T, FMAX, true>(L, ld, m, ubase[u], u, pf, mx, sizeof(KT) == 4 ? (1ull << lowbits) - 1 : kmask, hbase,
@@ -867,6 +871,7 @@ uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t 
     auto& s = c->count;
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
     HGA_REQUIRE(n_own >= 1 && n_own <= KX_MAX_OWN, HGA_ERR_INVALID, "n_owners must be in [1, 1024]");
     const int cb = count_pack_bits(c);
     HGA_REQUIRE(cb > 0, HGA_ERR_INVALID, "rows of this k / file count do not pack into 64 bits");
@@ -931,6 +936,7 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
     s.rows = 0;
     s.rows_cap = cap;
     s.xb_on = false;
+    s.dense_pending = false;
     if (n) {
         HGA_REQUIRE(pieces, HGA_ERR_INVALID, "input buffer required");
         // table slots per bucket (u64 key + F u32 counts): 32 KB for F <= 2, so four workgroups share a CU
@@ -1007,42 +1013,50 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
 // bucket if every rank holds as many rows as this one, within [EB0, min(2k, XB_MAXR)]).
 int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner) {
     auto& s = c->count;
-    count_settle(c);
-    HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
     HGA_REQUIRE(P >= 1 && P <= XB_MAXP, HGA_ERR_INVALID, "at most 1024 ranks");
-    const int cb = count_pack_bits(c);
-    HGA_REQUIRE(cb > 0, HGA_ERR_INVALID, "rows of this k / file count do not pack into 64 bits");
-    const PackFmt pf{2 * s.k, cb, s.n_files, (1ull << cb) - 1};
-    const Mix mx = make_mix(s.k);
     const int eb0 = std::min(10, 2 * s.k);
-    const int rmax = std::min(2 * s.k, XB_MAXR);
-    const uint64_t rows = s.rows;
-    if (s.xb_on && s.xb_P == P && !s.listed) {   // the count kernel already grouped the pieces
+    if (s.xb_on && s.xb_P == P) {   // the count kernel grouped the pieces (unless it left a bucket to kc_count)
+        // one host round trip: the count's counters and the per-owner totals come back together
         const int R = s.xb_R;
         const uint64_t nb = 1ull << R;
-        char* w = static_cast<char*>(s.xch.ensure((nb + 1) * 8 + 8 * (uint64_t)P + 64));
+        char* w = static_cast<char*>(s.xch.ensure((nb + 1) * 8 + 64));
         uint64_t* S = reinterpret_cast<uint64_t*>(w);
-        uint64_t* per_d = S + nb + 1;
+        auto* hp = static_cast<unsigned long long*>(s.xpack_h.ensure(8 * (8 + (uint64_t)P)));
         HGA_HIP(hipMemcpyAsync(S, s.xdir.p, nb * 8, hipMemcpyDeviceToDevice, c->stream));
         HGA_HIP(hipMemsetAsync(S + nb, 0, 8, c->stream));
         exclusive_scan_u64(c, S, nb + 1, s.scratch);
         c->launch("kx_xb_pack", [&] {
-            hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream, S, P, eb0, R, per_d);
+            hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream, S, P, eb0, R,
+                               reinterpret_cast<uint64_t*>(s.xpack_h.dev(hp + 8)));
         });
         c->check_launch("kx_xb_owner_tot");
-        HGA_HIP(hipMemcpyAsync(per_owner, per_d, 8 * (uint64_t)P, hipMemcpyDeviceToHost, c->stream));
+        const bool pend = s.pending;
+        if (pend) HGA_HIP(hipMemcpyAsync(hp, s.cursor.p, 64, hipMemcpyDeviceToHost, c->stream));
         c->sync();
-        uint64_t total = 0;
-        for (uint32_t o = 0; o < P; ++o) total += per_owner[o];
-        HGA_REQUIRE(total < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per rank");
-        uint64_t* out = static_cast<uint64_t*>(s.xsend.ensure(std::max<uint64_t>(total, 1) * 8 + 64));
-        c->launch("kx_xb_gather", [&] {
-            hipLaunchKernelGGL(kx_xb_gather, dim3(s.xb_nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(), s.xb_fs,
-                               s.n_files, s.xb_x, S, out);
-        });
-        c->check_launch("kx_xb_gather");
-        return R;
+        if (pend) count_settle(c, hp);
+        HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+        if (s.xb_on && !s.listed) {
+            uint64_t total = 0;
+            for (uint32_t o = 0; o < P; ++o) total += (per_owner[o] = hp[8 + o]);
+            HGA_REQUIRE(total < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per rank");
+            uint64_t* out = static_cast<uint64_t*>(s.xsend.ensure(std::max<uint64_t>(total, 1) * 8 + 64));
+            c->launch("kx_xb_gather", [&] {
+                hipLaunchKernelGGL(kx_xb_gather, dim3(s.xb_nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(),
+                                   s.xb_fs, s.n_files, s.xb_x, S, out);
+            });
+            c->check_launch("kx_xb_gather");
+            return R;
+        }
     }
+    count_settle(c);
+    HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
+    const int cb = count_pack_bits(c);
+    HGA_REQUIRE(cb > 0, HGA_ERR_INVALID, "rows of this k / file count do not pack into 64 bits");
+    const PackFmt pf{2 * s.k, cb, s.n_files, (1ull << cb) - 1};
+    const Mix mx = make_mix(s.k);
+    const int rmax = std::min(2 * s.k, XB_MAXR);
+    const uint64_t rows = s.rows;
     int R = eb0;
     while (R < rmax && ((uint64_t)1024 << R) < rows * P) ++R;
     if (const char* e = std::getenv("HGA_XB_R")) R = std::max(eb0, std::min(rmax, std::atoi(e)));   // test hook
@@ -1085,8 +1099,8 @@ int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner) {
 }
 
 // Owner: every sender's runs of this owner's buckets -> merged ctx rows (drop at min_c per file).
-void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from,
-                    uint32_t P, uint32_t me, uint32_t min_c) {
+void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* self, const uint64_t* n_from,
+                    const uint64_t* dir_in, const int* r_from, uint32_t P, uint32_t me, uint32_t min_c) {
     auto& s = c->count;
     count_settle(c);
     HGA_REQUIRE(min_c >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
@@ -1102,12 +1116,14 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, cons
         HGA_REQUIRE(r_from[p] >= eb0 && r_from[p] <= 2 * s.k, HGA_ERR_COMM, "exchange: bad bucket resolution");
         rmin = std::min(rmin, r_from[p]);
     }
-    std::vector<XbSrc> src(P);
-    uint64_t n = 0, nd = 0;
+    // the senders' run tables go up through mapped pinned memory (no pageable copy)
+    XbSrc* src = static_cast<XbSrc*>(s.xsrc_h.ensure(sizeof(XbSrc) * P + 64));
+    uint64_t n = 0, nd = 0, po = 0;
     for (uint32_t p = 0; p < P; ++p) {
-        src[p] = XbSrc{nd, (uint32_t)(r_from[p] - rmin), 0};
+        src[p] = XbSrc{nd, (uint32_t)(r_from[p] - rmin), 0, p == me ? self : in + po};
         nd += first(me + 1, r_from[p]) - first(me, r_from[p]);
         n += n_from[p];
+        if (p != me) po += n_from[p];
     }
     HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per merge");
     const uint64_t units = first(me + 1, rmin) - first(me, rmin);
@@ -1120,6 +1136,7 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, cons
     s.rows = 0;
     s.rows_cap = cap;
     s.xb_on = false;
+    s.dense_pending = false;
     // S (nd + 1) | ut = unit starts (units + 1) | kept (units + 1) | gstat 2 | wkey n | wcnt F n
     char* w = static_cast<char*>(s.xch2.ensure((nd + 1 + 2 * (units + 1) + 2 + n) * 8 + 4ull * F * n + 64));
     uint64_t* S = reinterpret_cast<uint64_t*>(w);
@@ -1129,7 +1146,7 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, cons
     uint64_t* wkey = reinterpret_cast<uint64_t*>(gstat + 2);
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(wkey + n);
     XbSrc* d_src = static_cast<XbSrc*>(s.xsrc.ensure(sizeof(XbSrc) * P + 64));
-    HGA_HIP(hipMemcpyAsync(d_src, src.data(), sizeof(XbSrc) * P, hipMemcpyHostToDevice, c->stream));
+    HGA_HIP(hipMemcpyAsync(d_src, src, sizeof(XbSrc) * P, hipMemcpyHostToDevice, c->stream));
     if (nd) HGA_HIP(hipMemcpyAsync(S, dir_in, nd * 8, hipMemcpyDeviceToDevice, c->stream));
     HGA_HIP(hipMemsetAsync(S + nd, 0, 8, c->stream));
     exclusive_scan_u64(c, S, nd + 1, s.scratch);

@@ -31,13 +31,16 @@ namespace hga {
 namespace proto {
 
 // Collectives of one rank.  Host-memory forms take host pointers; `alltoallv_eng` moves engine
-// memory (device memory in the product) with per-peer slices contiguous in rank order.
+// memory (device memory in the product) with per-peer slices contiguous in rank order; with
+// keep_self false the rank's own slice stays where it is (it keeps its place in the send buffer,
+// none in the receive buffer).
 struct Xport {
     int rank = 0, nranks = 1;
     virtual ~Xport() = default;
     virtual void allgather(const void* mine, uint64_t bytes, void* all) = 0;
     virtual std::vector<std::vector<char>> allgatherv(const void* mine, uint64_t bytes) = 0;
-    virtual void alltoallv_eng(const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes) = 0;
+    virtual void alltoallv_eng(const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes,
+                               bool keep_self = true) = 0;
 };
 
 // Owner ranges over canonical codes in [0, 4^k): canonical = min(fwd, rc) of uniform codes has mass
@@ -75,10 +78,11 @@ inline uint32_t xb_owner_of_cell(uint64_t c, int P, int eb0) { return (uint32_t)
 //         orders the pieces by bucket (owner-major) in engine memory xb_pieces() and counts them per
 //         bucket in xb_dir() (u64, 2^R entries); returns R; per_owner[o] = pieces for owner o
 //     const void* xb_pieces(); const void* xb_dir();
-//     void xb_merge(const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from,
-//                   uint32_t P, uint32_t me, uint32_t min);
-//         in = every sender's pieces for this owner (sender order, n_from[p] each); dir_in = every
-//         sender's counts of this owner's buckets at its resolution r_from[p] (sender order)
+//     void xb_merge(const uint64_t* in, const uint64_t* self, const uint64_t* n_from, const uint64_t* dir_in,
+//                   const int* r_from, uint32_t P, uint32_t me, uint32_t min);
+//         in = the other senders' pieces for this owner (sender order, n_from[p] each), self = this
+//         rank's own slice of its send buffer (it does not move); dir_in = every sender's counts of
+//         this owner's buckets at its resolution r_from[p] (sender order)
 //   wide (code-range owners):
 //     void partition(const uint64_t* spl, uint32_t P, uint64_t* keys, uint32_t* counts, uint64_t* per);
 //     void merge(const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min);
@@ -115,21 +119,25 @@ uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file, const std::vector
             rf[p] = (int)all[(size_t)p * W + P];
             nd += xb_first(me + 1, P, eb0, rf[p]) - xb_first(me, P, eb0, rf[p]);
         }
-        // engine receive memory: the pieces, then the directories (8-byte aligned)
-        char* in = static_cast<char*>(e.recv_buf((n + nd + 1) * 8));
-        uint64_t* dir_in = reinterpret_cast<uint64_t*>(in + n * 8);
+        // engine receive memory: the other senders' pieces, then the directories (8-byte aligned);
+        // this rank's own slice is merged from its send buffer
+        const uint64_t n_in = n - rn[me];
+        uint64_t self_off = 0;
+        for (int p = 0; p < me; ++p) self_off += per[p];
+        char* in = static_cast<char*>(e.recv_buf((n_in + nd + 1) * 8));
+        uint64_t* dir_in = reinterpret_cast<uint64_t*>(in + n_in * 8);
         for (int p = 0; p < P; ++p) {
             sb[p] = per[p] * 8;
-            rb[p] = rn[p] * 8;
+            rb[p] = p == me ? 0 : rn[p] * 8;
         }
-        x.alltoallv_eng(e.xb_pieces(), sb.data(), in, rb.data());
+        x.alltoallv_eng(e.xb_pieces(), sb.data(), in, rb.data(), false);
         for (int p = 0; p < P; ++p) {
             sb[p] = 8 * (xb_first(p + 1, P, eb0, R) - xb_first(p, P, eb0, R));
             rb[p] = 8 * (xb_first(me + 1, P, eb0, rf[p]) - xb_first(me, P, eb0, rf[p]));
         }
         x.alltoallv_eng(e.xb_dir(), sb.data(), dir_in, rb.data());
-        e.xb_merge(reinterpret_cast<const uint64_t*>(in), rn.data(), dir_in, rf.data(), (uint32_t)P, (uint32_t)me,
-                   min_per_file);
+        e.xb_merge(reinterpret_cast<const uint64_t*>(in), static_cast<const uint64_t*>(e.xb_pieces()) + self_off,
+                   rn.data(), dir_in, rf.data(), (uint32_t)P, (uint32_t)me, min_per_file);
         return n;
     }
     const std::vector<uint64_t> spl = owner_splitters(e.k(), P);

@@ -136,8 +136,10 @@ struct CountState {
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
         sel_keys, sel_tmp, sel_wtmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, blist,
-        binned3, file_start3, xsend, xrecv, xdir, xsrc, xslab, xemit;
-    char xemit_host[32] = {};   // the XbEmit last uploaded to xemit (count.hip)
+        binned3, file_start3, xsend, xrecv, xdir, xsrc, xslab, xemit, xrbase;
+    char xemit_host[64] = {};   // the XbEmit last uploaded to xemit (count.hip)
+    PinnedBuf xsrc_h;           // the owner merge's run table, staged for upload (exchange.hip)
+    PinnedBuf xpack_h;          // count counters + per-owner piece totals of count_xb_pack
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t sel_grid = 0;   // kc_select workgroups: as many as are resident at once (count.hip)
@@ -155,6 +157,9 @@ struct CountState {
     uint32_t xb_P = 0, xb_x = 0, xb_nbc = 0;
     int xb_R = 0;
     const uint64_t* xb_fs = nullptr;
+    const void* xb_dev = nullptr;    // the XbEmit in device memory
+    uint64_t xb_cap = 0;             // rows_key / rows_cnt capacity of that run
+    bool dense_pending = false;      // rows_key / rows_cnt not written yet (count_dense)
     bool pending = false;   // count_run's counters not read back yet (count_settle)
     bool dist = false;      // rows are this rank's owner range after hga_count_exchange
     ~CountState() {
@@ -195,6 +200,7 @@ struct ConnState {
 struct Comm {
     int rank = 0, nranks = 1;
     DevBuf stage;   // device staging of host-memory collectives over RCCL (grow-only: no hipMalloc per call)
+    PinnedBuf hstage;   // their host side
     virtual ~Comm() = default;
     // true: alltoallv moves device memory (RCCL); false: host memory (the caller stages)
     virtual bool on_device() const = 0;
@@ -269,7 +275,7 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
 // bucket order in `xsend` and its per-bucket counts in `xdir` (returns the resolution R), and the
 // owner's merge of every sender's runs of its buckets
 int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner);
-void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in,
+void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* self, const uint64_t* n_from, const uint64_t* dir_in,
                     const int* r_from, uint32_t P, uint32_t me, uint32_t min_c);
 
 // comm.hip: multi-GPU counting (hga_comm_*, hga_count_exchange) and the global query answers
@@ -277,7 +283,8 @@ void comm_init_rccl(hga_ctx* c, const void* id, int rank, int nranks);
 void comm_init_host(hga_ctx* c, int rank, int nranks, const hga_transport* t);
 void comm_allgather(hga_ctx* c, const void* mine, uint64_t bytes, void* all);
 std::vector<std::vector<char>> comm_allgatherv(hga_ctx* c, const void* mine, uint64_t bytes);
-void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb);
+void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb,
+                        bool keep_self = true);
 std::vector<uint64_t> owner_splitters(int k, int P);
 void count_exchange(hga_ctx* c, uint32_t min_per_file);
 void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out);
@@ -308,6 +315,7 @@ void radix_sort_u32_from(hga_ctx* c, const uint32_t* src_k, const uint32_t* src_
 // exclusive scan of u64 in place (sort.hip)
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
 void count_settle(hga_ctx* c, const unsigned long long* h = nullptr);
+void count_dense(hga_ctx* c);
 // stable per-segment sort by the low kbits of sk (lookup.hip); false when a segment passes 16384
 bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxlen, int kbits, uint64_t* sk,
                   uint32_t* sv, DevBuf& list_buf, unsigned long long* ctr2, const char* label,

@@ -46,9 +46,10 @@ struct HostXport : Xport {
         a2a(s.data(), sb.data(), r.data(), sz.data());
         return out;
     }
-    void alltoallv_eng(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
+    void alltoallv_eng(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb, bool keep_self) override {
         std::vector<const void*> s(nranks);
         std::vector<void*> r(nranks);
+        std::vector<uint64_t> ss(sb, sb + nranks), rr(rb, rb + nranks);
         uint64_t so = 0, ro = 0;
         for (int p = 0; p < nranks; ++p) {
             s[p] = static_cast<const char*>(send) + so;
@@ -56,7 +57,8 @@ struct HostXport : Xport {
             so += sb[p];
             ro += rb[p];
         }
-        a2a(s.data(), sb, r.data(), rb);
+        if (!keep_self) ss[rank] = rr[rank] = 0;
+        a2a(s.data(), ss.data(), r.data(), rr.data());
     }
 };
 
@@ -162,8 +164,8 @@ struct HostEngine {
     const void* xb_dir() const { return xbd.data(); }
     // every bucket of the coarsest resolution from all senders' runs; checks that each run holds only
     // keys of its bucket and that the runs cover every received piece
-    void xb_merge(const uint64_t* in, const uint64_t* n_from, const uint64_t* dir_in, const int* r_from, uint32_t P,
-                  uint32_t me, uint32_t min) {
+    void xb_merge(const uint64_t* in, const uint64_t* self, const uint64_t* n_from, const uint64_t* dir_in,
+                  const int* r_from, uint32_t P, uint32_t me, uint32_t min) {
         const int eb0 = hga::proto::xb_base_bits(k_);
         const int cb = pack_bits();
         const uint64_t kmask = 2 * k_ >= 64 ? ~0ull : (1ull << (2 * k_)) - 1, cmax = (1ull << cb) - 1;
@@ -177,8 +179,8 @@ struct HostEngine {
             pre[p].assign(ne + 1, 0);
             for (uint64_t j = 0; j < ne; ++j) pre[p][j + 1] = pre[p][j] + dir_in[dof + j];
             if (pre[p][ne] != n_from[p]) throw std::runtime_error("directory does not cover the pieces");
-            src[p] = in + po;
-            po += n_from[p];
+            src[p] = p == me ? self : in + po;   // the own slice stays in the send buffer
+            if (p != me) po += n_from[p];
             dof += ne;
         }
         const uint64_t u0 = hga::proto::xb_first(me, P, eb0, rmin), u1 = hga::proto::xb_first(me + 1, P, eb0, rmin);
@@ -194,7 +196,7 @@ struct HostEngine {
                     for (uint32_t f = 0; f < F; ++f) c[f] += (src[p][i] >> (2 * k_ + f * cb)) & cmax;
                 }
             }
-        if (seen != po) throw std::runtime_error("pieces outside every bucket");
+        if (seen != po + n_from[me]) throw std::runtime_error("pieces outside every bucket");
         set_rows(m, min);
     }
     void partition(const uint64_t* spl, uint32_t P, uint64_t* ko, uint32_t* co, uint64_t* per) {

@@ -68,3 +68,42 @@ def test_rccl_one_rank_lookup_and_connections_gather(monkeypatch, self_p2p):
                                         s.ctypes.data_as(hga._u64p), g.ctypes.data_as(hga._u8p))
         assert np.array_equal(x, rx) and np.array_equal(y, ry)
         assert np.array_equal(s, rs) and np.array_equal(g, rg)
+
+
+def _heavy_streams():
+    """make_streams plus one k-mer repeated past 65536 instances in a file: its bucket goes to the
+    generic count kernel (count.hip kc_count), which does not emit exchange pieces."""
+    a, b = make_streams()
+    return [a + b"\n".join([b"A" * 60] * 1800) + b"\n", b]
+
+
+@pytest.mark.parametrize("heavy", [False, True])
+@pytest.mark.parametrize("k", [13, 19])
+def test_local_queries_of_an_exchange_count(k, heavy):
+    """With a communicator attached, count_run(ctx, 1) writes exchange pieces instead of dense rows
+    (count.hip XbEmit); local queries before the exchange rebuild the rows from them (kc_xb_dense),
+    and the exchange of a count with a generic-kernel bucket bins its rows itself."""
+    streams = _heavy_streams() if heavy else make_streams()
+    ref1 = oracle.count_pipeline(streams, k, 3, 40, min_count=1)
+    ref2 = oracle.count_pipeline(streams, k, 3, 40)
+    for query_first in (True, False):
+        with hga.Ctx(0) as ctx:
+            ctx.comm_init(hga.comm_unique_id(), 0, 1)
+            ctx.count_begin(k, len(streams))
+            for f, s in enumerate(streams):
+                ctx.count_add(f, s)
+            ctx.count_run(1)
+            if query_first:   # the local count at min 1 (no exchange yet)
+                assert ctx.count_stats().distinct_rows == len(ref1["keys"])
+                assert np.array_equal(ctx.spec_hist(THR), ref1["hist"])
+                rk, rc = ctx.rows()
+                assert np.array_equal(rk, ref1["keys"]) and np.array_equal(rc, ref1["counts"])
+                keys, flags, nd = ctx.select(3, 40)
+                assert np.array_equal(keys, ref1["selected"]) and nd == ref1["n_discr"]
+            ctx.count_exchange(2)
+            assert np.array_equal(ctx.spec_hist(THR), ref2["hist"])
+            rk, rc = ctx.rows()
+            assert np.array_equal(rk, ref2["keys"]) and np.array_equal(rc, ref2["counts"])
+            if heavy:
+                assert int(rc.max()) > 65535
+            ctx.comm_destroy()
