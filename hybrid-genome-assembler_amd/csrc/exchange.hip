@@ -522,6 +522,7 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX, KT>& L, const Loa
     const int tid = threadIdx.x;
     uint64_t rb = 0;   // rows written so far (uniform)
     const uint32_t F = pf.F;
+    const bool can_wrap = (m * pf.cmax) >> 32 != 0;          // m pieces of <= cmax each
     uint32_t P = (uint32_t)((m * 4 + 3 * T - 1) / (3 * T));   // <= 3/4 load per pass
     P = pmul ? (P ? P : 1u) * pmul : 1u;   // pmul 0: one pass whatever the size (test hook)
     P = P < 256u ? P : 256u;
@@ -556,10 +557,14 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX, KT>& L, const Loa
                 }
                 for (uint32_t f = 0; f < F; ++f) {
                     const uint32_t c = (uint32_t)((v[q] >> (pf.kb + (int)f * pf.cb)) & pf.cmax);
-                    if (c) {   // counts saturate at 2^32 - 1 like count_merge's (a wrapping add is flagged)
-                        const uint32_t old = atomicAdd(&L.tcnt[f * T + slot], c);
-                        if (old + c < old) atomicOr(&L.tsat[(f * T + slot) >> 5], 1u << ((f * T + slot) & 31));
+                    if (!c) continue;
+                    if (!can_wrap) {   // no sum of this bucket can pass 2^32 - 1: a plain add, no return
+                        atomicAdd(&L.tcnt[f * T + slot], c);
+                        continue;
                     }
+                    // counts saturate at 2^32 - 1 like count_merge's (a wrapping add is flagged)
+                    const uint32_t old = atomicAdd(&L.tcnt[f * T + slot], c);
+                    if (old + c < old) atomicOr(&L.tsat[(f * T + slot) >> 5], 1u << ((f * T + slot) & 31));
                 }
             }
         }
@@ -571,15 +576,15 @@ __device__ __forceinline__ void merge_bucket(MergeLds<T, FMAX, KT>& L, const Loa
             }
             return;   // uniform: every thread read s_ovf after the barrier
         }
-        // each thread owns ES consecutive slots and writes its kept rows straight to their place
-        // (one block scan; rows stay in slot order, no LDS round trip)
+        // each thread reads slots j * MG_NT + tid (lanes on consecutive banks) and writes its kept
+        // rows straight to a range of its own (one block scan, no LDS round trip; rows in any order)
         constexpr int ES = T / MG_NT;
         KT kk[ES];
         uint32_t cc[ES * FMAX];
         uint32_t keep = 0;
 #pragma unroll
         for (int j = 0; j < ES; ++j) {
-            const uint32_t s = tid * ES + j;
+            const uint32_t s = j * MG_NT + tid;
             kk[j] = L.tkey[s];
             bool any = false;
 #pragma unroll
@@ -1130,6 +1135,7 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* self, const 
     const uint64_t u_first = first(me, rmin);
     const uint32_t lowbits = 2u * (uint32_t)s.k - (uint32_t)rmin;
     const bool small = lowbits <= 31 && !std::getenv("HGA_XB_WIDE");   // u32 table keys (HGA_XB_WIDE: test hook)
+    const bool big_units = units && n / units > 1100;   // about 2 K pieces per unit: a 4096-slot table
     const uint64_t cap = (std::max<uint64_t>(n, 1) + 3) & ~3ull;   // x4: 16-B row groups (kc_spec_hist)
     s.rows_key.ensure(cap * 8);
     s.rows_cnt.ensure(cap * 4 * F);
@@ -1165,7 +1171,8 @@ void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* self, const 
 #define HGA_XBM(TT, FM, KT, MP)                                                                             \
     hipLaunchKernelGGL((kx_xb_merge<TT, FM, KT, MP>), dim3(units), dim3(MG_NT), 0, c->stream, in, S, d_src, P, ut, pf, mx, \
                        kmask, u_first, lowbits, min_c, pmul, wkey, wcnt, n, kept, gstat)
-                if (F <= 2 && small && P <= 64) HGA_XBM(2048, 2, uint32_t, 64);
+                if (F <= 2 && small && P <= 64 && big_units) HGA_XBM(4096, 2, uint32_t, 64);
+                else if (F <= 2 && small && P <= 64) HGA_XBM(2048, 2, uint32_t, 64);
                 else if (F <= 2 && small) HGA_XBM(2048, 2, uint32_t, XB_MAXP);
                 else if (F <= 2 && P <= 64) HGA_XBM(2048, 2, unsigned long long, 64);
                 else if (F <= 2) HGA_XBM(2048, 2, unsigned long long, XB_MAXP);
