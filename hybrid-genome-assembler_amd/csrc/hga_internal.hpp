@@ -314,6 +314,14 @@ void radix_sort_u32_from(hga_ctx* c, const uint32_t* src_k, const uint32_t* src_
                          uint64_t n, int bits, DevBuf& scratch);
 // exclusive scan of u64 in place (sort.hip)
 void exclusive_scan_u64(hga_ctx* c, uint64_t* data, uint64_t n, DevBuf& scratch);
+// status words + tile-id counter for one chained scan of nt tiles (kmer_dev.hpp chained_lookback)
+struct ScanTicket {
+    unsigned long long* status;
+    unsigned long long* ctr;
+    uint64_t tbase;
+    uint32_t epoch;
+};
+ScanTicket scan_ticket(hga_ctx* c, uint64_t nt);
 void count_settle(hga_ctx* c, const unsigned long long* h = nullptr);
 void count_dense(hga_ctx* c);
 // stable per-segment sort by the low kbits of sk (lookup.hip); false when a segment passes 16384

@@ -314,6 +314,44 @@ __device__ __forceinline__ C wave_key_add(C* ctr, uint32_t o, bool live, uint32_
     return base + (C)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Chained scan with decoupled look-back over "tiles" that take their ids in start order (a
+// counter that only grows): 64-bit status words [flag 2 | epoch 22 | value 40] published with
+// agent-scope relaxed stores; words of other scans carry another epoch and count as unpublished,
+// so the status array is never cleared between scans.  A tile only waits on tiles with smaller
+// ids, which have started.  Called by one thread: publishes `agg`, returns the tile's exclusive
+// prefix (values < 2^40).
+constexpr uint64_t SCS_A = 1ull << 62, SCS_P = 2ull << 62, SCS_F = 3ull << 62;
+constexpr uint64_t SCS_V = (1ull << 40) - 1;
+constexpr uint32_t SCS_EPOCHS = 1u << 22;
+__device__ __forceinline__ uint64_t chained_lookback(unsigned long long* __restrict__ status, uint64_t tile,
+                                                     uint64_t agg, uint32_t epoch) {
+    const uint64_t tag = (uint64_t)epoch << 40;
+    unsigned long long* st = status + tile;
+    uint64_t excl = 0;
+    if (tile == 0) {
+        __hip_atomic_store(st, SCS_P | tag | (agg & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    __hip_atomic_store(st, SCS_A | tag | (agg & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t t = (int64_t)tile - 1;
+    while (true) {
+        const uint64_t w = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t f = (((w >> 40) & (SCS_EPOCHS - 1)) == epoch) ? (w & SCS_F) : 0ull;
+        if (f == SCS_P) {
+            excl += w & SCS_V;
+            break;
+        }
+        if (f == SCS_A) {
+            excl += w & SCS_V;
+            --t;
+        }   // else: tile t has not published yet, read it again
+    }
+    // the value field is 40 bits: a prefix of 2^40 or more wraps in the published word (its flag and
+    // epoch stay intact, so successors never spin on it); callers scan counts far below 2^40
+    __hip_atomic_store(st, SCS_P | tag | ((excl + agg) & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 // Block-wide exclusive scan of one value per thread; NT threads (multiple of 64,
 // <= 1024).  `ws` is LDS scratch of >= NT/64 + 1 words.  Returns the exclusive
 // prefix; *total receives the block sum.  Contains __syncthreads().

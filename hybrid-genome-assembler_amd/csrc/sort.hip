@@ -283,33 +283,13 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
 // the LDS (rare: a prefix holding > 16384 keys) are sorted by the global radix sort.
 constexpr int SS_T = 1024, SS_I = 16, SS_CAP = SS_T * SS_I;
 
-__global__ void __launch_bounds__(SS_T) ss_segsort(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
-                                                   const uint32_t* __restrict__ ghist, int bits_low) {
-    __shared__ uint64_t sk[SS_CAP];
-    __shared__ uint32_t wcnt[SS_T / 64][256];
-    __shared__ uint32_t ws[SS_T / 64 + 1];
-    __shared__ uint32_t s_start, s_cnt;
+// One segment of cnt <= SS_CAP keys (loaded by the caller into key[], items in (wave, j, lane)
+// order) sorted in LDS by the low bits_low bits: stable LSD passes over 8-bit digits, ballot-matched
+// ranks inside each wave, waves in order.
+__device__ __forceinline__ void lds_lsd_sort(uint64_t (&key)[SS_I], uint32_t cnt, int bits_low, uint64_t* sk,
+                                             uint32_t (*wcnt)[256], uint32_t* ws) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t seg = blockIdx.x;
-    {   // this segment's start: exclusive prefix of the digit totals
-        uint32_t tot;
-        const uint32_t h = tid < 256 ? ghist[tid] : 0u;
-        const uint32_t ex = block_excl_scan<SS_T>(h, ws, &tot);
-        if (tid == (int)seg) {
-            s_start = ex;
-            s_cnt = h;
-        }
-        __syncthreads();
-    }
-    const uint32_t start = s_start, cnt = s_cnt;
-    if (cnt == 0 || cnt > (uint32_t)SS_CAP) return;   // empty, or left to the global fallback
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint64_t key[SS_I];
-#pragma unroll
-    for (int j = 0; j < SS_I; ++j) {
-        const uint32_t i = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64 + lane;
-        key[j] = i < cnt ? kin[(uint64_t)start + i] : 0ull;
-    }
     for (int sh = 0; sh < bits_low; sh += 8) {
         const uint32_t dm = bits_low - sh >= 8 ? 255u : ((1u << (bits_low - sh)) - 1u);
         for (int i = tid; i < (SS_T / 64) * 256; i += SS_T) (&wcnt[0][0])[i] = 0;
@@ -366,6 +346,35 @@ __global__ void __launch_bounds__(SS_T) ss_segsort(const uint64_t* __restrict__ 
         }
         __syncthreads();
     }
+}
+
+__global__ void __launch_bounds__(SS_T) ss_segsort(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
+                                                   const uint32_t* __restrict__ ghist, int bits_low) {
+    __shared__ uint64_t sk[SS_CAP];
+    __shared__ uint32_t wcnt[SS_T / 64][256];
+    __shared__ uint32_t ws[SS_T / 64 + 1];
+    __shared__ uint32_t s_start, s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t seg = blockIdx.x;
+    {   // this segment's start: exclusive prefix of the digit totals
+        uint32_t tot;
+        const uint32_t h = tid < 256 ? ghist[tid] : 0u;
+        const uint32_t ex = block_excl_scan<SS_T>(h, ws, &tot);
+        if (tid == (int)seg) {
+            s_start = ex;
+            s_cnt = h;
+        }
+        __syncthreads();
+    }
+    const uint32_t start = s_start, cnt = s_cnt;
+    if (cnt == 0 || cnt > (uint32_t)SS_CAP) return;   // empty, or left to the global fallback
+    uint64_t key[SS_I];
+#pragma unroll
+    for (int j = 0; j < SS_I; ++j) {
+        const uint32_t i = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64 + lane;
+        key[j] = i < cnt ? kin[(uint64_t)start + i] : 0ull;
+    }
+    lds_lsd_sort(key, cnt, bits_low, sk, wcnt, ws);
 #pragma unroll
     for (int j = 0; j < SS_I; ++j) {
         const uint32_t i = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64 + lane;
@@ -374,17 +383,10 @@ __global__ void __launch_bounds__(SS_T) ss_segsort(const uint64_t* __restrict__ 
 }
 
 // ---- exclusive scans --------------------------------------------------------------
-// Single-pass exclusive scan (chained scan with decoupled look-back, one launch): each workgroup
-// takes the next tile id from a counter that only grows (tile = counter - the value at launch),
-// scans its SC_TILE elements, publishes its aggregate (A) and then its inclusive prefix (P) in a
-// 64-bit status word [flag 2 | epoch 22 | value 40] with agent-scope relaxed stores, after adding
-// the predecessors' words (newest first) until a P.  Words of other scans carry another epoch and
-// count as unpublished, so the status array is never cleared between scans (it is when the epoch
-// wraps).  A tile only waits on tiles with smaller ids, which have started.
-constexpr uint64_t SCS_A = 1ull << 62, SCS_P = 2ull << 62, SCS_F = 3ull << 62;
-constexpr uint64_t SCS_V = (1ull << 40) - 1;
-constexpr uint32_t SCS_EPOCHS = 1u << 22;
-
+// Single-pass exclusive scan (chained scan with decoupled look-back, one launch, kmer_dev.hpp
+// chained_lookback): each workgroup takes the next tile id from a counter that only grows (tile =
+// counter - the value at launch), scans its SC_TILE elements, publishes its aggregate and then its
+// inclusive prefix.
 template <class T>
 __global__ void __launch_bounds__(SC_T) sc_onepass(T* data, uint64_t n, unsigned long long* __restrict__ status,
                                                    unsigned long long* __restrict__ ctr, uint64_t tbase,
@@ -413,32 +415,7 @@ __global__ void __launch_bounds__(SC_T) sc_onepass(T* data, uint64_t n, unsigned
             ws[w] = agg;
             agg += x;
         }
-        const uint64_t tag = (uint64_t)epoch << 40;
-        unsigned long long* st = status + tile;
-        uint64_t excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(st, SCS_P | tag | (agg & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(st, SCS_A | tag | (agg & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t t = (int64_t)tile - 1;
-            while (true) {
-                const uint64_t w = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t f = (((w >> 40) & (SCS_EPOCHS - 1)) == epoch) ? (w & SCS_F) : 0ull;
-                if (f == SCS_P) {
-                    excl += w & SCS_V;
-                    break;
-                }
-                if (f == SCS_A) {
-                    excl += w & SCS_V;
-                    --t;
-                }   // else: tile t has not published yet, read it again
-            }
-            // the value field is 40 bits: a prefix of 2^40 or more wraps in the published word (its flag
-            // and epoch stay intact, so successors never spin on it) — callers scan element counts of
-            // HBM-resident arrays, far below 2^40 (exclusive_scan_u64's contract)
-            __hip_atomic_store(st, SCS_P | tag | ((excl + agg) & SCS_V), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_pre = excl;
+        s_pre = chained_lookback(status, tile, agg, epoch);
     }
     __syncthreads();
     uint64_t run = s_pre + ws[wave] + inc - sum;
@@ -449,10 +426,11 @@ __global__ void __launch_bounds__(SC_T) sc_onepass(T* data, uint64_t n, unsigned
     }
 }
 
-template <class T>
-void excl_scan_impl(hga_ctx* c, T* data, uint64_t n) {
-    if (n == 0) return;
-    const uint64_t nt = (n + SC_TILE - 1) / SC_TILE;
+}  // namespace
+
+// Status words and tile ids for nt tiles of one chained scan (chained_lookback): a fresh epoch, the
+// tile counter's value at launch.
+ScanTicket scan_ticket(hga_ctx* c, uint64_t nt) {
     const size_t need = 256 + nt * 8;
     const bool fresh = need > c->scan_state.cap;
     auto* st = static_cast<unsigned long long*>(c->scan_state.ensure(std::max<size_t>(need, 1 << 16)));
@@ -464,14 +442,23 @@ void excl_scan_impl(hga_ctx* c, T* data, uint64_t n) {
         HGA_HIP(hipMemsetAsync(st + 32, 0, c->scan_state.cap - 256, c->stream));
         c->scan_epoch = 1;
     }
-    unsigned long long* ctr = st;        // first 256 B: the tile counter
-    unsigned long long* status = st + 32;
+    ScanTicket t{st + 32, st, c->scan_tiles, c->scan_epoch};   // first 256 B: the tile counter
+    c->scan_tiles += nt;
+    return t;
+}
+
+namespace {
+
+template <class T>
+void excl_scan_impl(hga_ctx* c, T* data, uint64_t n) {
+    if (n == 0) return;
+    const uint64_t nt = (n + SC_TILE - 1) / SC_TILE;
+    const ScanTicket t = scan_ticket(c, nt);
     c->launch("scan", [&] {
-        hipLaunchKernelGGL(sc_onepass<T>, dim3((unsigned)nt), dim3(SC_T), 0, c->stream, data, n, status, ctr,
-                           c->scan_tiles, c->scan_epoch);
+        hipLaunchKernelGGL(sc_onepass<T>, dim3((unsigned)nt), dim3(SC_T), 0, c->stream, data, n, t.status, t.ctr,
+                           t.tbase, t.epoch);
     });
     c->check_launch("sc_onepass");
-    c->scan_tiles += nt;
 }
 
 // n below which the onesweep path is used (env HGA_ONESWEEP_MAX overrides per call; 0 disables).

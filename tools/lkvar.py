@@ -16,7 +16,7 @@ bases, offsets = bench.make_c3(ga, gb, 0)
 c2 = hga.Ctx(0); c2.lookup_load(19, sdk); c2.lookup_set_reads(bases, offsets, 1); c2.lookup_run()
 c2.profile(True); c2.profile_reset()
 for _ in range(3): c2.lookup_run()
-names = ("lk_count", "lk_emit", "lk_post", "lk_sort", "radix_upsweep", "radix_downsweep", "scan")
+names = ("lk_pack", "lk_count", "lk_emit", "lk_post", "lk_sort", "lk_kci", "radix_segsort", "radix_upsweep", "radix_downsweep", "scan")
 k = {n: round(c2.profile_get(n)[0] / 3, 4) for n in names}
 c2.profile(False)
 import time
