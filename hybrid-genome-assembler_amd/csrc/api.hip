@@ -146,7 +146,7 @@ hga_status hga_count_get_stats(hga_ctx* c, hga_count_stats* out) {
         for (auto l : s.seq_len) b += l;
         out->bytes = b;
         if (s.dist) {   // after hga_count_exchange: the whole input over all ranks (no collective)
-            out->distinct_rows = s.g_rows;
+            out->distinct_rows = hga::count_global_rows(c);
             out->instances = s.g_instances;
             out->bytes = s.g_bytes;
         }

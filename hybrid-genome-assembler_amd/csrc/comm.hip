@@ -263,13 +263,45 @@ void count_exchange(hga_ctx* c, uint32_t min_per_file) {
     proto::count_exchange(e, x, min_per_file, mine, &g);
     s.g_instances = g[0];
     s.g_bytes = g[1];
-    // the global row count once, here, so hga_count_get_stats stays local (not a collective)
-    std::vector<uint64_t> gr(x.nranks);
-    uint64_t r = s.rows;
-    comm_allgather(c, &r, 8, gr.data());
-    s.g_rows = 0;
-    for (auto v : gr) s.g_rows += v;
+    // the global row count once, here, so hga_count_get_stats stays local (not a collective); over
+    // RCCL it is only enqueued (pinned staging both ways) and summed when get_stats asks for it
+    Comm& m = *c->comm;
+    const int P = x.nranks;
+    if (m.on_device()) {
+        uint64_t* hs = static_cast<uint64_t*>(s.g_rows_h.ensure(8 * ((uint64_t)P + 1)));
+        char* ds = static_cast<char*>(m.stage.ensure(8 * ((uint64_t)P + 1) + 16));
+        hs[0] = s.rows;
+        std::vector<uint64_t> sz(P, 8);
+        std::vector<const void*> sp(P, ds);
+        std::vector<void*> rp(P);
+        for (int p = 0; p < P; ++p) rp[p] = ds + 8 * (p + 1);
+        HGA_HIP(hipMemcpyAsync(ds, hs, 8, hipMemcpyHostToDevice, c->stream));
+        m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+        HGA_HIP(hipMemcpyAsync(hs + 1, ds + 8, 8 * (uint64_t)P, hipMemcpyDeviceToHost, c->stream));
+        s.g_rows_pending = true;
+        s.g_rows_P = P;
+    } else {
+        std::vector<uint64_t> gr(P);
+        uint64_t r = s.rows;
+        comm_allgather(c, &r, 8, gr.data());
+        s.g_rows = 0;
+        for (auto v : gr) s.g_rows += v;
+        s.g_rows_pending = false;
+    }
     s.dist = true;
+}
+
+// The global row count of the last exchange (its all-gather was enqueued by count_exchange).
+uint64_t count_global_rows(hga_ctx* c) {
+    auto& s = c->count;
+    if (s.g_rows_pending) {
+        c->sync();
+        const uint64_t* hs = static_cast<const uint64_t*>(s.g_rows_h.p);
+        s.g_rows = 0;
+        for (int p = 0; p < s.g_rows_P; ++p) s.g_rows += hs[1 + p];
+        s.g_rows_pending = false;
+    }
+    return s.g_rows;
 }
 
 // ---- global answers of the count queries after hga_count_exchange ----------------------------

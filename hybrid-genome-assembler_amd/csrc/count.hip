@@ -737,6 +737,22 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 constexpr uint32_t QN_C = 128;   // miss-queue entries per wave
+// Exchange emission (hga_count_exchange's hash buckets, exchange.hip count_xb_pack): with a
+// communicator attached, count_run(ctx, 1) writes every bucket's rows as packed pieces that carry
+// the mix h of the key (h in the low 2k bits, file f's count in bits [2k + f cb, ...), a count past
+// 2^cb - 1 split over several adjacent pieces) into `slab` from the bucket's first binned position
+// (pieces <= instances), and the bucket's piece count into dir[b]; the sender's gather groups them
+// by the next hash bits.  The dense rows are not written then: each bucket reserves its row range
+// once (rbase[b]) and kc_xb_dense fills it from the pieces if a local query needs them.  kc_count
+// (the buckets kc_count_s leaves to it) emits the same way.
+struct XbEmit {
+    uint64_t* slab;   // nullptr: off
+    uint64_t* dir;
+    uint64_t* rbase;
+    uint32_t cb, kb, cmax;
+};
+static_assert(sizeof(XbEmit) <= 64, "CountState::xemit_host holds one XbEmit");
+
 #ifndef HGA_EMIT_STAGE
 #define HGA_EMIT_STAGE 1
 #endif
@@ -752,9 +768,10 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
                                                  KP kp, uint64_t* __restrict__ out_key,
                                                  uint32_t* __restrict__ out_cnt, uint64_t cap,
                                                  unsigned long long* __restrict__ gstat,
-                                                 const uint32_t* __restrict__ blist) {
+                                                 const uint32_t* __restrict__ blist,
+                                                 const XbEmit* __restrict__ xep = nullptr) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_TAB];
-    __shared__ uint32_t s_occ, s_ovf, s_sp, s_ranges;
+    __shared__ uint32_t s_occ, s_ovf, s_sp, s_ranges, s_xw, s_xrows;
     __shared__ uint32_t stk_lo[40], stk_hi[40];
     __shared__ uint32_t ws[NT_C / 64 + 1];
     __shared__ unsigned long long s_base;
@@ -781,6 +798,8 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
         stk_hi[0] = full_hi;
         s_sp = 1;
         s_ranges = 0;
+        s_xw = 0;
+        s_xrows = 0;
     }
     __syncthreads();
     while (true) {
@@ -914,7 +933,7 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
             continue;
         }
         // emit the rows of this sub-range
-        if (HGA_EMIT_STAGE && F <= EMIT_F && T == (uint32_t)NT_C * EMIT_S) {
+        if (HGA_EMIT_STAGE && !xep && F <= EMIT_F && T == (uint32_t)NT_C * EMIT_S) {
             // each thread owns EMIT_S consecutive slots: rows are compacted through LDS (in
             // place, after everyone has read its slots) and then written out coalesced
             E rk[EMIT_S];
@@ -966,6 +985,40 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
             __syncthreads();
             continue;
         }
+        if (xep) {   // exchange emission (F <= 2): pieces appended to the bucket's slab run, no dense rows
+            const XbEmit xe = *xep;
+            uint64_t* __restrict__ slab = xe.slab + f[0];
+            uint32_t rows = 0;
+            for (uint32_t i0 = 0; i0 < T; i0 += NT_C) {   // uniform trip count
+                const uint32_t i = i0 + tid;
+                const E r = keys[i];
+                uint32_t c0 = 0, c1 = 0;
+                if (r != EMPTY) {
+                    c0 = cnt[i] >= mc ? cnt[i] : 0u;
+                    if (F > 1) c1 = cnt[(size_t)T + i] >= mc ? cnt[(size_t)T + i] : 0u;
+                }
+                const uint32_t big = max(c0, c1);
+                const uint32_t np = big == 0u ? 0u : big <= xe.cmax ? 1u : (uint32_t)(((uint64_t)big + xe.cmax - 1) / xe.cmax);
+                rows += np != 0u;
+                const uint32_t inc = wave_incl_scan(np, (int)lane);
+                uint32_t base = 0;
+                if (lane == 63 && inc) base = atomicAdd(&s_xw, inc);
+                base = __shfl(base, 63, 64);
+                if (!np) continue;
+                uint64_t at = (uint64_t)base + inc - np;
+                const uint64_t h = (kp.fb ? ((uint64_t)b << rbits) : 0ull) | (uint64_t)r;
+                while (c0 | c1) {   // one piece, or several adjacent ones past the piece width
+                    const uint32_t q0 = min(c0, xe.cmax), q1 = min(c1, xe.cmax);
+                    slab[at++] = h | ((uint64_t)q0 << xe.kb) | ((uint64_t)q1 << (xe.kb + xe.cb));
+                    c0 -= q0;
+                    c1 -= q1;
+                }
+            }
+            if (rows) atomicAdd(&s_xrows, rows);
+            if (tid == 0) ++s_ranges;
+            __syncthreads();
+            continue;
+        }
         uint32_t mine = 0;
         for (uint32_t i = tid; i < T; i += NT_C) {
             if (keys[i] == EMPTY) continue;
@@ -1000,6 +1053,12 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
             }
         }
         __syncthreads();
+    }
+    if (xep && tid == 0) {   // the bucket's piece count and its dense row range, reserved once
+        xep->dir[b] = s_xw;
+        const uint64_t base = s_xrows ? atomicAdd(&gstat[0], (unsigned long long)s_xrows) : 0ull;
+        if (base + s_xrows > cap) atomicOr(&gstat[2], 2ull);
+        xep->rbase[b] = base;
     }
     if (tid == 0) atomicMax(&gstat[1], (unsigned long long)s_ranges);
     }
@@ -1082,23 +1141,6 @@ __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t
     return false;
 }
 
-// Exchange emission (hga_count_exchange's hash buckets, exchange.hip count_xb_pack): with a
-// communicator attached, count_run(ctx, 1) also writes every bucket's rows as packed pieces that
-// carry the mix h of the key (h in the low 2k bits, file f's count in bits [2k + f cb, ...), a count
-// past 2^cb - 1 split over several pieces) into `slab` from the bucket's first binned position
-// (pieces <= instances), grouped by the next x bits of h in ascending order (sub-ranges of a split
-// bucket are emitted in ascending order too), and each (bucket, sub-bin)'s piece count into
-// dir[(b << x) + sub].  The owner side then needs no hashing and the sender no binning pass.
-// The dense rows are not written then: each bucket reserves its row range once (rbase[b]) and
-// kc_xb_dense fills it from the pieces if a local query needs the rows (count_dense).
-struct XbEmit {
-    uint64_t* slab;   // nullptr: off
-    uint64_t* dir;
-    uint64_t* rbase;
-    uint32_t x, cb, kb, cmax;
-};
-constexpr uint32_t XE_MAXSUB = 64;
-static_assert(sizeof(XbEmit) <= 64, "CountState::xemit_host holds one XbEmit");
 
 __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t* __restrict__ binned,
                                                       const uint64_t* __restrict__ fs, uint32_t F,
@@ -1113,7 +1155,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
     __shared__ uint32_t stk_lo[40], stk_hi[40];
     __shared__ uint32_t ws[NT_P / 64 + 1];
     __shared__ unsigned long long s_base;
-    __shared__ uint32_t s_xe[XE_MAXSUB], s_xpre[XE_MAXSUB], s_xtot[XE_MAXSUB], s_xw, s_xrows;   // exchange emission
+    __shared__ uint32_t s_xw, s_xrows;   // exchange emission: pieces and rows so far
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     uint32_t* myq = qbuf[tid >> 6];
@@ -1122,7 +1164,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
     for (uint32_t ff = 0; ff < F; ++ff)
         if (f[ff + 1] - f[ff] >= 65536u && F > 1) {   // a count could pass 16 bits: kc_count takes it
             if (tid == 0) blist[atomicAdd(&gstat[5], 1ull)] = b;
-            if (xep && (uint32_t)tid < (1u << xep->x)) xep->dir[((uint64_t)b << xep->x) + tid] = 0;   // no pieces here
+            if (xep && tid == 0) xep->dir[b] = 0;   // no pieces here
             return;
         }
     const uint32_t rbits = kp.rbits;
@@ -1137,7 +1179,6 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         s_xw = 0;
         s_xrows = 0;
     }
-    if (tid < (int)XE_MAXSUB) s_xe[tid] = s_xtot[tid] = 0;
     __syncthreads();
     while (true) {
         const uint32_t sp = s_sp;
@@ -1331,53 +1372,29 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                 }
             }
         }
-        if (xep) {   // uniform: the exchange pieces of these rows, by sub-bin, after the earlier ranges'
+        if (xep) {   // uniform: the exchange pieces of these rows after the earlier ranges' (any order)
             const XbEmit xe = *xep;
-            const uint32_t nsub = 1u << xe.x;
-            // wave-aggregated sub-bin adds (few sub-bins: per-lane LDS adds would serialise); a wave
-            // with a row past the piece width adds per lane (its row takes several pieces)
-            auto sub_add = [&](uint32_t* ctr, uint32_t j, bool ret) {
-                const bool live = j < tot;
-                const uint32_t c = live ? tcnt[j] : 0u, r = live ? tkey[j] : 0u;
-                const uint32_t big = F == 1 ? c : max(c & 0xFFFFu, c >> 16);
-                const uint32_t np = big <= xe.cmax ? 1u : (big + xe.cmax - 1) / xe.cmax;
-                const uint32_t sb = xe.x ? r >> (rbits - xe.x) : 0u;
-                uint32_t at = 0;
-                if (__ballot(live && np > 1)) {
-                    if (live) at = atomicAdd(&ctr[sb], np);
-                } else {
-                    at = wave_key_add<uint32_t>(ctr, sb, live, nsub, (int)xe.x);
-                }
-                (void)ret;
-                return at;
-            };
-            for (uint32_t j0 = 0; j0 < tot; j0 += NT_P) (void)sub_add(s_xe, j0 + tid, false);
-            __syncthreads();
-            if (tid < 64) {   // sub-bin cursors after the pieces already written for this bucket
-                const uint32_t v = (uint32_t)tid < nsub ? s_xe[tid] : 0u;
-                const uint32_t inc = wave_incl_scan(v, tid);
-                const uint32_t w0 = s_xw;
-                s_xpre[tid] = w0 + inc - v;
-                if ((uint32_t)tid < nsub) {
-                    s_xtot[tid] += v;
-                    s_xe[tid] = 0;
-                }
-                if (tid == 63) s_xw = w0 + inc;
-            }
-            __syncthreads();
             uint64_t* __restrict__ slab = xe.slab + f[0];
             for (uint32_t j0 = 0; j0 < tot; j0 += NT_P) {
                 const uint32_t j = j0 + tid;
-                uint64_t at = sub_add(s_xpre, j, true);
-                if (j >= tot) continue;
-                const uint32_t c = tcnt[j], r = tkey[j];
-                const uint64_t h = hb | r;
+                const bool live = j < tot;
+                const uint32_t c = live ? tcnt[j] : 0u;
                 uint32_t c0 = F == 1 ? c : c & 0xFFFFu, c1 = F == 1 ? 0u : c >> 16;
-                if (max(c0, c1) <= xe.cmax) {
+                const uint32_t big = max(c0, c1);
+                const uint32_t np = !live ? 0u : big <= xe.cmax ? 1u : (big + xe.cmax - 1) / xe.cmax;
+                // wave-aggregated slots: one LDS add per wave
+                const uint32_t inc = wave_incl_scan(np, (int)lane);
+                uint32_t base = 0;
+                if (lane == 63 && inc) base = atomicAdd(&s_xw, inc);
+                base = __shfl(base, 63, 64);
+                if (!live) continue;
+                uint64_t at = (uint64_t)base + inc - np;
+                const uint64_t h = hb | tkey[j];
+                if (np == 1) {
                     slab[at] = h | ((uint64_t)c0 << xe.kb) | ((uint64_t)c1 << (xe.kb + xe.cb));
                     continue;
                 }
-                while (c0 | c1) {   // a count past the piece width: several pieces of one row
+                while (c0 | c1) {   // a count past the piece width: several adjacent pieces of one row
                     const uint32_t q0 = min(c0, xe.cmax), q1 = min(c1, xe.cmax);
                     slab[at++] = h | ((uint64_t)q0 << xe.kb) | ((uint64_t)q1 << (xe.kb + xe.cb));
                     c0 -= q0;
@@ -1387,8 +1404,9 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
         }
         __syncthreads();
     }
-    if (xep && (uint32_t)tid < (1u << xep->x)) xep->dir[((uint64_t)b << xep->x) + tid] = s_xtot[tid];
-    if (xep && tid == 0) {   // the bucket's dense row range, reserved once
+    __syncthreads();
+    if (xep && tid == 0) {   // the bucket's piece count and its dense row range, reserved once
+        xep->dir[b] = s_xw;
         const uint64_t base = s_xrows ? atomicAdd(&gstat[0], (unsigned long long)s_xrows) : 0ull;
         if (base + s_xrows > cap) atomicOr(&gstat[2], 2ull);
         xep->rbase[b] = base;
@@ -1406,8 +1424,7 @@ __global__ void __launch_bounds__(256) kc_xb_dense(const uint64_t* __restrict__ 
     __shared__ uint32_t ws[256 / 64 + 1];
     const XbEmit xe = *xep;
     const uint64_t b = blockIdx.x;
-    uint64_t m = 0;
-    for (uint32_t j = 0; j < (1u << xe.x); ++j) m += xe.dir[(b << xe.x) + j];
+    const uint64_t m = xe.dir[b];
     const uint64_t* __restrict__ src = slab + fs[b * (F + 1)];
     const uint64_t kmask = xe.kb >= 64 ? ~0ull : (1ull << xe.kb) - 1, cmax = xe.cmax;
     uint64_t o = xe.rbase[b];
@@ -1914,7 +1931,10 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const uint64_t per_bucket = packed ? HGA_PB_P : 16384;
     uint32_t fb = 0, fb_max = MAX_FB;
     if (const char* e = std::getenv("HGA_FB_MAX")) fb_max = std::min<uint32_t>(MAX_FB, (uint32_t)std::atoi(e));
-    while (fb < fb_max && fb < nbits && (total_bytes >> fb) > per_bucket) ++fb;
+    // HGA_FB_MIN (test hook): at least that many bucket bits, so small inputs take the paths of large
+    // ones (the exchange emission needs fb >= 10)
+    const uint32_t fb_min = std::getenv("HGA_FB_MIN") ? (uint32_t)std::atoi(std::getenv("HGA_FB_MIN")) : 0u;
+    while (fb < fb_max && fb < nbits && ((total_bytes >> fb) > per_bucket || fb < fb_min)) ++fb;
     kp.fb = fb;
     kp.nb = 1u << fb;
     kp.rbits = nbits - fb;
@@ -1972,8 +1992,6 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     const size_t esz1 = e1_32 ? 4 : 8, esz = e32 ? 4 : 8;
     uint64_t cap = (total_bytes / std::max<uint32_t>(1, min_per_file) + 4) & ~3ull;   // x4: 16-B row groups
     if (const char* e = std::getenv("HGA_ROW_CAP")) cap = std::max<uint64_t>(4, std::strtoull(e, nullptr, 10) & ~3ull);   // test hook
-    s.rows_key.ensure(cap * 8);
-    s.rows_cnt.ensure(cap * 4 * F);
     const uint32_t slot_b = (uint32_t)esz + 4u * F;
     uint32_t T = 1;
     while ((uint64_t)T * 2 * slot_b <= LDS_TAB) T *= 2;
@@ -2089,13 +2107,14 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
         const int xoff = std::getenv("HGA_XB_XOFF") ? std::atoi(std::getenv("HGA_XB_XOFF")) : 2;   // tuning
         uint32_t x = (uint32_t)std::max(0, xoff);   // 2: C2 units of ~1024 pieces (1: 0.21 ms merge, 3: 0.19, 2: 0.14)
         for (uint32_t q = 1; q < P; q <<= 1) ++x;
-        if (kp.fb + x < eb0) x = eb0 - kp.fb;
-        if (cbits >= 4 && (1u << x) <= XE_MAXSUB && x <= kp.rbits) {
+        x = std::min<uint32_t>(x, 6u);
+        // owners' cells (EB0 bits) must be whole count buckets: the per-owner sizes come from the
+        // per-bucket counts before the gather sub-bins them
+        if (cbits >= 4 && kp.fb >= eb0 && x <= kp.rbits) {
             const uint64_t slab_n = fb3 ? (total_bytes + total_bytes / 4 + (uint64_t)nbc * SLACK_3 + 64) : total_bytes;
             xe.slab = static_cast<uint64_t*>(s.xslab.ensure(std::max<uint64_t>(slab_n, 1) * 8));
-            xe.dir = static_cast<uint64_t*>(s.xdir.ensure(((uint64_t)nbc << x) * 8 + 64));
+            xe.dir = static_cast<uint64_t*>(s.xdir_b.ensure((uint64_t)nbc * 8 + 64));
             xe.rbase = static_cast<uint64_t*>(s.xrbase.ensure((uint64_t)nbc * 8 + 64));
-            xe.x = x;
             xe.cb = (uint32_t)cbits;
             xe.kb = nbits;
             xe.cmax = (uint32_t)((1ull << cbits) - 1);
@@ -2116,6 +2135,12 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
             s.xb_cap = cap;
         }
     }
+    // the dense rows (an emitting count writes none: count_dense allocates them if a query needs them;
+    // at a C4 rank shard's min-1 capacity they would be 60 GB)
+    if (!d_xe) {
+        s.rows_key.ensure(cap * 8);
+        s.rows_cnt.ensure(cap * 4 * F);
+    }
     // C: per-bucket count
     if (packed && e32) {
         uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nbc * 4));
@@ -2127,7 +2152,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
             hipLaunchKernelGGL(kc_count<uint32_t>, dim3(std::min<uint32_t>(nbc, (uint32_t)c->num_cu)), dim3(NT_C), 0,
                                c->stream, static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,
                                s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat,
-                               (const uint32_t*)blist);
+                               (const uint32_t*)blist, d_xe);
         });
         c->check_launch("kc_count");
     } else
@@ -2182,6 +2207,8 @@ void count_dense(hga_ctx* c) {
     if (!s.dense_pending) return;
     s.dense_pending = false;
     if (!s.xb_nbc) return;
+    s.rows_key.ensure(s.xb_cap * 8);
+    s.rows_cnt.ensure(s.xb_cap * 4 * s.n_files);
     c->launch("kc_xb_dense", [&] {
         hipLaunchKernelGGL(kc_xb_dense, dim3(s.xb_nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(), s.xb_fs,
                            s.n_files, static_cast<const XbEmit*>(s.xb_dev), make_mix(s.k), s.rows_key.as<uint64_t>(),

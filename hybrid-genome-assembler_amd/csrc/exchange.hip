@@ -768,14 +768,44 @@ __global__ void __launch_bounds__(XB_NT) kx_xb_scatter(const uint64_t* __restric
 }
 
 // Pieces of the count kernel's exchange emission (count.hip XbEmit) from each count bucket's slab
-// range to its place in the send buffer (S = scanned per-(bucket, sub-bin) counts, 2^x per bucket).
+// run to its place in the send buffer (S = scanned per-bucket counts), grouped by the next x bits
+// of the hash on the way (wave-aggregated LDS ranks; any order inside a group), and the bucket's
+// 2^x group counts into the directory at resolution fb + x.
 __global__ void __launch_bounds__(256) kx_xb_gather(const uint64_t* __restrict__ slab, const uint64_t* __restrict__ fs,
-                                                    uint32_t F, uint32_t x, const uint64_t* __restrict__ S,
-                                                    uint64_t* __restrict__ out) {
+                                                    uint32_t F, uint32_t x, int sub_shift,
+                                                    const uint64_t* __restrict__ S, uint64_t* __restrict__ out,
+                                                    uint64_t* __restrict__ dir) {
+    __shared__ uint32_t cnt[64];
     const uint64_t b = blockIdx.x;
-    const uint64_t a = S[b << x], m = S[(b + 1) << x] - a;
+    const uint64_t a = S[b], m = S[b + 1] - a;
     const uint64_t* __restrict__ src = slab + fs[b * (F + 1)];
-    for (uint64_t j = threadIdx.x; j < m; j += 256) out[a + j] = src[j];
+    const uint32_t nsub = 1u << x, tid = threadIdx.x;
+    if (tid < 64) cnt[tid] = 0;
+    __syncthreads();
+    for (uint64_t i0 = 0; i0 < m; i0 += 256) {   // uniform trip count
+        const uint64_t i = i0 + tid;
+        const bool live = i < m;
+        const uint32_t sb = live ? (uint32_t)(src[i] >> sub_shift) & (nsub - 1) : 0u;
+        (void)wave_key_add<uint32_t>(cnt, sb, live, nsub, (int)x);
+    }
+    __syncthreads();
+    if (tid < 64) {   // group starts; the directory entries
+        const uint32_t v = tid < nsub ? cnt[tid] : 0u;
+        const uint32_t inc = wave_incl_scan(v, (int)tid);
+        if (tid < nsub) {
+            cnt[tid] = inc - v;
+            dir[(b << x) + tid] = v;
+        }
+    }
+    __syncthreads();
+    for (uint64_t i0 = 0; i0 < m; i0 += 256) {
+        const uint64_t i = i0 + tid;
+        const bool live = i < m;
+        const uint64_t v = live ? src[i] : 0ull;
+        const uint32_t sb = (uint32_t)(v >> sub_shift) & (nsub - 1);
+        const uint32_t pos = wave_key_add<uint32_t>(cnt, sb, live, nsub, (int)x);
+        if (live) out[a + pos] = v;
+    }
 }
 
 // Per-owner piece totals from the scanned bucket starts S (2^R + 1 entries).
@@ -1020,18 +1050,19 @@ int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner) {
     auto& s = c->count;
     HGA_REQUIRE(P >= 1 && P <= XB_MAXP, HGA_ERR_INVALID, "at most 1024 ranks");
     const int eb0 = std::min(10, 2 * s.k);
-    if (s.xb_on && s.xb_P == P) {   // the count kernel grouped the pieces (unless it left a bucket to kc_count)
-        // one host round trip: the count's counters and the per-owner totals come back together
-        const int R = s.xb_R;
-        const uint64_t nb = 1ull << R;
-        char* w = static_cast<char*>(s.xch.ensure((nb + 1) * 8 + 64));
+    if (s.xb_on && s.xb_P == P) {   // the count kernels wrote the pieces
+        // one host round trip: the count's counters and the per-owner totals come back together;
+        // owners hold whole count buckets (count_run checked fb >= EB0)
+        const int R = s.xb_R, fbc = s.xb_R - (int)s.xb_x;
+        const uint64_t nbc = s.xb_nbc;
+        char* w = static_cast<char*>(s.xch.ensure((nbc + 1) * 8 + 64));
         uint64_t* S = reinterpret_cast<uint64_t*>(w);
         auto* hp = static_cast<unsigned long long*>(s.xpack_h.ensure(8 * (8 + (uint64_t)P)));
-        HGA_HIP(hipMemcpyAsync(S, s.xdir.p, nb * 8, hipMemcpyDeviceToDevice, c->stream));
-        HGA_HIP(hipMemsetAsync(S + nb, 0, 8, c->stream));
-        exclusive_scan_u64(c, S, nb + 1, s.scratch);
+        HGA_HIP(hipMemcpyAsync(S, s.xdir_b.p, nbc * 8, hipMemcpyDeviceToDevice, c->stream));
+        HGA_HIP(hipMemsetAsync(S + nbc, 0, 8, c->stream));
+        exclusive_scan_u64(c, S, nbc + 1, s.scratch);
         c->launch("kx_xb_pack", [&] {
-            hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream, S, P, eb0, R,
+            hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream, S, P, eb0, fbc,
                                reinterpret_cast<uint64_t*>(s.xpack_h.dev(hp + 8)));
         });
         c->check_launch("kx_xb_owner_tot");
@@ -1040,14 +1071,15 @@ int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner) {
         c->sync();
         if (pend) count_settle(c, hp);
         HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
-        if (s.xb_on && !s.listed) {
+        if (s.xb_on) {
             uint64_t total = 0;
             for (uint32_t o = 0; o < P; ++o) total += (per_owner[o] = hp[8 + o]);
             HGA_REQUIRE(total < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per rank");
             uint64_t* out = static_cast<uint64_t*>(s.xsend.ensure(std::max<uint64_t>(total, 1) * 8 + 64));
+            uint64_t* dir = static_cast<uint64_t*>(s.xdir.ensure((8ull << R) + 64));
             c->launch("kx_xb_gather", [&] {
-                hipLaunchKernelGGL(kx_xb_gather, dim3(s.xb_nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(),
-                                   s.xb_fs, s.n_files, s.xb_x, S, out);
+                hipLaunchKernelGGL(kx_xb_gather, dim3((unsigned)nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(),
+                                   s.xb_fs, s.n_files, s.xb_x, 2 * s.k - R, S, out, dir);
             });
             c->check_launch("kx_xb_gather");
             return R;

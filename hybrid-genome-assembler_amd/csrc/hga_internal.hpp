@@ -136,7 +136,7 @@ struct CountState {
     // pipeline scratch
     DevBuf file_start, cursor2, fine_hist, regions, binned1, binned, rows_key, rows_cnt, cursor, scratch,
         sel_keys, sel_tmp, sel_wtmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, blist,
-        binned3, file_start3, xsend, xrecv, xdir, xsrc, xslab, xemit, xrbase;
+        binned3, file_start3, xsend, xrecv, xdir, xsrc, xslab, xemit, xrbase, xdir_b;
     char xemit_host[64] = {};   // the XbEmit last uploaded to xemit (count.hip)
     PinnedBuf xsrc_h;           // the owner merge's run table, staged for upload (exchange.hip)
     PinnedBuf xpack_h;          // count counters + per-owner piece totals of count_xb_pack
@@ -144,6 +144,9 @@ struct CountState {
     uint64_t instances = 0, rows = 0, rows_cap = 0, n_sel = 0;
     uint32_t sel_grid = 0;   // kc_select workgroups: as many as are resident at once (count.hip)
     uint64_t g_instances = 0, g_bytes = 0, g_rows = 0;   // over all ranks (set by count_exchange)
+    bool g_rows_pending = false;   // g_rows' all-gather enqueued, not summed yet (count_global_rows)
+    int g_rows_P = 0;
+    PinnedBuf g_rows_h;
     std::vector<char> tab_host;
     std::vector<double> thr_dev;   // thresholds last uploaded next to the histogram (count_spec_hist)   // last uploaded per-file tables
     // pre-counted dump rows per file (hga_count_add_rows), merged verbatim at the end of count_run
@@ -287,6 +290,7 @@ void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb, void* 
                         bool keep_self = true);
 std::vector<uint64_t> owner_splitters(int k, int P);
 void count_exchange(hga_ctx* c, uint32_t min_per_file);
+uint64_t count_global_rows(hga_ctx* c);
 void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out);
 void count_select_global(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* nd);
 void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags);

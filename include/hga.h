@@ -173,9 +173,10 @@ hga_status hga_count_merge_packed(hga_ctx* ctx, const uint64_t* pieces, uint64_t
  *   then hga_count_spec_hist / _select / _select_ex / _rows / _dump / _get_stats answer for the
  *   whole input, identically on every rank (collectives: call them on every rank, same order);
  *   hga_count_select_device leaves each owner's sorted slice on its device and returns the global
- *   (n, n_discriminative).  Owners hold ascending disjoint code ranges, so gathered results are
- *   in the reference's order (JellyfishOccurrenceReader.cpp:63-135).  A later hga_count_run makes
- *   the ctx local again until the next exchange.
+ *   (n, n_discriminative).  Gathered results are the owners' sorted slices merged by key, i.e. the
+ *   reference's order (JellyfishOccurrenceReader.cpp:63-135).  A later hga_count_run makes the ctx
+ *   local again until the next exchange.  With a communicator attached, hga_count_run(ctx, 1)
+ *   already groups its rows for the exchange; local queries before the exchange still work.
  * ------------------------------------------------------------------------------ */
 #define HGA_UNIQUE_ID_BYTES 128
 /* RCCL unique id (ncclGetUniqueId): create on one rank, hand the bytes to all ranks. */
@@ -198,9 +199,10 @@ hga_status hga_comm_init_host(hga_ctx* ctx, int rank, int nranks, const hga_tran
 hga_status hga_comm_info(hga_ctx* ctx, int* rank, int* nranks);
 hga_status hga_comm_destroy(hga_ctx* ctx);
 
-/* Owner exchange after hga_count_run(ctx, 1) on every rank: rows partitioned by canonical code,
- * one all-to-all-v of packed row pieces (one u64 each; wide rows when they do not pack), owner
- * merge with the per-file drop count >= min_per_file (jellyfish --bc, run_jellyfish.sh:3-6). */
+/* Owner exchange after hga_count_run(ctx, 1) on every rank: owners hold ranges of a hash of the
+ * k-mer; one all-to-all-v of packed row pieces (one u64 each) and one of per-bucket counts, owner
+ * merge with the per-file drop count >= min_per_file (jellyfish --bc, run_jellyfish.sh:3-6); rows
+ * that do not pack go as (key, counts) rows to canonical-code ranges. */
 hga_status hga_count_exchange(hga_ctx* ctx, uint32_t min_per_file);
 
 /* ------------------------------------------------------------------------------

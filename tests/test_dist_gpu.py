@@ -122,7 +122,8 @@ def _worker(rank, world, port, out_path, k, envs=None, big=False):
 
 
 GEN = {"HGA_XB_GENERIC": "1"}           # sender bins its rows itself (kx_xb_hist / kx_xb_scatter)
-WIDE = {"HGA_XB_WIDE": "1"}             # owner table with u64 keys
+WIDE = {"HGA_XB_WIDE": "1", "HGA_FB_MIN": "10"}   # owner table with u64 keys
+EMIT = {"HGA_FB_MIN": "10"}             # count buckets fine enough for the count kernel's emission
 
 
 def _gen(r):
@@ -131,9 +132,10 @@ def _gen(r):
 
 @pytest.mark.parametrize("world,k,envs,big,one_pass", [
     (2, 13, None, False, False), (3, 27, None, False, False), (3, 19, (WIDE,) * 3, False, False),
+    (2, 13, (EMIT, EMIT), False, False), (3, 27, (EMIT,) * 3, False, False),
     (2, 13, (_gen(10), _gen(12)), False, False),                  # senders at different resolutions
-    (3, 19, ({}, _gen(10), _gen(13)), False, False),              # count-kernel emission next to generic senders
-    (2, 19, None, True, False), (2, 19, (GEN, GEN), True, False),
+    (3, 19, (EMIT, _gen(10), _gen(13)), False, False),            # count-kernel emission next to generic senders
+    (2, 19, (EMIT, EMIT), True, False), (2, 19, (GEN, GEN), True, False),
     (1, 19, (_gen(10),), True, False), (1, 19, (_gen(10),), True, True)])   # multi-pass / overflowing buckets
 def test_count_exchange_processes(tmp_path, monkeypatch, world, k, envs, big, one_pass):
     """The hash-bucket exchange (exchange.hip kx_xb_*): senders' pieces grouped by the count kernel

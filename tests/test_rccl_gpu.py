@@ -18,11 +18,14 @@ pytestmark = pytest.mark.gpu
 THR = oracle.THRESHOLDS
 
 
+@pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("self_p2p", [False, True])
 @pytest.mark.parametrize("k", [13, 27])
-def test_rccl_one_rank_count_exchange(monkeypatch, self_p2p, k):
+def test_rccl_one_rank_count_exchange(monkeypatch, self_p2p, k, emit):
     if self_p2p:
         monkeypatch.setenv("HGA_RCCL_SELF", "1")
+    if emit:   # buckets fine enough for the count kernel's exchange emission
+        monkeypatch.setenv("HGA_FB_MIN", "10")
     streams = make_streams()
     ref = oracle.count_pipeline(streams, k, 3, 40)
     with hga.Ctx(0) as ctx:
@@ -33,6 +36,7 @@ def test_rccl_one_rank_count_exchange(monkeypatch, self_p2p, k):
             ctx.count_add(f, s)
         ctx.count_run(1)
         ctx.count_exchange(2)
+        assert ctx.count_stats().distinct_rows == len(ref["keys"])   # the enqueued row-count gather
         assert np.array_equal(ctx.spec_hist(THR), ref["hist"])
         keys, flags, nd = ctx.select(3, 40)
         assert np.array_equal(keys, ref["selected"]) and nd == ref["n_discr"]
@@ -79,10 +83,11 @@ def _heavy_streams():
 
 @pytest.mark.parametrize("heavy", [False, True])
 @pytest.mark.parametrize("k", [13, 19])
-def test_local_queries_of_an_exchange_count(k, heavy):
+def test_local_queries_of_an_exchange_count(monkeypatch, k, heavy):
     """With a communicator attached, count_run(ctx, 1) writes exchange pieces instead of dense rows
     (count.hip XbEmit); local queries before the exchange rebuild the rows from them (kc_xb_dense),
     and the exchange of a count with a generic-kernel bucket bins its rows itself."""
+    monkeypatch.setenv("HGA_FB_MIN", "10")   # buckets fine enough for the emission
     streams = _heavy_streams() if heavy else make_streams()
     ref1 = oracle.count_pipeline(streams, k, 3, 40, min_count=1)
     ref2 = oracle.count_pipeline(streams, k, 3, 40)
