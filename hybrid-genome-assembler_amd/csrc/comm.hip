@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "exchange_protocol.hpp"
@@ -306,20 +307,102 @@ uint64_t count_global_rows(hga_ctx* c) {
 
 // ---- global answers of the count queries after hga_count_exchange ----------------------------
 
+namespace {
+// A rank's histogram slot for the one-shot gather: [overflow rows, pairs, the first cap pairs].
+constexpr uint64_t HS_CAP = 1024;
+constexpr uint64_t HS_WORDS = 2 + 2 * HS_CAP;
+__global__ void kx_hist_slot(const unsigned long long* __restrict__ ctrl, const unsigned long long* __restrict__ pairs,
+                             unsigned long long* __restrict__ slot) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        slot[0] = ctrl[0];
+        slot[1] = ctrl[2];
+    }
+    const uint64_t n = ctrl[2] < HS_CAP ? ctrl[2] : HS_CAP;
+    for (uint64_t i = t; i < 2 * n; i += (uint64_t)gridDim.x * blockDim.x) slot[2 + i] = pairs[i];
+}
+}  // namespace
+
 void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out) {
+    Comm& m = need_comm(c);
     std::vector<int64_t> local;
-    count_spec_hist(c, thr, n_thr, local);
     CtxXport x(c);
-    out = proto::spec_hist_global(x, local);
+    if (!m.on_device()) {
+        count_spec_hist(c, thr, n_thr, local);
+        out = proto::spec_hist_global(x, local);
+        return;
+    }
+    // RCCL: every rank's device pairs gathered inside the local call's one synchronisation; a rank
+    // with an overflow list or more than HS_CAP pairs sends everyone to the general gather
+    const int P = m.nranks;
+    const uint64_t sb = HS_WORDS * 8;
+    char* ds = static_cast<char*>(m.stage.ensure(sb * (P + 1) + 16));
+    auto* hs = static_cast<unsigned long long*>(m.hstage.ensure(sb * P + 16));
+    const SpecHook hook = [&](const unsigned long long* ctrl, const unsigned long long* pairs) {
+        hipLaunchKernelGGL(kx_hist_slot, dim3(8), dim3(256), 0, c->stream, ctrl, pairs,
+                           reinterpret_cast<unsigned long long*>(ds));
+        c->check_launch("kx_hist_slot");
+        std::vector<uint64_t> sz(P, sb);
+        std::vector<const void*> sp(P, ds);
+        std::vector<void*> rp(P);
+        for (int p = 0; p < P; ++p) rp[p] = ds + sb * (p + 1);
+        m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+        HGA_HIP(hipMemcpyAsync(hs, ds + sb, sb * P, hipMemcpyDeviceToHost, c->stream));
+    };
+    count_spec_hist(c, thr, n_thr, local, &hook);
+    bool fits = true;
+    for (int p = 0; p < P; ++p) fits = fits && hs[p * HS_WORDS] == 0 && hs[p * HS_WORDS + 1] <= HS_CAP;
+    if (!fits) {   // the same decision on every rank (the same gathered words)
+        out = proto::spec_hist_global(x, local);
+        return;
+    }
+    std::map<std::pair<int64_t, int64_t>, int64_t> bins;
+    for (int p = 0; p < P; ++p) {
+        const unsigned long long* sl = hs + p * HS_WORDS;
+        for (uint64_t i = 0; i < sl[1]; ++i) {
+            const uint64_t key = sl[2 + 2 * i];
+            bins[{(int64_t)(key >> 56), (int64_t)(key & ((1ull << 56) - 1))}] += (int64_t)sl[3 + 2 * i];
+        }
+    }
+    out.clear();
+    out.reserve(3 * bins.size());
+    for (const auto& b : bins) {
+        out.push_back(b.first.first);
+        out.push_back(b.first.second);
+        out.push_back(b.second);
+    }
 }
 
 void count_select_global(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* nd) {
+    Comm& m = need_comm(c);
     std::vector<uint64_t> mine(2);
-    count_select(c, lower, upper, &mine[0], &mine[1]);
-    CtxXport x(c);
-    const std::vector<uint64_t> g = proto::sum_u64(x, mine);
-    *n = g[0];
-    *nd = g[1];
+    if (!m.on_device()) {
+        count_select(c, lower, upper, &mine[0], &mine[1]);
+        CtxXport x(c);
+        const std::vector<uint64_t> g = proto::sum_u64(x, mine);
+        *n = g[0];
+        *nd = g[1];
+        return;
+    }
+    // RCCL: the counters' gather rides in the local call's one synchronisation
+    const int P = m.nranks;
+    char* ds = static_cast<char*>(m.stage.ensure(16 * ((uint64_t)P + 1) + 16));
+    auto* hs = static_cast<uint64_t*>(m.hstage.ensure(16 * (uint64_t)P + 16));
+    const SelHook hook = [&](const unsigned long long* stat) {
+        HGA_HIP(hipMemcpyAsync(ds, stat, 16, hipMemcpyDeviceToDevice, c->stream));
+        std::vector<uint64_t> sz(P, 16);
+        std::vector<const void*> sp(P, ds);
+        std::vector<void*> rp(P);
+        for (int p = 0; p < P; ++p) rp[p] = ds + 16 * (p + 1);
+        m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+        HGA_HIP(hipMemcpyAsync(hs, ds + 16, 16 * (uint64_t)P, hipMemcpyDeviceToHost, c->stream));
+    };
+    count_select(c, lower, upper, &mine[0], &mine[1], &hook);
+    *n = *nd = 0;
+    for (int p = 0; p < P; ++p) {
+        *n += hs[2 * p];
+        *nd += hs[2 * p + 1];
+    }
 }
 
 // The whole export on every rank (after count_select): keys ascending, flags.

@@ -2275,7 +2275,8 @@ void merge_dump_rows(hga_ctx* c) {
     s.min_per_file = min_c;
 }
 
-void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::vector<int64_t>& out) {
+void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::vector<int64_t>& out,
+                     const SpecHook* before_publish) {
     auto& s = c->count;
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
     count_dense(c);
@@ -2328,6 +2329,7 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     c->launch("kc_spec_hist", [&] {
         hipLaunchKernelGGL(kc_hist_compact, dim3(blocks_for(nd, NT_HC)), dim3(NT_HC), 0, c->stream, hist, n_thr, comp,
                            ctrl, ncap, c->pinned.dev(hcomp), SPEC_CHUNK);
+        if (before_publish) (*before_publish)(ctrl, comp);
         // one synchronisation: counters and (speculatively) the first chunk of triples together,
         // written into the mapped staging by the kernels themselves
         hipLaunchKernelGGL(kc_spec_publish, dim3(1), dim3(64), 0, c->stream, ctrl,
@@ -2372,7 +2374,8 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     }
 }
 
-void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uint64_t* n_discr) {
+void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uint64_t* n_discr,
+                  const SelHook* before_sync) {
     auto& s = c->count;
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
@@ -2431,6 +2434,7 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     // one synchronisation: counts, the MSD digit span and its 256 digit counts together (kc_sel_span
     // writes them into the mapped staging; without it, one copy)
     if (!(s.rows && msd)) HGA_HIP(hipMemcpyAsync(hs, stat, 64, hipMemcpyDeviceToHost, c->stream));
+    if (before_sync) (*before_sync)(stat);
     c->sync();
     const uint64_t n = hs[0];
     if (msd && n > 1) {

@@ -10,11 +10,15 @@
 //                                keys (one row per source rank at most), apply the per-file
 //                                `--bc` drop (run_jellyfish.sh:3-6, count >= min), and rebuild the
 //                                ctx rows so spec_hist / select / rows / dump run unchanged.
-// The packed form (one u64 piece per row, the default exchange) partitions with one LDS atomic
-// per owner per wave (kx_piece_hist / kx_pack_scatter) and merges without a sort: pieces are
-// binned by a hash of the key and every bin is summed in an LDS table (kx_mb_*).
-// Owners hold disjoint ascending code ranges, so per-owner exports concatenated in rank order
-// are the reference's LC_ALL=C export order (JellyfishOccurrenceReader.cpp:110-135).
+// The caller-driven packed form (hga_count_partition_packed / hga_count_merge_packed: one u64
+// piece per row, code-range owners) partitions with one LDS atomic per owner per wave
+// (kx_piece_hist / kx_pack_scatter) and merges without a sort: pieces are binned by a hash of the
+// key and every bin is summed in an LDS table (kx_mb_*).
+// hga_count_exchange uses hash-bucket owners instead (kx_xb_*, below): the count kernels write the
+// pieces (count.hip XbEmit), the sender groups them by bucket (kx_xb_gather; kx_xb_hist /
+// kx_xb_scatter when it has to bin dense rows), the owner sums each bucket from every sender's run
+// (kx_xb_merge).  Exports and rows are then the owners' sorted slices merged by key
+// (exchange_protocol.hpp merge_sorted) = the reference's LC_ALL=C order (:110-135).
 #include <cstdlib>
 
 #include "hga_internal.hpp"

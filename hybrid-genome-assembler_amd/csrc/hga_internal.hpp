@@ -11,6 +11,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/hga.h"
@@ -259,8 +260,17 @@ namespace hga {
 void count_begin(hga_ctx* c, int k, uint32_t n_files);
 void count_add(hga_ctx* c, uint32_t file, const char* seq, uint64_t n);
 void count_run(hga_ctx* c, uint32_t min_per_file);
-void count_spec_hist(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out);
-void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* n_discr);
+// before_publish (optional): called once the histogram's (threshold << 56 | total, count) pairs are
+// compacted on the device (ctrl[0] overflow rows, ctrl[2] pairs), before the call's one
+// synchronisation — the multi-GPU gather enqueues its collective there
+using SpecHook = std::function<void(const unsigned long long* d_ctrl, const unsigned long long* d_pairs)>;
+void count_spec_hist(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out,
+                     const SpecHook* before_publish = nullptr);
+// before_sync (optional): called with the device counters [n, n_discriminative] once kc_select has
+// been enqueued, before the call's one synchronisation (the multi-GPU sum enqueues its collective)
+using SelHook = std::function<void(const unsigned long long* d_stat)>;
+void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* n_discr,
+                  const SelHook* before_sync = nullptr);
 void count_fetch_selected(hga_ctx* c, uint64_t* dst, uint8_t* flags);
 void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);
 void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* keys_out,
