@@ -3,7 +3,7 @@
 # submit again, up to ~25 minutes.  Any other exit code (the command ran) is returned as is.
 # usage: tools/gpurun_wait.sh <timeout_s> '<command>'
 T=$1; shift
-for i in $(seq 1 20); do
+for i in $(seq 1 60); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@"
   rc=$?
   [ $rc -ne 3 ] && exit $rc
