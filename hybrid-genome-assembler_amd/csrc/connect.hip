@@ -222,44 +222,120 @@ __device__ __forceinline__ bool cn_insert64(uint64_t* t, uint32_t mask, uint32_t
     return false;
 }
 
-// Inclusive max-scan of own[0..CN_W) in place (CN_U consecutive entries per thread).
+// ---- Candidate order of a pivot's run.  Every tier emits its pairs sorted by candidate, so the
+// final order (score desc, pivot, candidate) is one stable pass over the score bits of the
+// pivot-ordered runs.  Sort keys are candidate << 32 | score (candidates < 2^32 - 1), ~0 pads.
+constexpr uint64_t CN_PAD = ~0ull;
+constexpr uint32_t CN_SORT_W = 512;   // runs up to this long are sorted by cn_runs_keys (one wave, 8 keys a lane)
+__device__ __forceinline__ uint64_t cn_key(uint64_t ent) { return (ent << 32) | (ent >> 32); }
+
+// Lane exchange of a u64 with lane ^ X: DPP quad permutes for X = 1, 2, ds_bpermute otherwise.
+template <int X>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
+    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    int a, b;
+    if constexpr (X == 1) {
+        a = __builtin_amdgcn_update_dpp(0, lo, 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
+        b = __builtin_amdgcn_update_dpp(0, hi, 0xB1, 0xf, 0xf, true);
+    } else if constexpr (X == 2) {
+        a = __builtin_amdgcn_update_dpp(0, lo, 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
+        b = __builtin_amdgcn_update_dpp(0, hi, 0x4E, 0xf, 0xf, true);
+    } else {
+        a = __shfl_xor(lo, X, 64);
+        b = __shfl_xor(hi, X, 64);
+    }
+    return ((uint64_t)(uint32_t)b << 32) | (uint32_t)a;
+}
+
+// Ascending bitonic sort of 64 x R keys held blocked by one wave (key index lane * R + u).
+template <int R, int K, int J>
+__device__ __forceinline__ void bitonic_step(uint64_t (&v)[R], uint32_t lane) {
+    if constexpr (J < R) {   // partners in the same lane
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if ((u & J) == 0) {
+                const bool asc = ((lane * R + u) & K) == 0;
+                const uint64_t a = v[u], b = v[u ^ J];
+                const bool sw = asc ? (a > b) : (a < b);
+                v[u] = sw ? b : a;
+                v[u ^ J] = sw ? a : b;
+            }
+        }
+    } else {   // partner lane ^ (J / R), same register
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const uint64_t o = lane_xor64<J / R>(v[u]);
+            const uint32_t i = lane * R + u;
+            const bool keep_min = ((i & J) == 0) == ((i & K) == 0);
+            v[u] = keep_min ? min(v[u], o) : max(v[u], o);
+        }
+    }
+    if constexpr (J > 1) bitonic_step<R, K, J / 2>(v, lane);
+}
+template <int R, int K>
+__device__ __forceinline__ void bitonic_stage(uint64_t (&v)[R], uint32_t lane) {
+    bitonic_step<R, K, K / 2>(v, lane);
+    if constexpr (K < 64 * R) bitonic_stage<R, K * 2>(v, lane);
+}
+
+// Bitonic sort of tab[0, n) in LDS by the whole workgroup (n a power of two, <= CN_CAP).
+__device__ void block_bitonic_sort(uint64_t* tab, uint32_t n) {
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j; j >>= 1) {
+            for (uint32_t x = threadIdx.x; x < n / 2; x += CN_T) {
+                const uint32_t i = 2 * x - (x & (j - 1)), q = i + j;
+                const uint64_t a = tab[i], b = tab[q];
+                const bool asc = (i & k) == 0;
+                if (asc ? a > b : a < b) {
+                    tab[i] = b;
+                    tab[q] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Inclusive max-scan of own[0..CN_W) in place (CN_U = 8 consecutive bytes per thread, one u64).
+static_assert(CN_U == 8, "owner map: eight pairs (one u64 of bytes) per thread");
 __device__ __forceinline__ void cn_owner_scan(uint8_t* own, uint32_t* ws) {
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint64_t* own64 = reinterpret_cast<uint64_t*>(own);
+    const uint64_t ov = own64[t];
     uint32_t v[CN_U];
     uint32_t m = 0;
 #pragma unroll
     for (int u = 0; u < CN_U; ++u) {
-        m = max(m, (uint32_t)own[t * CN_U + u]);
+        m = max(m, (uint32_t)(ov >> (8 * u)) & 0xFFu);
         v[u] = m;
     }
-    uint32_t x = m;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x = max(x, y);
-    }
+    const uint32_t x = wave_scan_max_dpp(m);
     if (lane == 63) ws[wave] = x;
     __syncthreads();
-    uint32_t pre = __shfl_up(x, 1, 64);
-    if (lane == 0) pre = 0;
+    uint32_t pre = dpp_take<0x138, 0xf>(x);   // wave_shr:1: the max over earlier lanes
     for (uint32_t w = 0; w < wave; ++w) pre = max(pre, ws[w]);
+    uint64_t nv = 0;
 #pragma unroll
-    for (int u = 0; u < CN_U; ++u) own[t * CN_U + u] = (uint8_t)max(pre, v[u]);
+    for (int u = 0; u < CN_U; ++u) nv |= (uint64_t)max(pre, v[u]) << (8 * u);
+    own64[t] = nv;
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint32_t* __restrict__ piv,
-                                                 uint32_t* __restrict__ ovf_list, unsigned long long* __restrict__ ovf_n,
-                                                 uint32_t limit) {
-    __shared__ uint64_t tab[CN_CAP];
-    __shared__ uint64_t lo[CN_T];
-    __shared__ uint32_t off[CN_T + 1];
-    __shared__ uint8_t own[CN_W];
-    __shared__ uint32_t sh[12];   // [0] fill, [1] ovf, [2..] scan scratch
+struct CnBlockLds {
+    uint64_t tab[CN_CAP];
+    uint64_t lo[CN_T];   // per hit of the chunk: kci offset of its list minus its first pair index
+    uint32_t sh[12];   // [0] fill, [1] ovf, [2..] scan scratch, [11] next listed pivot
+    alignas(8) uint8_t own[CN_W];
+    unsigned long long base_s;
+};
+
+// Pivot p by the whole workgroup (every thread calls it; the return is uniform).  False when its
+// distinct candidates passed `limit`: nothing was emitted and the caller lists p for the next tier.
+__device__ bool cn_block_pivot(const CnIn& in, const CnOut& out, uint32_t p, uint32_t limit, CnBlockLds& L) {
     const uint32_t t = threadIdx.x;
-    const uint32_t p = piv ? piv[blockIdx.x] : blockIdx.x;
+    __syncthreads();   // the previous pivot's table reads are done
     const uint64_t b = in.hit_ptr[p], e = in.hit_ptr[p + 1];
-    if (e - b < (uint64_t)in.min_kmers || e == b) return;
+    if (e - b < (uint64_t)in.min_kmers || e == b) return true;
     // pair count -> table size (>= 2 x distinct candidates when it fits)
     uint64_t acc = 0;
     for (uint64_t i = b + t; i < e; i += CN_T) {
@@ -268,15 +344,15 @@ __global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint3
     }
 #pragma unroll
     for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((t & 63) == 0) sh[4 + (t >> 6)] = (uint32_t)min<uint64_t>(acc, 1u << 30);
-    if (t < 2) sh[t] = 0;
+    if ((t & 63) == 0) L.sh[4 + (t >> 6)] = (uint32_t)min<uint64_t>(acc, 1u << 30);
+    if (t < 2) L.sh[t] = 0;
     __syncthreads();
-    const uint64_t pairs = (uint64_t)sh[4] + sh[5] + sh[6] + sh[7];
+    const uint64_t pairs = (uint64_t)L.sh[4] + L.sh[5] + L.sh[6] + L.sh[7];
     uint32_t size = 256;
     while (size < CN_CAP && size < 2 * pairs) size <<= 1;
     const uint32_t mask = size - 1;
     const uint32_t lim = min(limit, size * 3 / 4 + (size < CN_CAP ? size : 0u));   // small tables cannot fill
-    for (uint32_t s2 = t; s2 < size; s2 += CN_T) tab[s2] = CN_EMPTY64;
+    for (uint32_t s2 = t; s2 < size; s2 += CN_T) L.tab[s2] = CN_EMPTY64;
     __syncthreads();
     bool ok = true;
     for (uint64_t cb = b; cb < e && ok; cb += CN_T) {
@@ -289,76 +365,84 @@ __global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint3
             len = (uint32_t)(in.kci_ptr[kid + 1] - l0);
         }
         uint32_t T;
-        const uint32_t o = block_excl_scan<CN_T>(len, sh + 2, &T);
-        lo[t] = l0;
-        off[t] = o;
-        if (t == 0) off[CN_T] = T;
+        const uint32_t o = block_excl_scan<CN_T>(len, L.sh + 2, &T);
+        L.lo[t] = l0 - o;   // pair j of this hit reads kci[l0 + j - o]
         for (uint32_t w0 = 0; w0 < T && ok; w0 += CN_W) {
             // owner map of pairs [w0, w0 + CN_W): segment starts, then a max-scan
-#pragma unroll
-            for (int u = 0; u < CN_U; ++u) own[t * CN_U + u] = 0;
+            reinterpret_cast<uint64_t*>(L.own)[t] = 0;
             __syncthreads();
-            if (len && o >= w0 && o < w0 + CN_W) own[o - w0] = (uint8_t)t;
-            if (w0 && o < w0 && o + len > w0) own[0] = (uint8_t)t;   // segment straddling the window start
+            if (len && o >= w0 && o < w0 + CN_W) L.own[o - w0] = (uint8_t)t;
+            if (w0 && o < w0 && o + len > w0) L.own[0] = (uint8_t)t;   // segment straddling the window start
             __syncthreads();
-            cn_owner_scan(own, sh + 2);
+            cn_owner_scan(L.own, L.sh + 2);
             uint32_t cand[CN_U];
 #pragma unroll
             for (int u = 0; u < CN_U; ++u) {
                 const uint32_t j = w0 + t + CN_T * u;
                 cand[u] = CN_EMPTY;
-                if (j < T) {
-                    const uint32_t a = own[j - w0];
-                    cand[u] = in.kci[lo[a] + (j - off[a])];
-                }
+                if (j < T) cand[u] = in.kci[L.lo[L.own[j - w0]] + j];
             }
 #pragma unroll
             for (int u = 0; u < CN_U; ++u)
-                if (cand[u] != CN_EMPTY && cand[u] != p) (void)cn_insert64(tab, mask, cand[u], &sh[0], lim, &sh[1]);
+                if (cand[u] != CN_EMPTY && cand[u] != p) (void)cn_insert64(L.tab, mask, cand[u], &L.sh[0], lim, &L.sh[1]);
             __syncthreads();
-            ok = __atomic_load_n(&sh[1], __ATOMIC_RELAXED) == 0;
+            ok = __atomic_load_n(&L.sh[1], __ATOMIC_RELAXED) == 0;
         }
         __syncthreads();
     }
-    if (!ok) {
-        if (t == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = p;
-        return;
-    }
-    // emit: survivors compacted with one global atomic per workgroup
+    if (!ok) return false;
+    // emit: survivors compacted to tab[0, total), sorted by candidate, one global atomic per workgroup
     const uint32_t per = size / CN_T ? size / CN_T : 1;
     const uint32_t s0 = t * per;
+    uint64_t ent[CN_CAP / CN_T];
     uint32_t cnt = 0, mx = 0;
-    for (uint32_t s2 = s0; s2 < s0 + per && s2 < size; ++s2) {
-        const uint64_t v = tab[s2];
-        const uint32_t c = (uint32_t)(v >> 32);
-        if ((uint32_t)v != CN_EMPTY && c >= in.min_score) {
-            ++cnt;
-            mx = max(mx, c);
+#pragma unroll
+    for (uint32_t u = 0; u < CN_CAP / CN_T; ++u) {
+        ent[u] = CN_PAD;
+        if (u < per && s0 + u < size) {
+            const uint64_t v = L.tab[s0 + u];
+            const uint32_t c = (uint32_t)(v >> 32);
+            if ((uint32_t)v != CN_EMPTY && c >= in.min_score) {
+                ent[u] = cn_key(v);
+                ++cnt;
+                mx = max(mx, c);
+            }
         }
     }
 #pragma unroll
     for (int o2 = 32; o2; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o2, 64));
     uint32_t total;
-    const uint32_t pre = block_excl_scan<CN_T>(cnt, sh + 2, &total);
-    if (total == 0) return;
-    __shared__ unsigned long long base_s;
+    const uint32_t pre = block_excl_scan<CN_T>(cnt, L.sh + 2, &total);   // its barriers end the table reads
+    if (total == 0) return true;
+    uint32_t n2 = 2;
+    while (n2 < total) n2 <<= 1;
+    uint32_t w0 = pre;
+#pragma unroll
+    for (uint32_t u = 0; u < CN_CAP / CN_T; ++u)
+        if (ent[u] != CN_PAD) L.tab[w0++] = ent[u];
+    for (uint32_t i = total + t; i < n2; i += CN_T) L.tab[i] = CN_PAD;
     const uint32_t reg = p % CN_R;
     if (t == 0) {
-        base_s = cn_reserve(out, reg, total);
-        cn_note(out, p, reg, base_s, total);
+        L.base_s = cn_reserve(out, reg, total);
+        cn_note(out, p, reg, L.base_s, total);
     }
     if ((t & 63) == 0 && mx) atomicMax(&out.ctr[1], (unsigned long long)mx);
     __syncthreads();
-    uint64_t w = base_s + pre;
-    for (uint32_t s2 = s0; s2 < s0 + per && s2 < size && cnt; ++s2) {
-        const uint64_t v = tab[s2];
-        const uint32_t c = (uint32_t)(v >> 32);
-        if ((uint32_t)v != CN_EMPTY && c >= in.min_score) {
-            cn_put(out, reg, w, p, (uint32_t)v, c);
-            ++w;
-            --cnt;
-        }
+    if (total > CN_SORT_W) block_bitonic_sort(L.tab, n2);   // shorter runs: cn_runs_keys
+    const uint64_t base = L.base_s;
+    for (uint32_t i = t; i < total; i += CN_T) {
+        const uint64_t k = L.tab[i];
+        cn_put(out, reg, base + i, p, (uint32_t)(k >> 32), (uint32_t)k);
     }
+    return true;
+}
+
+__global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint32_t* __restrict__ piv,
+                                                 uint32_t* __restrict__ ovf_list, unsigned long long* __restrict__ ovf_n,
+                                                 uint32_t limit) {
+    __shared__ CnBlockLds L;
+    const uint32_t p = piv ? piv[blockIdx.x] : blockIdx.x;
+    if (!cn_block_pivot(in, out, p, limit, L) && threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = p;
 }
 
 // ---- cn_wave: the first tier — one wave per pivot, pivots taken from a work counter.
@@ -376,22 +460,59 @@ constexpr uint32_t CNW_CAP = HGA_CNW_CAP;
 constexpr uint32_t CNW_W = 512;            // pairs per owner-map window
 constexpr int CNW_U = CNW_W / 64;
 constexpr int CNW_WAVES = HGA_CNW_WAVES;
-constexpr uint32_t CNW_GRAB = 8;         // pivots per work-counter atomic
+#ifndef HGA_CNW_GRAB
+#define HGA_CNW_GRAB 2
+#endif
+#ifndef HGA_CNW_MINW
+#define HGA_CNW_MINW 7
+#endif
+#ifndef HGA_CN_BIG_HITS
+#define HGA_CN_BIG_HITS 768
+#endif
+constexpr uint32_t CNW_GRAB = HGA_CNW_GRAB;   // pivots per work-counter atomic
 
 struct CnWaveLds {
     uint64_t tab[CNW_CAP];
-    uint64_t lo[64];
-    uint32_t off[64];
-    uint8_t own[CNW_W];
+    uint64_t base[64];             // per hit of the chunk: kci offset of its list minus its first pair index
+    uint64_t own[CNW_W / 8];       // owner map, one byte per pair of the window
     uint32_t fill, ovf;
 };
+static_assert(CNW_U == 8, "owner map: eight pairs (one u64 of bytes) per lane");
+static_assert(CNW_CAP * 3 / 4 <= CN_SORT_W, "wave-tier runs are sorted by cn_runs_keys");
 
-__global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, const uint32_t* __restrict__ piv,
+// Tiers 1 and 2 in one launch: every workgroup first takes listed pivots (more than `big_hits`
+// hits, from cn_big_list) one at a time as a workgroup (cn_block_pivot), then its waves take the
+// other pivots one wave each.  The long pivots start first and the short ones fill in behind
+// them, with no host round trip between the tiers; a listed pivot that overflows the workgroup
+// table goes to ovf2 (the HBM tier), a wave pivot that overflows its wave table to ovf_list.
+union CnFusedLds {
+    CnBlockLds B;
+    CnWaveLds W[CNW_WAVES];
+};
+
+__global__ void __launch_bounds__(64 * CNW_WAVES, HGA_CNW_MINW) cn_wave(CnIn in, CnOut out, const uint32_t* __restrict__ piv,
                                                           uint64_t n_piv, uint32_t* __restrict__ ovf_list,
-                                                          uint32_t limit) {
-    __shared__ CnWaveLds S[CNW_WAVES];
+                                                          uint32_t limit, const uint32_t* __restrict__ big,
+                                                          uint64_t big_hits, uint32_t limit_b,
+                                                          uint32_t* __restrict__ ovf2) {
+    static_assert(64 * CNW_WAVES == CN_T, "the workgroup tier runs on the wave tier's workgroups");
+    __shared__ CnFusedLds U;
+    {
+        const unsigned long long n_big = out.ctr[0];
+        while (true) {
+            __syncthreads();
+            if (threadIdx.x == 0) U.B.sh[11] = (uint32_t)atomicAdd(out.ctr + 7, 1ull);
+            __syncthreads();
+            const uint32_t idx = U.B.sh[11];
+            if (idx >= n_big) break;
+            const uint32_t p = big[idx];
+            if (!cn_block_pivot(in, out, p, limit_b, U.B) && threadIdx.x == 0) ovf2[atomicAdd(out.ctr + 3, 1ull)] = p;
+        }
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    CnWaveLds& W = S[wave];
+    CnWaveLds& W = U.W[wave];
+    uint8_t* own8 = reinterpret_cast<uint8_t*>(W.own);
     for (uint32_t s2 = lane; s2 < CNW_CAP; s2 += 64) W.tab[s2] = CN_EMPTY64;
     // pivots are taken CNW_GRAB at a time (device-wide same-address atomics serialise) and the
     // largest score is kept per wave until the end
@@ -408,7 +529,7 @@ __global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, co
         const uint32_t p = piv ? piv[q] : (uint32_t)q;
         ++q;
         const uint64_t b = in.hit_ptr[p], e = in.hit_ptr[p + 1];
-        if (e - b < (uint64_t)in.min_kmers || e == b) continue;
+        if (e - b < (uint64_t)in.min_kmers || e == b || e - b > big_hits) continue;   // listed: done above
         if (lane == 0) {
             W.fill = 0;
             W.ovf = 0;
@@ -424,51 +545,52 @@ __global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, co
                 l0 = in.kci_ptr[kid];
                 len = (uint32_t)(in.kci_ptr[kid + 1] - l0);
             }
-            const uint32_t inc = wave_incl_scan(len, (int)lane);
+            // pairs of the chunk numbered 0..T: hit h owns [o, o + len); pair j of h reads kci[l0 + j - o]
+            const uint32_t inc = wave_scan_add_dpp(len);
             const uint32_t o = inc - len;
-            const uint32_t T = __shfl(inc, 63, 64);
-            W.lo[lane] = l0;
-            W.off[lane] = o;
+            const uint32_t T = wave_lane(inc, 63);
+            W.base[lane] = l0 - o;
             for (uint32_t w0 = 0; w0 < T && ok; w0 += CNW_W) {
-                // owner map of pairs [w0, w0 + CNW_W): segment starts, then a wave max-scan
-#pragma unroll
-                for (int u = 0; u < CNW_U; ++u) W.own[lane * CNW_U + u] = 0;
+                // owner map of pairs [w0, w0 + CNW_W): segment starts, then a max-scan (bytes within a
+                // lane's u64, then across lanes)
+                W.own[lane] = 0;
                 wave_lds_sync();
-                if (len && o >= w0 && o < w0 + CNW_W) W.own[o - w0] = (uint8_t)lane;
-                if (w0 && o < w0 && o + len > w0) W.own[0] = (uint8_t)lane;
+                if (len && o >= w0 && o < w0 + CNW_W) own8[o - w0] = (uint8_t)lane;
+                if (w0 && o < w0 && o + len > w0) own8[0] = (uint8_t)lane;
                 wave_lds_sync();
+                const uint64_t ov = W.own[lane];
                 uint32_t v[CNW_U];
                 uint32_t m = 0;
 #pragma unroll
                 for (int u = 0; u < CNW_U; ++u) {
-                    m = max(m, (uint32_t)W.own[lane * CNW_U + u]);
+                    m = max(m, (uint32_t)(ov >> (8 * u)) & 0xFFu);
                     v[u] = m;
                 }
-                uint32_t x = m;
+                // the largest owner over earlier lanes: the inclusive max-scan moved up one lane (wave_shr:1)
+                const uint32_t before = dpp_take<0x138, 0xf>(wave_scan_max_dpp(m));
+                uint64_t nv = 0;
 #pragma unroll
-                for (int o2 = 1; o2 < 64; o2 <<= 1) {
-                    const uint32_t y = __shfl_up(x, o2, 64);
-                    if (lane >= (uint32_t)o2) x = max(x, y);
-                }
-                uint32_t pre = __shfl_up(x, 1, 64);
-                if (lane == 0) pre = 0;
+                for (int u = 0; u < CNW_U; ++u) nv |= (uint64_t)max(before, v[u]) << (8 * u);
                 wave_lds_sync();
-#pragma unroll
-                for (int u = 0; u < CNW_U; ++u) W.own[lane * CNW_U + u] = (uint8_t)max(pre, v[u]);
+                W.own[lane] = nv;
                 wave_lds_sync();
                 uint32_t cand[CNW_U];
 #pragma unroll
                 for (int u = 0; u < CNW_U; ++u) {
                     const uint32_t j = w0 + lane + 64 * u;
                     cand[u] = CN_EMPTY;
-                    if (j < T) {
-                        const uint32_t a = W.own[j - w0];
-                        cand[u] = in.kci[W.lo[a] + (j - W.off[a])];
-                    }
+                    if (j < T) cand[u] = in.kci[W.base[own8[j - w0]] + j];
                 }
 #pragma unroll
                 for (int u = 0; u < CNW_U; ++u)
-                    if (cand[u] != CN_EMPTY && cand[u] != p)
+                    if (cand[u] != CN_EMPTY && cand[u] != p
+#ifdef HGA_CN_DIAG_HALF
+                        && cand[u] > p
+#endif
+#ifdef HGA_CN_DIAG_NOINS
+                        && cand[u] == 0xFFFFFFF0u
+#endif
+                    )
                         (void)cn_insert64(W.tab, CNW_CAP - 1, cand[u], &W.fill, limit, &W.ovf);
                 wave_lds_sync();
                 ok = __atomic_load_n(&W.ovf, __ATOMIC_RELAXED) == 0;
@@ -481,7 +603,7 @@ __global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, co
             wave_lds_sync();
             continue;
         }
-        // emit (and reset the table for the next pivot)
+        // emit (and reset the table for the next pivot); cn_runs_keys sorts the run by candidate
         constexpr int PER = CNW_CAP / 64;
         uint64_t ent[PER];
         uint32_t cnt = 0, mx = 0;
@@ -498,8 +620,8 @@ __global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, co
             }
         }
         wave_lds_sync();
-        const uint32_t inc = wave_incl_scan(cnt, (int)lane);
-        const uint32_t tot = __shfl(inc, 63, 64);
+        const uint32_t inc = wave_scan_add_dpp(cnt);
+        const uint32_t tot = wave_lane(inc, 63);
         if (!tot) continue;
 #pragma unroll
         for (int o2 = 32; o2; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o2, 64));
@@ -521,6 +643,17 @@ __global__ void __launch_bounds__(64 * CNW_WAVES) cn_wave(CnIn in, CnOut out, co
         }
     }
     if (lane == 0 && wmax) atomicMax(&out.ctr[1], (unsigned long long)wmax);
+}
+
+// Pivots with more than big_hits hits (and at least min_kmers), for cn_wave's workgroup tier.
+__global__ void cn_big_list(const uint64_t* __restrict__ hit_ptr, const uint32_t* __restrict__ piv, uint64_t n_piv,
+                            uint32_t min_kmers, uint64_t big_hits, uint32_t* __restrict__ big,
+                            unsigned long long* __restrict__ n_big) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n_piv) return;
+    const uint32_t p = piv ? piv[q] : (uint32_t)q;
+    const uint64_t h = hit_ptr[p + 1] - hit_ptr[p];
+    if (h > big_hits && h >= min_kmers) big[atomicAdd(n_big, 1ull)] = p;
 }
 
 // Upper bound of a pivot's distinct candidates: its (id, candidate) pair count.
@@ -647,6 +780,45 @@ __global__ void __launch_bounds__(256) cn_gather(const uint64_t* __restrict__ ps
         sv[o + i] = s[g + i];
     }
 }
+// Pivot p's run copied to its scanned offset as the final sort key
+// (pivot << ib | candidate) << sb | (max - score), in candidate order: one wave per pivot; runs of
+// up to CN_SORT_W pairs are sorted here in registers (64 x R keys, R the smallest power of two
+// that holds the run), longer ones come sorted from the workgroup tier.
+template <int R>
+__device__ __forceinline__ void cn_run_sort_put(uint64_t p, uint64_t o, uint64_t m, uint64_t g, uint32_t lane, int ib,
+                                                int sb, uint32_t mxs, const uint32_t* __restrict__ y,
+                                                const uint32_t* __restrict__ s, uint64_t* __restrict__ key) {
+    uint64_t v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint32_t i = lane * R + u;
+        v[u] = i < m ? ((uint64_t)y[g + i] << 32) | s[g + i] : CN_PAD;
+    }
+    bitonic_stage<R, 2>(v, lane);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint32_t i = lane * R + u;
+        if (i < m) key[o + i] = (((p << ib) | (v[u] >> 32)) << sb) | (uint64_t)(mxs - (uint32_t)v[u]);
+    }
+}
+__global__ void __launch_bounds__(256) cn_runs_keys(const uint64_t* __restrict__ pst, const uint64_t* __restrict__ poff,
+                                                    uint64_t nr, int ib, int sb, uint32_t mxs,
+                                                    const uint32_t* __restrict__ y, const uint32_t* __restrict__ s,
+                                                    uint64_t* __restrict__ key) {
+    const uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= nr) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t o = poff[p], m = poff[p + 1] - o;
+    if (!m) return;
+    const uint64_t g = pst[p];
+    if (m <= 64) cn_run_sort_put<1>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
+    else if (m <= 128) cn_run_sort_put<2>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
+    else if (m <= 256) cn_run_sort_put<4>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
+    else if (m <= CN_SORT_W) cn_run_sort_put<8>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
+    else
+        for (uint64_t i = lane; i < m; i += 64)
+            key[o + i] = ((((uint64_t)p << ib) | y[g + i]) << sb) | (uint64_t)(mxs - s[g + i]);
+}
 // key = (pivot << ib | candidate) << sb | (max - score): a stable sort by the low sb bits of keys
 // already in (pivot, candidate) order gives (score desc, pivot, candidate)
 __global__ void cn_keys3(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint64_t n, uint32_t mxs,
@@ -715,6 +887,21 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
         d_piv = S.piv.as<uint32_t>();
         c->sync();
     }
+#ifdef HGA_CN_DIAG_LPT
+    if (!pivots) {   // experiment: pivots in descending hit count (host order)
+        std::vector<uint64_t> hp(nr + 1);
+        HGA_HIP(hipMemcpyAsync(hp.data(), L.hit_ptr.p, (nr + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        std::vector<uint32_t> idx(nr);
+        for (uint64_t i = 0; i < nr; ++i) idx[i] = (uint32_t)i;
+        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b2) {
+            return hp[a + 1] - hp[a] > hp[b2 + 1] - hp[b2];
+        });
+        HGA_HIP(hipMemcpyAsync(S.piv.ensure(nr * 4), idx.data(), nr * 4, hipMemcpyHostToDevice, c->stream));
+        d_piv = S.piv.as<uint32_t>();
+        c->sync();
+    }
+#endif
     HGA_REQUIRE(P < (1u << 31), HGA_ERR_INVALID, "too many pivots");
     const int32_t* d_cat = nullptr;
     if (categories) {
@@ -746,6 +933,12 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
         c->sync();
         std::memcpy(h, hc.data(), sizeof(h));
     };
+    // pivots with more hits than this start first, one workgroup each (inside cn_wave); ~0: none.
+    // The wave tables hold 3/4 x CNW_CAP distinct candidates: on C3, 2.3 % of the reads pass
+    // that, nearly all of them long reads (tools/cnstats.py).
+    uint64_t big_hits = force_block ? ~0ull : HGA_CN_BIG_HITS;
+    if (const char* bh = std::getenv("HGA_CN_BIG_HITS")) big_hits = std::strtoull(bh, nullptr, 10);
+    uint32_t* big = static_cast<uint32_t*>(S.big.ensure(P * 4));
     std::vector<uint64_t> rpre(CN_R + 1, 0);
     for (int attempt = 0; attempt < 2; ++attempt) {
         const uint64_t cap = rcap * CN_R;
@@ -753,10 +946,19 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
                   static_cast<uint32_t*>(S.s.ensure(cap * 4)), rcap, ctr, rcur, pst, pcnt};
         HGA_HIP(hipMemsetAsync(ctr, 0, ctr_bytes, c->stream));
         if (pcnt) HGA_HIP(hipMemsetAsync(pcnt, 0, (nr + 1) * 8, c->stream));
-        const uint64_t wblk = std::min<uint64_t>((P + CNW_WAVES - 1) / CNW_WAVES, (uint64_t)c->num_cu * 7);
+        static const int wres = [] {   // resident cn_wave workgroups per CU: one round of the grid
+            int nb = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cn_wave, 64 * CNW_WAVES, 0) != hipSuccess || nb < 1) nb = 4;
+            return nb;
+        }();
+        const uint64_t wblk = std::min<uint64_t>((P + CNW_WAVES - 1) / CNW_WAVES, (uint64_t)c->num_cu * wres);
         c->launch("cn_wave", [&] {
+            if (big_hits != ~0ull)
+                hipLaunchKernelGGL(cn_big_list, dim3(cn_blocks(P, 256)), dim3(256), 0, c->stream, in.hit_ptr, d_piv, P,
+                                   min_kmers, big_hits, big, ctr);
             hipLaunchKernelGGL(cn_wave, dim3((unsigned)wblk), dim3(64 * CNW_WAVES), 0, c->stream, in, out, d_piv, P,
-                               ovf, force_block ? 1u : CNW_CAP * 3 / 4);
+                               ovf, force_block ? 1u : CNW_CAP * 3 / 4, big, big_hits,
+                               force_global ? 1u : CN_CAP * 3 / 4, ovf2);
         });
         c->check_launch("cn_wave");
         readback();
@@ -822,6 +1024,23 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     if (n && runs && sb + 2 * ib <= 64) {
         // pivot-ordered runs, each sorted by candidate, then one stable pass over the score bits
         exclusive_scan_u64(c, pcnt, nr + 1, L.scratch);
+        if (!h[3] && !std::getenv("HGA_CN_SEGSORT")) {   // no HBM-tier run: sorted in cn_runs_keys
+            uint64_t* key = static_cast<uint64_t*>(S.key.ensure(n * 8));
+            c->launch("cn_sort", [&] {
+                hipLaunchKernelGGL(cn_runs_keys, dim3(cn_blocks(nr, 4)), dim3(256), 0, c->stream, pst, pcnt, nr, ib,
+                                   sb, mxs, S.y.as<uint32_t>(), S.s.as<uint32_t>(), key);
+            });
+            c->check_launch("cn_runs_keys");
+            radix_sort_u64(c, key, nullptr, n, sb, L.scratch);
+            c->launch("cn_sort", [&] {
+                hipLaunchKernelGGL(cn_decode3, dim3(cn_blocks(n, 256)), dim3(256), 0, c->stream, key, n, mxs, ib, sb,
+                                   d_cat, L.first_read_id, ox, oy, os, og);
+            });
+            c->check_launch("cn_decode3");
+            done = true;
+        }
+    }
+    if (n && runs && !done && sb + 2 * ib <= 64) {   // an HBM-tier pivot's run is in table order
         uint64_t* sk = static_cast<uint64_t*>(S.sk2.ensure(n * 8));
         uint32_t* sv = static_cast<uint32_t*>(S.sv2.ensure(n * 4));
         c->launch("cn_sort", [&] {

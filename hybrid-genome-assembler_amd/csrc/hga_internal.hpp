@@ -196,7 +196,7 @@ struct LookupState {
 struct ConnState {
     bool ready = false;
     uint64_t n = 0, cap_hint = 0;
-    DevBuf piv, cat, ctr, rpre, ovf, ovf2, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og, pst, pcnt, sk2, sv2,
+    DevBuf piv, cat, ctr, rpre, ovf, ovf2, big, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og, pst, pcnt, sk2, sv2,
         lst;
 };
 

@@ -259,6 +259,35 @@ __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("" ::: "memory");
 }
 
+// Inclusive wave64 scans through DPP row shifts and row broadcasts: VALU only, no LDS-pipe
+// traffic (a shuffle scan issues one ds_bpermute per step).  Lanes whose DPP source is outside
+// the row, and the rows a broadcast step leaves out, read the identity 0, so the operation must
+// have 0 as its identity (unsigned add / max).  All 64 lanes must be active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_take(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_scan_add_dpp(uint32_t x) {
+    x += dpp_take<0x111, 0xf>(x);   // row_shr:1
+    x += dpp_take<0x112, 0xf>(x);   // row_shr:2
+    x += dpp_take<0x114, 0xf>(x);   // row_shr:4
+    x += dpp_take<0x118, 0xf>(x);   // row_shr:8
+    x += dpp_take<0x142, 0xa>(x);   // row_bcast:15 into rows 1, 3
+    x += dpp_take<0x143, 0xc>(x);   // row_bcast:31 into rows 2, 3
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_scan_max_dpp(uint32_t x) {
+    x = max(x, dpp_take<0x111, 0xf>(x));
+    x = max(x, dpp_take<0x112, 0xf>(x));
+    x = max(x, dpp_take<0x114, 0xf>(x));
+    x = max(x, dpp_take<0x118, 0xf>(x));
+    x = max(x, dpp_take<0x142, 0xa>(x));
+    x = max(x, dpp_take<0x143, 0xc>(x));
+    return x;
+}
+// Value of lane L (uniform result, no LDS).
+__device__ __forceinline__ uint32_t wave_lane(uint32_t x, int L) { return (uint32_t)__builtin_amdgcn_readlane((int)x, L); }
+
 // Wave / block scans (wave64).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll

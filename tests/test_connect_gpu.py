@@ -60,10 +60,12 @@ def test_connections_filters_and_pivots(gpu_ctx, golden_case):
 
 
 @pytest.mark.parametrize("env", [None, "HGA_CN_FORCE_BLOCK", "HGA_CN_FORCE_GLOBAL", "HGA_CN_TWO_STAGE", "HGA_CN_RCAP",
-                                 "HGA_CN_FULL_SORT"])
+                                 "HGA_CN_FULL_SORT", "HGA_CN_BIG_HITS=0", "HGA_CN_BIG_HITS=60"])
 def test_connections_random_first_id(gpu_ctx, hga_mod, monkeypatch, env):
+    """HGA_CN_BIG_HITS: pivots with more hits than that take cn_wave's workgroup tier first (0: all)."""
     if env:
-        monkeypatch.setenv(env, "1")
+        name, _, val = env.partition("=")
+        monkeypatch.setenv(name, val or "1")
     gnm = hga_mod.gen_genome(60_000, 11)
     r = hga_mod.gen_nanosim(gnm, 300, 12)
     c, _ = oracle.kmer_windows(gnm, 17)
@@ -92,6 +94,12 @@ def test_connections_overflow_pivot(gpu_ctx, hga_mod):
     exp = oracle.connections(idx, min_score=1)
     assert int((exp[0] == 1).sum()) > 3500   # the long read's row
     same(got, exp)
+    # the long read listed for the workgroup tier up front (its table overflows there too)
+    os.environ["HGA_CN_BIG_HITS"] = "100"
+    try:
+        same(gpu_ctx.connections(min_score=1), exp)
+    finally:
+        del os.environ["HGA_CN_BIG_HITS"]
 
 
 def test_connections_duplicate_kmers(gpu_ctx):
