@@ -229,33 +229,47 @@ constexpr uint64_t CN_PAD = ~0ull;
 constexpr uint32_t CN_SORT_W = 512;   // runs up to this long are sorted by cn_runs_keys (one wave, 8 keys a lane)
 __device__ __forceinline__ uint64_t cn_key(uint64_t ent) { return (ent << 32) | (ent >> 32); }
 
-// Lane exchange of a u64 with lane ^ X: DPP quad permutes for X = 1, 2, ds_bpermute otherwise.
+// Value of lane ^ X, on the VALU: DPP quad permutes (X = 1, 2), row shifts (4), a row rotate (8),
+// the gfx950 permlane swaps (16, 32).  A swap of a register with itself leaves one of its two
+// results equal to the lane's own value and the other the partner's, whichever half the
+// instruction moves, so the partner is the result that differs (equal values: either).
 template <int X>
-__device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
-    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
-    int a, b;
+__device__ __forceinline__ uint32_t lane_xor32(uint32_t v) {
     if constexpr (X == 1) {
-        a = __builtin_amdgcn_update_dpp(0, lo, 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
-        b = __builtin_amdgcn_update_dpp(0, hi, 0xB1, 0xf, 0xf, true);
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
     } else if constexpr (X == 2) {
-        a = __builtin_amdgcn_update_dpp(0, lo, 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
-        b = __builtin_amdgcn_update_dpp(0, hi, 0x4E, 0xf, 0xf, true);
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
+    } else if constexpr (X == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xf, 0xf, true);   // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+        return (__lane_id() & 4) ? dn : up;
+    } else if constexpr (X == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, true);   // row_ror:8
+    } else if constexpr (X == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return r[0] == v ? r[1] : r[0];
     } else {
-        a = __shfl_xor(lo, X, 64);
-        b = __shfl_xor(hi, X, 64);
+        static_assert(X == 32, "lane_xor32: X in {1, 2, 4, 8, 16, 32}");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return r[0] == v ? r[1] : r[0];
     }
-    return ((uint64_t)(uint32_t)b << 32) | (uint32_t)a;
 }
+template <int X>
+__device__ __forceinline__ uint64_t lane_xor(uint64_t v) {
+    return ((uint64_t)lane_xor32<X>((uint32_t)(v >> 32)) << 32) | lane_xor32<X>((uint32_t)v);
+}
+template <int X>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) { return lane_xor32<X>(v); }
 
 // Ascending bitonic sort of 64 x R keys held blocked by one wave (key index lane * R + u).
-template <int R, int K, int J>
-__device__ __forceinline__ void bitonic_step(uint64_t (&v)[R], uint32_t lane) {
+template <int R, int K, int J, class T>
+__device__ __forceinline__ void bitonic_step(T (&v)[R], uint32_t lane) {
     if constexpr (J < R) {   // partners in the same lane
 #pragma unroll
         for (int u = 0; u < R; ++u) {
             if ((u & J) == 0) {
                 const bool asc = ((lane * R + u) & K) == 0;
-                const uint64_t a = v[u], b = v[u ^ J];
+                const T a = v[u], b = v[u ^ J];
                 const bool sw = asc ? (a > b) : (a < b);
                 v[u] = sw ? b : a;
                 v[u ^ J] = sw ? a : b;
@@ -264,7 +278,7 @@ __device__ __forceinline__ void bitonic_step(uint64_t (&v)[R], uint32_t lane) {
     } else {   // partner lane ^ (J / R), same register
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            const uint64_t o = lane_xor64<J / R>(v[u]);
+            const T o = lane_xor<J / R>(v[u]);
             const uint32_t i = lane * R + u;
             const bool keep_min = ((i & J) == 0) == ((i & K) == 0);
             v[u] = keep_min ? min(v[u], o) : max(v[u], o);
@@ -272,8 +286,8 @@ __device__ __forceinline__ void bitonic_step(uint64_t (&v)[R], uint32_t lane) {
     }
     if constexpr (J > 1) bitonic_step<R, K, J / 2>(v, lane);
 }
-template <int R, int K>
-__device__ __forceinline__ void bitonic_stage(uint64_t (&v)[R], uint32_t lane) {
+template <int R, int K, class T>
+__device__ __forceinline__ void bitonic_stage(T (&v)[R], uint32_t lane) {
     bitonic_step<R, K, K / 2>(v, lane);
     if constexpr (K < 64 * R) bitonic_stage<R, K * 2>(v, lane);
 }
@@ -437,12 +451,18 @@ __device__ bool cn_block_pivot(const CnIn& in, const CnOut& out, uint32_t p, uin
     return true;
 }
 
+// Pivots listed in piv[0, *n_piv) (the wave tier's overflow list, final when this launch starts),
+// one workgroup each over a fixed grid: launched without reading the count back.
 __global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint32_t* __restrict__ piv,
+                                                 const unsigned long long* __restrict__ n_piv,
                                                  uint32_t* __restrict__ ovf_list, unsigned long long* __restrict__ ovf_n,
                                                  uint32_t limit) {
     __shared__ CnBlockLds L;
-    const uint32_t p = piv ? piv[blockIdx.x] : blockIdx.x;
-    if (!cn_block_pivot(in, out, p, limit, L) && threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = p;
+    const unsigned long long n = *n_piv;
+    for (unsigned long long q = blockIdx.x; q < n; q += gridDim.x) {
+        const uint32_t p = piv[q];
+        if (!cn_block_pivot(in, out, p, limit, L) && threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = p;
+    }
 }
 
 // ---- cn_wave: the first tier — one wave per pivot, pivots taken from a work counter.
@@ -784,40 +804,67 @@ __global__ void __launch_bounds__(256) cn_gather(const uint64_t* __restrict__ ps
 // (pivot << ib | candidate) << sb | (max - score), in candidate order: one wave per pivot; runs of
 // up to CN_SORT_W pairs are sorted here in registers (64 x R keys, R the smallest power of two
 // that holds the run), longer ones come sorted from the workgroup tier.
-template <int R>
+// Sort keys: candidate << sbits | score in a u32 when they fit (sbits = 0: u64 keys, candidate << 32).
+template <int R, class T>
 __device__ __forceinline__ void cn_run_sort_put(uint64_t p, uint64_t o, uint64_t m, uint64_t g, uint32_t lane, int ib,
-                                                int sb, uint32_t mxs, const uint32_t* __restrict__ y,
+                                                int sb, uint32_t mxs, int sbits, const uint32_t* __restrict__ y,
                                                 const uint32_t* __restrict__ s, uint64_t* __restrict__ key) {
-    uint64_t v[R];
+    constexpr int SH = sizeof(T) == 8 ? 32 : 0;
+    const int sh = SH ? SH : sbits;
+    const T smask = (T)(((uint64_t)1 << sh) - 1);
+    T v[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
         const uint32_t i = lane * R + u;
-        v[u] = i < m ? ((uint64_t)y[g + i] << 32) | s[g + i] : CN_PAD;
+        v[u] = i < m ? (T)(((T)y[g + i] << sh) | s[g + i]) : (T)~(T)0;
     }
     bitonic_stage<R, 2>(v, lane);
 #pragma unroll
     for (int u = 0; u < R; ++u) {
         const uint32_t i = lane * R + u;
-        if (i < m) key[o + i] = (((p << ib) | (v[u] >> 32)) << sb) | (uint64_t)(mxs - (uint32_t)v[u]);
+        if (i < m)
+            key[o + i] = (((p << ib) | (uint64_t)(v[u] >> sh)) << sb) | (uint64_t)(mxs - (uint32_t)(v[u] & smask));
     }
 }
+template <class T>
+__device__ __forceinline__ void cn_run_sort_any(uint64_t p, uint64_t o, uint64_t m, uint64_t g, uint32_t lane, int ib,
+                                                int sb, uint32_t mxs, int sbits, const uint32_t* __restrict__ y,
+                                                const uint32_t* __restrict__ s, uint64_t* __restrict__ key) {
+    if (m <= 64) cn_run_sort_put<1, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+    else if (m <= 128) cn_run_sort_put<2, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+    else if (m <= 256) cn_run_sort_put<4, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+    else cn_run_sort_put<8, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+}
+#ifndef HGA_CN_RK_PPW
+#define HGA_CN_RK_PPW 4
+#endif
+constexpr int CN_RK_PPW = HGA_CN_RK_PPW;   // pivots per wave (their offsets loaded by one coalesced load)
 __global__ void __launch_bounds__(256) cn_runs_keys(const uint64_t* __restrict__ pst, const uint64_t* __restrict__ poff,
-                                                    uint64_t nr, int ib, int sb, uint32_t mxs,
+                                                    uint64_t nr, int ib, int sb, uint32_t mxs, int sbits,
                                                     const uint32_t* __restrict__ y, const uint32_t* __restrict__ s,
                                                     uint64_t* __restrict__ key) {
-    const uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (p >= nr) return;
+    const uint64_t p0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * CN_RK_PPW;
+    if (p0 >= nr) return;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t o = poff[p], m = poff[p + 1] - o;
-    if (!m) return;
-    const uint64_t g = pst[p];
-    if (m <= 64) cn_run_sort_put<1>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
-    else if (m <= 128) cn_run_sort_put<2>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
-    else if (m <= 256) cn_run_sort_put<4>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
-    else if (m <= CN_SORT_W) cn_run_sort_put<8>(p, o, m, g, lane, ib, sb, mxs, y, s, key);
-    else
-        for (uint64_t i = lane; i < m; i += 64)
-            key[o + i] = ((((uint64_t)p << ib) | y[g + i]) << sb) | (uint64_t)(mxs - s[g + i]);
+    uint64_t lo = 0, lm = 0, lg = 0;
+    if (lane < CN_RK_PPW && p0 + lane < nr) {
+        lo = poff[p0 + lane];
+        lm = poff[p0 + lane + 1] - lo;
+        lg = pst[p0 + lane];
+    }
+    for (int j = 0; j < CN_RK_PPW; ++j) {
+        const uint64_t p = p0 + j;
+        const uint64_t m = __shfl(lm, j, 64);
+        if (p >= nr) break;
+        if (!m) continue;
+        const uint64_t o = __shfl(lo, j, 64), g = __shfl(lg, j, 64);
+        if (m <= CN_SORT_W) {
+            if (sbits) cn_run_sort_any<uint32_t>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+            else cn_run_sort_any<uint64_t>(p, o, m, g, lane, ib, sb, mxs, 0, y, s, key);
+        } else
+            for (uint64_t i = lane; i < m; i += 64)
+                key[o + i] = ((((uint64_t)p << ib) | y[g + i]) << sb) | (uint64_t)(mxs - s[g + i]);
+    }
 }
 // key = (pivot << ib | candidate) << sb | (max - score): a stable sort by the low sb bits of keys
 // already in (pivot, candidate) order gives (score desc, pivot, candidate)
@@ -961,15 +1008,13 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
                                force_global ? 1u : CN_CAP * 3 / 4, ovf2);
         });
         c->check_launch("cn_wave");
+        // pivots with more distinct candidates than a wave table: one workgroup each
+        c->launch("cn_local", [&] {
+            hipLaunchKernelGGL(cn_local, dim3((unsigned)std::min<uint64_t>(P, (uint64_t)c->num_cu * 4)), dim3(CN_T), 0,
+                               c->stream, in, out, ovf, ctr + 2, ovf2, ctr + 3, force_global ? 1u : CN_CAP * 3 / 4);
+        });
+        c->check_launch("cn_local");
         readback();
-        if (h[2]) {   // pivots with more distinct candidates than a wave table: one workgroup each
-            c->launch("cn_local", [&] {
-                hipLaunchKernelGGL(cn_local, dim3((unsigned)h[2]), dim3(CN_T), 0, c->stream, in, out, ovf, ovf2,
-                                   ctr + 3, force_global ? 1u : CN_CAP * 3 / 4);
-            });
-            c->check_launch("cn_local");
-            readback();
-        }
         if (h[3]) {   // overflow pivots: HBM tables of 2 x (largest pair count), in batches of <= 1 GiB
             auto* mx = ctr + 4;
             c->launch("cn_global", [&] {
@@ -1025,15 +1070,18 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
         // pivot-ordered runs, each sorted by candidate, then one stable pass over the score bits
         exclusive_scan_u64(c, pcnt, nr + 1, L.scratch);
         if (!h[3] && !std::getenv("HGA_CN_SEGSORT")) {   // no HBM-tier run: sorted in cn_runs_keys
+            // u32 sort keys (candidate << sbits | score) when they fit, u64 otherwise
+            const int sbits = (bits_for(mxs) + ib <= 32 && !std::getenv("HGA_CN_KEY64")) ? std::max(1, bits_for(mxs)) : 0;
             uint64_t* key = static_cast<uint64_t*>(S.key.ensure(n * 8));
             c->launch("cn_sort", [&] {
-                hipLaunchKernelGGL(cn_runs_keys, dim3(cn_blocks(nr, 4)), dim3(256), 0, c->stream, pst, pcnt, nr, ib,
-                                   sb, mxs, S.y.as<uint32_t>(), S.s.as<uint32_t>(), key);
+                hipLaunchKernelGGL(cn_runs_keys, dim3(cn_blocks(nr, 4 * CN_RK_PPW)), dim3(256), 0, c->stream, pst, pcnt, nr, ib,
+                                   sb, mxs, sbits, S.y.as<uint32_t>(), S.s.as<uint32_t>(), key);
             });
             c->check_launch("cn_runs_keys");
-            radix_sort_u64(c, key, nullptr, n, sb, L.scratch);
+            uint64_t* sorted = static_cast<uint64_t*>(S.sk2.ensure(n * 8));
+            radix_sort_u64_from(c, key, sorted, n, sb, L.scratch);
             c->launch("cn_sort", [&] {
-                hipLaunchKernelGGL(cn_decode3, dim3(cn_blocks(n, 256)), dim3(256), 0, c->stream, key, n, mxs, ib, sb,
+                hipLaunchKernelGGL(cn_decode3, dim3(cn_blocks(n, 256)), dim3(256), 0, c->stream, sorted, n, mxs, ib, sb,
                                    d_cat, L.first_read_id, ox, oy, os, og);
             });
             c->check_launch("cn_decode3");

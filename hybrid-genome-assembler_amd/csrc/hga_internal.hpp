@@ -321,6 +321,8 @@ void hll_registers(hga_ctx* c, int k, int b, uint8_t* regs);
 // optional u32 payload.  Result ends in keys/vals (scratch used as ping-pong).
 void radix_sort_u64(hga_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n, int bits,
                     DevBuf& scratch);
+// keys <- src_k sorted by the low `bits` bits (src_k is left intact)
+void radix_sort_u64_from(hga_ctx* c, const uint64_t* src_k, uint64_t* keys, uint64_t n, int bits, DevBuf& scratch);
 void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int bits,
                     DevBuf& scratch);
 // the same with the input read from src_k / src_v (left intact), the result in keys / vals

@@ -24,18 +24,22 @@ constexpr int RS_T = 256;              // threads per tile
 constexpr int RS_I = HGA_RS_I;         // items per thread
 constexpr int RS_TILE = RS_T * RS_I;   // 4096 keys per tile
 constexpr int SC_T = 1024, SC_I = 4, SC_TILE = SC_T * SC_I;
+#ifndef HGA_RS_MAX_DIGIT
+#define HGA_RS_MAX_DIGIT 10
+#endif
 #ifndef HGA_LBW
 #define HGA_LBW 8   // predecessor tiles read per look-back step (independent loads per digit thread)
 #endif
 
 // dmask: the pass's digit mask (the last pass may cover fewer than 8 bits: bits above the sort
 // width are payload and must not order the keys).
-template <class K>
+template <class K, int DB>
 __global__ void __launch_bounds__(RS_T) rs_upsweep(const K* __restrict__ keys, uint64_t n,
                                                    int shift, uint32_t dmask, uint32_t* __restrict__ counts,
                                                    uint32_t n_tiles) {
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
+    constexpr int NB = 1 << DB;
+    __shared__ uint32_t h[NB];
+    for (int d = threadIdx.x; d < NB; d += RS_T) h[d] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
 #pragma unroll
@@ -44,10 +48,12 @@ __global__ void __launch_bounds__(RS_T) rs_upsweep(const K* __restrict__ keys, u
         if (i < n) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & dmask], 1u);
     }
     __syncthreads();
-    counts[(uint64_t)threadIdx.x * n_tiles + blockIdx.x] = h[threadIdx.x];
+    for (int d = threadIdx.x; d < NB; d += RS_T) counts[(uint64_t)d * n_tiles + blockIdx.x] = h[d];
 }
 
-template <class K, bool HAS_V>
+// DB-bit digits (DB = 8 .. 11): NB = 2^DB bins, each thread owns NB / RS_T consecutive digits in
+// the tile's digit scan.
+template <class K, bool HAS_V, int DB>
 __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
                                                      const uint32_t* __restrict__ vin,
                                                      K* __restrict__ kout,
@@ -55,14 +61,17 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
                                                      int shift, uint32_t dmask,
                                                      const uint32_t* __restrict__ offs,
                                                      uint32_t n_tiles) {
-    __shared__ uint32_t wcnt[4][256];
-    __shared__ uint32_t dstart[256];
+    constexpr uint32_t NB = 1u << DB;
+    constexpr int DPT = (int)NB / RS_T;
+    static_assert(DPT >= 1, "at least one digit per thread");
+    __shared__ uint32_t wcnt[4][NB];
+    __shared__ uint32_t dstart[NB];
     __shared__ uint32_t ws[8];
     __shared__ K sk[RS_TILE];
     __shared__ uint32_t sv[HAS_V ? RS_TILE : 1];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < 4 * 256; i += RS_T) (&wcnt[0][0])[i] = 0;
+    for (uint32_t i = tid; i < 4 * NB; i += RS_T) (&wcnt[0][0])[i] = 0;
     __syncthreads();
 
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
@@ -77,16 +86,16 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
         const bool ok = i < n;
         key[j] = ok ? kin[i] : K(0);
         if (HAS_V) val[j] = ok ? vin[i] : 0u;
-        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & dmask) : 256u;
+        dig[j] = ok ? ((uint32_t)(key[j] >> shift) & dmask) : NB;
     }
     // Stable rank inside the wave: items in (j, lane) order.
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
         const uint32_t d = dig[j];
-        const bool ok = d < 256u;
+        const bool ok = d < NB;
         uint64_t m = __ballot(ok);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < DB; ++b) {
             const bool bit = (d >> b) & 1u;
             const uint64_t bb = __ballot(bit);
             m &= bit ? bb : ~bb;
@@ -100,20 +109,34 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
     __syncthreads();
     // digit starts inside the tile, then per-wave starts
     {
-        const int d = tid;
-        const uint32_t c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
+        uint32_t c[DPT][4];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < DPT; ++q) {
+            const uint32_t d = tid * DPT + q;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                c[q][w] = wcnt[w][d];
+                sum += c[q][w];
+            }
+        }
         uint32_t tot;
-        const uint32_t ex = block_excl_scan<RS_T>(c0 + c1 + c2 + c3, ws, &tot);
-        dstart[d] = ex;
-        wcnt[0][d] = ex;
-        wcnt[1][d] = ex + c0;
-        wcnt[2][d] = ex + c0 + c1;
-        wcnt[3][d] = ex + c0 + c1 + c2;
+        uint32_t run = block_excl_scan<RS_T>(sum, ws, &tot);
+#pragma unroll
+        for (int q = 0; q < DPT; ++q) {
+            const uint32_t d = tid * DPT + q;
+            dstart[d] = run;
+            wcnt[0][d] = run;
+            wcnt[1][d] = run + c[q][0];
+            wcnt[2][d] = run + c[q][0] + c[q][1];
+            wcnt[3][d] = run + c[q][0] + c[q][1] + c[q][2];
+            run += c[q][0] + c[q][1] + c[q][2] + c[q][3];
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < RS_I; ++j) {
-        if (dig[j] < 256u) {
+        if (dig[j] < NB) {
             const uint32_t lp = wcnt[wave][dig[j]] + rank[j];
             sk[lp] = key[j];
             if (HAS_V) sv[lp] = val[j];
@@ -129,7 +152,6 @@ __global__ void __launch_bounds__(RS_T) rs_downsweep(const K* __restrict__ kin,
         if (HAS_V) vout[g] = sv[i];
     }
 }
-
 
 // ---- onesweep: one histogram kernel for all passes, then ONE kernel per pass ----------------
 // Each tile takes the next tile id (atomic), ranks its keys stably in LDS as above, publishes
@@ -462,6 +484,12 @@ void excl_scan_impl(hga_ctx* c, T* data, uint64_t n) {
 }
 
 // n below which the onesweep path is used (env HGA_ONESWEEP_MAX overrides per call; 0 disables).
+// Widest radix digit of the classic (upsweep / scan / downsweep) passes: HGA_RS_MAX_DIGIT, 8..11.
+inline int rs_max_digit() {
+    const char* e = std::getenv("HGA_RS_MAX_DIGIT");
+    const int v = e ? std::atoi(e) : HGA_RS_MAX_DIGIT;
+    return v < 8 ? 8 : (v > 11 ? 11 : v);
+}
 inline uint64_t hga_onesweep_max() {
     const char* e = std::getenv("HGA_ONESWEEP_MAX");
     return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)(4ull << 20);
@@ -482,7 +510,17 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
     if (n <= 1 || bits <= 0) return;
     HGA_REQUIRE(n < (1ull << 32), HGA_ERR_INVALID, "radix sort: n >= 2^32");
     const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
-    const uint64_t n_cnt = (uint64_t)256 * n_tiles;
+    const int npass = (bits + 7) / 8;
+    const bool one = n < (uint64_t)hga_onesweep_max() && npass <= 8;
+    // classic passes: 8-bit digits, or up to rs_max_digit() bits when that saves passes (one key
+    // read and write per pass; wider digits cost a larger count table and scan)
+    int db = 8;
+    if (!one) {
+        const int mx = rs_max_digit();
+        const int npw = (bits + mx - 1) / mx;
+        if (npw < npass) db = std::max(8, (bits + npw - 1) / npw);
+    }
+    const uint64_t n_cnt = ((uint64_t)1 << db) * n_tiles;
     const size_t kb = ((n * sizeof(K) + 255) & ~255ull);
     const size_t vb = vals ? ((n * 4 + 255) & ~255ull) : 0;
     const size_t cb = ((n_cnt * 4 + 255) & ~255ull);
@@ -494,9 +532,8 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
     K* kbuf = k2;
     uint32_t* va = vals;
     uint32_t* vbuf = v2;
-    const int npass = (bits + 7) / 8;
     // onesweep where launch count dominates (small n); the classic pass is faster per byte
-    if (n < (uint64_t)hga_onesweep_max() && npass <= 8) {
+    if (one) {
         const size_t hb = (size_t)npass * 256 * 4, stb = (size_t)npass * n_tiles * 256 * 4, tcb = 64;
         char* ob = static_cast<char*>(scratch.ensure(kb + vb + hb + stb + tcb));
         K* k2o = reinterpret_cast<K*>(ob);
@@ -551,31 +588,43 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
         return;
     }
     if (src_k) {
+        const int np = (bits + db - 1) / db;
         ka = const_cast<K*>(src_k);
         va = const_cast<uint32_t*>(src_v);
-        kbuf = (npass & 1) ? keys : k2;
-        vbuf = (npass & 1) ? vals : v2;
+        kbuf = (np & 1) ? keys : k2;
+        vbuf = (np & 1) ? vals : v2;
     }
-    for (int shift = 0; shift < bits; shift += 8) {
-        const uint32_t dm = bits - shift >= 8 ? 255u : ((1u << (bits - shift)) - 1u);
+    for (int shift = 0; shift < bits; shift += db) {
+        const uint32_t dm = bits - shift >= db ? (1u << db) - 1u : ((1u << (bits - shift)) - 1u);
         c->launch("radix_upsweep", [&] {
-            hipLaunchKernelGGL(rs_upsweep<K>, dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n,
-                               shift, dm, cnt, n_tiles);
+            switch (db) {
+            case 8: hipLaunchKernelGGL((rs_upsweep<K, 8>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n, shift, dm, cnt, n_tiles); break;
+            case 9: hipLaunchKernelGGL((rs_upsweep<K, 9>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n, shift, dm, cnt, n_tiles); break;
+            case 10: hipLaunchKernelGGL((rs_upsweep<K, 10>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n, shift, dm, cnt, n_tiles); break;
+            default: hipLaunchKernelGGL((rs_upsweep<K, 11>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, n, shift, dm, cnt, n_tiles); break;
+            }
         });
         c->check_launch("rs_upsweep");
         excl_scan_impl<uint32_t>(c, cnt, n_cnt);
-        if (vals) {
-            c->launch("radix_downsweep", [&] {
-                hipLaunchKernelGGL((rs_downsweep<K, true>), dim3(n_tiles), dim3(RS_T), 0, c->stream,
-                                   ka, va, kbuf, vbuf, n, shift, dm, cnt, n_tiles);
-            });
-        } else {
-            c->launch("radix_downsweep", [&] {
-                hipLaunchKernelGGL((rs_downsweep<K, false>), dim3(n_tiles), dim3(RS_T), 0,
-                                   c->stream, ka, (const uint32_t*)nullptr, kbuf,
-                                   (uint32_t*)nullptr, n, shift, dm, cnt, n_tiles);
-            });
-        }
+        c->launch("radix_downsweep", [&] {
+            if (vals) {
+                switch (db) {
+                case 8: hipLaunchKernelGGL((rs_downsweep<K, true, 8>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, va, kbuf, vbuf, n, shift, dm, cnt, n_tiles); break;
+                case 9: hipLaunchKernelGGL((rs_downsweep<K, true, 9>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, va, kbuf, vbuf, n, shift, dm, cnt, n_tiles); break;
+                case 10: hipLaunchKernelGGL((rs_downsweep<K, true, 10>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, va, kbuf, vbuf, n, shift, dm, cnt, n_tiles); break;
+                default: hipLaunchKernelGGL((rs_downsweep<K, true, 11>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, va, kbuf, vbuf, n, shift, dm, cnt, n_tiles); break;
+                }
+            } else {
+                const uint32_t* nv = nullptr;
+                uint32_t* nvo = nullptr;
+                switch (db) {
+                case 8: hipLaunchKernelGGL((rs_downsweep<K, false, 8>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, nv, kbuf, nvo, n, shift, dm, cnt, n_tiles); break;
+                case 9: hipLaunchKernelGGL((rs_downsweep<K, false, 9>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, nv, kbuf, nvo, n, shift, dm, cnt, n_tiles); break;
+                case 10: hipLaunchKernelGGL((rs_downsweep<K, false, 10>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, nv, kbuf, nvo, n, shift, dm, cnt, n_tiles); break;
+                default: hipLaunchKernelGGL((rs_downsweep<K, false, 11>), dim3(n_tiles), dim3(RS_T), 0, c->stream, ka, nv, kbuf, nvo, n, shift, dm, cnt, n_tiles); break;
+                }
+            }
+        });
         c->check_launch("rs_downsweep");
         if (src_k && shift == 0) {   // the source is never written: continue between keys and k2
             ka = kbuf;
@@ -643,6 +692,9 @@ void sort_export_u64(hga_ctx* c, uint64_t* keys, uint64_t n, int shift, uint32_t
         }
         st += h_hist[d];
     }
+}
+void radix_sort_u64_from(hga_ctx* c, const uint64_t* src_k, uint64_t* keys, uint64_t n, int bits, DevBuf& scratch) {
+    radix_sort_impl<uint64_t>(c, keys, nullptr, n, bits, scratch, src_k, nullptr);
 }
 void radix_sort_u32(hga_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int bits,
                     DevBuf& scratch) {

@@ -60,7 +60,8 @@ def test_connections_filters_and_pivots(gpu_ctx, golden_case):
 
 
 @pytest.mark.parametrize("env", [None, "HGA_CN_FORCE_BLOCK", "HGA_CN_FORCE_GLOBAL", "HGA_CN_TWO_STAGE", "HGA_CN_RCAP",
-                                 "HGA_CN_FULL_SORT", "HGA_CN_BIG_HITS=0", "HGA_CN_BIG_HITS=60"])
+                                 "HGA_CN_FULL_SORT", "HGA_CN_BIG_HITS=0", "HGA_CN_BIG_HITS=60",
+                                 "HGA_CN_SEGSORT", "HGA_CN_KEY64"])
 def test_connections_random_first_id(gpu_ctx, hga_mod, monkeypatch, env):
     """HGA_CN_BIG_HITS: pivots with more hits than that take cn_wave's workgroup tier first (0: all)."""
     if env:
