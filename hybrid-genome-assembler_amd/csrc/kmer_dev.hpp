@@ -288,6 +288,69 @@ __device__ __forceinline__ uint32_t wave_scan_max_dpp(uint32_t x) {
 // Value of lane L (uniform result, no LDS).
 __device__ __forceinline__ uint32_t wave_lane(uint32_t x, int L) { return (uint32_t)__builtin_amdgcn_readlane((int)x, L); }
 
+// Value of lane ^ X, on the VALU: DPP quad permutes (X = 1, 2), row shifts (4), a row rotate (8),
+// the gfx950 permlane swaps (16, 32).  A swap of a register with itself leaves one of its two
+// results equal to the lane's own value and the other the partner's, whichever half the
+// instruction moves, so the partner is the result that differs (equal values: either).
+template <int X>
+__device__ __forceinline__ uint32_t lane_xor32(uint32_t v) {
+    if constexpr (X == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
+    } else if constexpr (X == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
+    } else if constexpr (X == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xf, 0xf, true);   // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+        return (__lane_id() & 4) ? dn : up;
+    } else if constexpr (X == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, true);   // row_ror:8
+    } else if constexpr (X == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return r[0] == v ? r[1] : r[0];
+    } else {
+        static_assert(X == 32, "lane_xor32: X in {1, 2, 4, 8, 16, 32}");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return r[0] == v ? r[1] : r[0];
+    }
+}
+template <int X>
+__device__ __forceinline__ uint64_t lane_xor(uint64_t v) {
+    return ((uint64_t)lane_xor32<X>((uint32_t)(v >> 32)) << 32) | lane_xor32<X>((uint32_t)v);
+}
+template <int X>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) { return lane_xor32<X>(v); }
+
+// Ascending bitonic sort of 64 x R keys held blocked by one wave (key index lane * R + u).
+template <int R, int K, int J, class T>
+__device__ __forceinline__ void bitonic_step(T (&v)[R], uint32_t lane) {
+    if constexpr (J < R) {   // partners in the same lane
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if ((u & J) == 0) {
+                const bool asc = ((lane * R + u) & K) == 0;
+                const T a = v[u], b = v[u ^ J];
+                const bool sw = asc ? (a > b) : (a < b);
+                v[u] = sw ? b : a;
+                v[u ^ J] = sw ? a : b;
+            }
+        }
+    } else {   // partner lane ^ (J / R), same register
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const T o = lane_xor<J / R>(v[u]);
+            const uint32_t i = lane * R + u;
+            const bool keep_min = ((i & J) == 0) == ((i & K) == 0);
+            v[u] = keep_min ? min(v[u], o) : max(v[u], o);
+        }
+    }
+    if constexpr (J > 1) bitonic_step<R, K, J / 2>(v, lane);
+}
+template <int R, int K, class T>
+__device__ __forceinline__ void bitonic_stage(T (&v)[R], uint32_t lane) {
+    bitonic_step<R, K, K / 2>(v, lane);
+    if constexpr (K < 64 * R) bitonic_stage<R, K * 2>(v, lane);
+}
+
 // Wave / block scans (wave64).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll
