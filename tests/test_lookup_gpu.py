@@ -143,3 +143,25 @@ def test_lookup_many_dense_reads(gpu_ctx):
     want = oracle.construct_indices(bases, offsets, k, sdk, 1)
     for _ in range(3):
         assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 1), want)
+
+
+@pytest.mark.parametrize("n_share", [40, 300, 700, 1500])
+def test_lookup_shared_kmer_lists(gpu_ctx, n_share):
+    """kmer_component_index lists of many lengths: one k-mer shared by n_share reads."""
+    rng = random.Random(n_share)
+    k = 15
+    rnd = lambda n: "".join(rng.choice("ACGT") for _ in range(n))
+    shared = rnd(k)
+    reads = [(rnd(rng.randint(0, 30)) + shared + rnd(rng.randint(0, 30))).encode() for _ in range(n_share)]
+    rng.shuffle(reads)
+    pool = set()
+    for r in reads[:20]:
+        c, _ = oracle.kmer_windows(r, k)
+        pool.update(c.tolist())
+    sdk = np.array(sorted(pool), np.uint64)
+    bases = b"".join(reads)
+    offsets = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
+    exp = oracle.construct_indices(bases, offsets, k, sdk, 5)
+    assert int(np.diff(exp["kci_ptr"]).max()) >= n_share
+    assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 5), exp)
+
