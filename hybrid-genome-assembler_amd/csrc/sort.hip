@@ -512,14 +512,11 @@ void radix_sort_impl(hga_ctx* c, K* keys, uint32_t* vals, uint64_t n, int bits, 
     const uint32_t n_tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     const int npass = (bits + 7) / 8;
     const bool one = n < (uint64_t)hga_onesweep_max() && npass <= 8;
-    // classic passes: 8-bit digits, or up to rs_max_digit() bits when that saves passes (one key
-    // read and write per pass; wider digits cost a larger count table and scan)
+    // classic passes: 8-bit digits, or one pass of up to rs_max_digit() bits
+    // (9..10 bits: one wide pass instead of 8 + 1-2; wider keys keep 8-bit digits — 10-bit passes
+    // measured slower per key, C4's 27-bit export sort 2.67 -> 3.16 ms in three of them)
     int db = 8;
-    if (!one) {
-        const int mx = rs_max_digit();
-        const int npw = (bits + mx - 1) / mx;
-        if (npw < npass) db = std::max(8, (bits + npw - 1) / npw);
-    }
+    if (!one && bits > 8 && bits <= rs_max_digit()) db = bits;
     const uint64_t n_cnt = ((uint64_t)1 << db) * n_tiles;
     const size_t kb = ((n * sizeof(K) + 255) & ~255ull);
     const size_t vb = vals ? ((n * 4 + 255) & ~255ull) : 0;

@@ -139,3 +139,27 @@ def test_connections_long_kmer_lists(gpu_ctx):
     idx = lookup(gpu_ctx, bases, offsets, 17, sdk)
     for ms in (1, 4):
         same(gpu_ctx.connections(min_score=ms), oracle.connections(idx, min_score=ms))
+
+
+@pytest.mark.parametrize("env", [{}, {"HGA_ONESWEEP_MAX": "0"}, {"HGA_ONESWEEP_MAX": "0", "HGA_RS_MAX_DIGIT": "8"}])
+def test_connections_wide_scores(gpu_ctx, hga_mod, monkeypatch, env):
+    """Scores of several hundred (9-10 score bits): with HGA_ONESWEEP_MAX=0 the score order takes the
+    classic radix passes, one wide-digit pass (or 8 + 2 bits with HGA_RS_MAX_DIGIT=8)."""
+    for kv in env.items():
+        monkeypatch.setenv(*kv)
+    gnm = hga_mod.gen_genome(6_000, 31)
+    rng = np.random.default_rng(5)
+    reads = []
+    for _ in range(40):
+        L = int(rng.integers(1200, 2000))
+        s = int(rng.integers(0, 6_000 - L))
+        reads.append(gnm[s:s + L])
+    bases = b"".join(reads)
+    offsets = np.cumsum([0] + [len(x) for x in reads]).astype(np.uint64)
+    c, _ = oracle.kmer_windows(gnm, 15)
+    sdk = np.unique(c)[::2]
+    idx = lookup(gpu_ctx, bases, offsets, 15, sdk)
+    got = gpu_ctx.connections(min_score=1)
+    exp = oracle.connections(idx, min_score=1)
+    assert 256 <= int(exp[2].max()) < 1024
+    same(got, exp)
