@@ -226,7 +226,8 @@ __device__ __forceinline__ bool cn_insert64(uint64_t* t, uint32_t mask, uint32_t
 // final order (score desc, pivot, candidate) is one stable pass over the score bits of the
 // pivot-ordered runs.  Sort keys are candidate << 32 | score (candidates < 2^32 - 1), ~0 pads.
 constexpr uint64_t CN_PAD = ~0ull;
-constexpr uint32_t CN_SORT_W = 512;   // runs up to this long are sorted by cn_runs_keys (one wave, 8 keys a lane)
+constexpr uint32_t CN_SORT_W = 1024;   // runs up to this long are sorted by cn_runs_keys (one wave, 16 keys a lane)
+constexpr uint32_t CN_SORT_N = 512;    // ... up to this long by its common launch (8 keys a lane)
 __device__ __forceinline__ uint64_t cn_key(uint64_t ent) { return (ent << 32) | (ent >> 32); }
 
 // Bitonic sort of tab[0, n) in LDS by the whole workgroup (n a power of two, <= CN_CAP).
@@ -405,10 +406,12 @@ __global__ void __launch_bounds__(CN_T) cn_local(CnIn in, CnOut out, const uint3
 // ---- cn_wave: the first tier — one wave per pivot, pivots taken from a work counter.
 // Every wave owns a CNW_CAP-entry LDS table (u64 entries as in cn_local) and its own chunk /
 // owner-map state, so a workgroup walks four pivots at once without workgroup barriers (a
-// wave's LDS accesses are ordered) and a CU keeps ~28 pivots' dependent load chains in flight.
-// A pivot whose distinct candidates pass 3/4 of the table goes to the cn_local list.
+// wave's LDS accesses are ordered) and a CU keeps 16 pivots' dependent load chains in flight.
+// A pivot whose distinct candidates pass 3/4 of the table goes to the cn_local list.  1024 entries
+// (4 workgroups a CU) against 512 (7 a CU): on C3 almost no pivot overflows to cn_local any more
+// (cn_wave + cn_local 1.50 -> 1.41 ms, profiles/r04cn_variants_3.txt).
 #ifndef HGA_CNW_CAP
-#define HGA_CNW_CAP 512
+#define HGA_CNW_CAP 1024
 #endif
 #ifndef HGA_CNW_WAVES
 #define HGA_CNW_WAVES 4
@@ -421,7 +424,7 @@ constexpr int CNW_WAVES = HGA_CNW_WAVES;
 #define HGA_CNW_GRAB 2
 #endif
 #ifndef HGA_CNW_MINW
-#define HGA_CNW_MINW 7
+#define HGA_CNW_MINW 4
 #endif
 #ifndef HGA_CN_BIG_HITS
 #define HGA_CN_BIG_HITS 768
@@ -763,23 +766,30 @@ __device__ __forceinline__ void cn_run_sort_put(uint64_t p, uint64_t o, uint64_t
             key[o + i] = (((p << ib) | (uint64_t)(v[u] >> sh)) << sb) | (uint64_t)(mxs - (uint32_t)(v[u] & smask));
     }
 }
-template <class T>
+template <class T, bool WIDE>
 __device__ __forceinline__ void cn_run_sort_any(uint64_t p, uint64_t o, uint64_t m, uint64_t g, uint32_t lane, int ib,
                                                 int sb, uint32_t mxs, int sbits, const uint32_t* __restrict__ y,
                                                 const uint32_t* __restrict__ s, uint64_t* __restrict__ key) {
-    if (m <= 64) cn_run_sort_put<1, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
-    else if (m <= 128) cn_run_sort_put<2, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
-    else if (m <= 256) cn_run_sort_put<4, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
-    else cn_run_sort_put<8, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+    if constexpr (WIDE) {
+        cn_run_sort_put<16, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+    } else {
+        if (m <= 64) cn_run_sort_put<1, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+        else if (m <= 128) cn_run_sort_put<2, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+        else if (m <= 256) cn_run_sort_put<4, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+        else cn_run_sort_put<8, T>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+    }
 }
 #ifndef HGA_CN_RK_PPW
 #define HGA_CN_RK_PPW 4
 #endif
 constexpr int CN_RK_PPW = HGA_CN_RK_PPW;   // pivots per wave (their offsets loaded by one coalesced load)
+// Runs of up to CN_SORT_N pairs sorted here, runs over CN_SORT_W copied (they come sorted from the
+// workgroup tier); the pivots of the runs in between are listed for cn_runs_keys_wide.
 __global__ void __launch_bounds__(256) cn_runs_keys(const uint64_t* __restrict__ pst, const uint64_t* __restrict__ poff,
                                                     uint64_t nr, int ib, int sb, uint32_t mxs, int sbits,
                                                     const uint32_t* __restrict__ y, const uint32_t* __restrict__ s,
-                                                    uint64_t* __restrict__ key) {
+                                                    uint64_t* __restrict__ key, uint32_t* __restrict__ wide,
+                                                    unsigned long long* __restrict__ n_wide) {
     const uint64_t p0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * CN_RK_PPW;
     if (p0 >= nr) return;
     const uint32_t lane = threadIdx.x & 63;
@@ -795,12 +805,30 @@ __global__ void __launch_bounds__(256) cn_runs_keys(const uint64_t* __restrict__
         if (p >= nr) break;
         if (!m) continue;
         const uint64_t o = __shfl(lo, j, 64), g = __shfl(lg, j, 64);
-        if (m <= CN_SORT_W) {
-            if (sbits) cn_run_sort_any<uint32_t>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
-            else cn_run_sort_any<uint64_t>(p, o, m, g, lane, ib, sb, mxs, 0, y, s, key);
-        } else
+        if (m <= CN_SORT_N) {
+            if (sbits) cn_run_sort_any<uint32_t, false>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+            else cn_run_sort_any<uint64_t, false>(p, o, m, g, lane, ib, sb, mxs, 0, y, s, key);
+        } else if (m <= CN_SORT_W) {
+            if (lane == 0) wide[atomicAdd(n_wide, 1ull)] = (uint32_t)p;
+        } else {
             for (uint64_t i = lane; i < m; i += 64)
                 key[o + i] = ((((uint64_t)p << ib) | y[g + i]) << sb) | (uint64_t)(mxs - s[g + i]);
+        }
+    }
+}
+// The listed runs (CN_SORT_N + 1 .. CN_SORT_W pairs, 16 keys a lane): a separate kernel so that its
+// registers do not cost the common runs occupancy; a fixed grid reading the count on the device.
+__global__ void __launch_bounds__(256) cn_runs_keys_wide(const uint64_t* __restrict__ pst, const uint64_t* __restrict__ poff,
+                                                         int ib, int sb, uint32_t mxs, int sbits,
+                                                         const uint32_t* __restrict__ y, const uint32_t* __restrict__ s,
+                                                         uint64_t* __restrict__ key, const uint32_t* __restrict__ wide,
+                                                         const unsigned long long* __restrict__ n_wide) {
+    const unsigned long long n = *n_wide;
+    const uint32_t lane = threadIdx.x & 63;
+    for (unsigned long long q = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < n; q += (uint64_t)gridDim.x * 4) {
+        const uint64_t p = wide[q], o = poff[p], m = poff[p + 1] - o, g = pst[p];
+        if (sbits) cn_run_sort_any<uint32_t, true>(p, o, m, g, lane, ib, sb, mxs, sbits, y, s, key);
+        else cn_run_sort_any<uint64_t, true>(p, o, m, g, lane, ib, sb, mxs, 0, y, s, key);
     }
 }
 // key = (pivot << ib | candidate) << sb | (max - score): a stable sort by the low sb bits of keys
@@ -1009,10 +1037,14 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
         if (!h[3] && !std::getenv("HGA_CN_SEGSORT")) {   // no HBM-tier run: sorted in cn_runs_keys
             // u32 sort keys (candidate << sbits | score) when they fit, u64 otherwise
             const int sbits = (bits_for(mxs) + ib <= 32 && !std::getenv("HGA_CN_KEY64")) ? std::max(1, bits_for(mxs)) : 0;
+            uint32_t* wide = static_cast<uint32_t*>(S.big.ensure(std::max<uint64_t>(nr, P) * 4));   // the long-pivot list is done
+            HGA_HIP(hipMemsetAsync(ctr, 0, 8, c->stream));
             uint64_t* key = static_cast<uint64_t*>(S.key.ensure(n * 8));
             c->launch("cn_sort", [&] {
-                hipLaunchKernelGGL(cn_runs_keys, dim3(cn_blocks(nr, 4 * CN_RK_PPW)), dim3(256), 0, c->stream, pst, pcnt, nr, ib,
-                                   sb, mxs, sbits, S.y.as<uint32_t>(), S.s.as<uint32_t>(), key);
+                hipLaunchKernelGGL(cn_runs_keys, dim3(cn_blocks(nr, 4 * CN_RK_PPW)), dim3(256), 0, c->stream, pst, pcnt, nr,
+                                   ib, sb, mxs, sbits, S.y.as<uint32_t>(), S.s.as<uint32_t>(), key, wide, ctr);
+                hipLaunchKernelGGL(cn_runs_keys_wide, dim3((unsigned)c->num_cu), dim3(256), 0, c->stream, pst, pcnt, ib, sb,
+                                   mxs, sbits, S.y.as<uint32_t>(), S.s.as<uint32_t>(), key, wide, ctr);
             });
             c->check_launch("cn_runs_keys");
             uint64_t* sorted = static_cast<uint64_t*>(S.sk2.ensure(n * 8));

@@ -163,3 +163,22 @@ def test_connections_wide_scores(gpu_ctx, hga_mod, monkeypatch, env):
     exp = oracle.connections(idx, min_score=1)
     assert 256 <= int(exp[2].max()) < 1024
     same(got, exp)
+
+
+@pytest.mark.parametrize("n_short", [300, 800])
+def test_connections_wide_runs(gpu_ctx, hga_mod, n_short):
+    """One long read overlapped by n_short short reads: its run (300 / 800 pairs) is sorted by the
+    common run kernel or listed for the 16-keys-a-lane one (512 < run <= 1024)."""
+    gnm = hga_mod.gen_genome(30_000, 23)
+    rng = np.random.default_rng(n_short)
+    reads = [gnm]
+    for s in rng.integers(0, 30_000 - 150, n_short):
+        reads.append(gnm[s:s + 150])
+    bases = b"".join(reads)
+    offsets = np.cumsum([0] + [len(x) for x in reads]).astype(np.uint64)
+    c, _ = oracle.kmer_windows(gnm, 15)
+    sdk = np.unique(c)[::9]
+    idx = lookup(gpu_ctx, bases, offsets, 15, sdk)
+    exp = oracle.connections(idx, min_score=1)
+    assert int((exp[0] == 1).sum()) > 0.9 * n_short
+    same(gpu_ctx.connections(min_score=1), exp)
