@@ -610,10 +610,22 @@ __global__ void cn_big_list(const uint64_t* __restrict__ hit_ptr, const uint32_t
                             uint32_t min_kmers, uint64_t big_hits, uint32_t* __restrict__ big,
                             unsigned long long* __restrict__ n_big) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n_piv) return;
-    const uint32_t p = piv ? piv[q] : (uint32_t)q;
-    const uint64_t h = hit_ptr[p + 1] - hit_ptr[p];
-    if (h > big_hits && h >= min_kmers) big[atomicAdd(n_big, 1ull)] = p;
+    uint32_t p = 0;
+    bool take = false;
+    if (q < n_piv) {
+        p = piv ? piv[q] : (uint32_t)q;
+        const uint64_t h = hit_ptr[p + 1] - hit_ptr[p];
+        take = h > big_hits && h >= min_kmers;
+    }
+    // one counter atomic per wave (same-address device atomics serialise)
+    const uint64_t m = __ballot(take);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    unsigned long long base = 0;
+    if (lane == first) base = atomicAdd(n_big, (unsigned long long)__popcll(m));
+    base = __shfl(base, (int)first, 64);
+    if (take) big[base + (uint64_t)__popcll(m & ((1ull << lane) - 1))] = p;
 }
 
 // Upper bound of a pivot's distinct candidates: its (id, candidate) pair count.
