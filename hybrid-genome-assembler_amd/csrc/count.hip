@@ -36,9 +36,6 @@
 #ifndef HGA_B1_BRANCHFREE
 #define HGA_B1_BRANCHFREE 0   // 1: kc_bin1 ranks every window (invalid ones into per-lane dummy counters)
 #endif
-#ifndef HGA_XB1_NOFHIST
-#define HGA_XB1_NOFHIST 0   // timing experiment only (tools/build_variants.sh): 1 = no fine histogram (wrong results)
-#endif
 
 namespace hga {
 namespace {
@@ -283,16 +280,14 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
             if (HGA_B1_BRANCHFREE) {   // invalid windows count into this lane's dummy counters
                 const bool ok = (wm >> j) & 1u;
                 const uint32_t r = atomicAdd(&cnt1[ok ? dd[j] : NB1_MAX + (uint32_t)(tid & 63)], 1u);
-                if (!HGA_XB1_NOFHIST)
-                    atomicAdd(&fhist[ok ? (K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp))
-                                        : MAX_NB + (uint32_t)(tid & 63)], 1u);
+                atomicAdd(&fhist[ok ? (K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp))
+                                    : MAX_NB + (uint32_t)(tid & 63)], 1u);
                 rk[j] = ok ? r : ~0u;
             } else {
                 rk[j] = ~0u;   // invalid window: staged into this lane's dummy slot (no mask kept live)
                 if ((wm >> j) & 1u) {
                     rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
-                    if (!HGA_XB1_NOFHIST)
-                        atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp)], 1u);
+                    atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp)], 1u);
                 }
             }
         }
