@@ -344,15 +344,15 @@ __device__ bool cn_block_pivot(const CnIn& in, const CnOut& out, uint32_t p, uin
     }
     if (!ok) return false;
     // emit: survivors compacted to tab[0, total), sorted by candidate, one global atomic per workgroup
-    const uint32_t per = size / CN_T ? size / CN_T : 1;
-    const uint32_t s0 = t * per;
+    // slots read thread-strided (slot u * CN_T + t): consecutive lanes on consecutive entries, no
+    // bank conflicts (a thread-contiguous block of 8 entries put 16 lanes on one bank)
     uint64_t ent[CN_CAP / CN_T];
     uint32_t cnt = 0, mx = 0;
 #pragma unroll
     for (uint32_t u = 0; u < CN_CAP / CN_T; ++u) {
         ent[u] = CN_PAD;
-        if (u < per && s0 + u < size) {
-            const uint64_t v = L.tab[s0 + u];
+        if (u * CN_T + t < size) {
+            const uint64_t v = L.tab[u * CN_T + t];
             const uint32_t c = (uint32_t)(v >> 32);
             if ((uint32_t)v != CN_EMPTY && c >= in.min_score) {
                 ent[u] = cn_key(v);
@@ -569,8 +569,8 @@ __global__ void __launch_bounds__(64 * CNW_WAVES, HGA_CNW_MINW) cn_wave(CnIn in,
         uint32_t cnt = 0, mx = 0;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            ent[u] = W.tab[lane * PER + u];
-            W.tab[lane * PER + u] = CN_EMPTY64;
+            ent[u] = W.tab[u * 64 + lane];   // lane-strided: no bank conflicts
+            W.tab[u * 64 + lane] = CN_EMPTY64;
             const uint32_t c = (uint32_t)(ent[u] >> 32);
             if ((uint32_t)ent[u] != CN_EMPTY && c >= in.min_score) {
                 ++cnt;
