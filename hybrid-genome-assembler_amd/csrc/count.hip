@@ -1310,13 +1310,16 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
             __syncthreads();
             continue;
         }
-        // emit: each thread owns ES consecutive slots; kept rows are compacted in place
+        // emit: each thread owns ES slots, four consecutive ones per 16-B read, the reads thread-strided
+        // (quad (j / 4) * NT_P + tid: lanes on consecutive 16-B groups, no bank conflicts; a
+        // thread-contiguous block of 16 slots put every fourth lane on the same banks); kept rows are
+        // compacted in place (rows leave a bucket in any order)
         constexpr int ES = T_S / NT_P;
         uint32_t kk[ES], cc[ES];
 #pragma unroll
         for (int j = 0; j < ES; j += 4) {
-            const uint4 k4 = reinterpret_cast<const uint4*>(tkey)[(tid * ES + j) / 4];
-            const uint4 c4 = reinterpret_cast<const uint4*>(tcnt)[(tid * ES + j) / 4];
+            const uint4 k4 = reinterpret_cast<const uint4*>(tkey)[(j / 4) * NT_P + tid];
+            const uint4 c4 = reinterpret_cast<const uint4*>(tcnt)[(j / 4) * NT_P + tid];
             kk[j] = k4.x; kk[j + 1] = k4.y; kk[j + 2] = k4.z; kk[j + 3] = k4.w;
             cc[j] = c4.x; cc[j + 1] = c4.y; cc[j + 2] = c4.z; cc[j + 3] = c4.w;
         }
