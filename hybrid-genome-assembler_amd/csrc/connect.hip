@@ -427,7 +427,7 @@ constexpr int CNW_WAVES = HGA_CNW_WAVES;
 #define HGA_CNW_MINW 4
 #endif
 #ifndef HGA_CN_BIG_HITS
-#define HGA_CN_BIG_HITS 768
+#define HGA_CN_BIG_HITS 896
 #endif
 constexpr uint32_t CNW_GRAB = HGA_CNW_GRAB;   // pivots per work-counter atomic
 
