@@ -365,10 +365,57 @@ def hll_leg(ctx2, D, n_bases, bases, offsets, args):
     return out
 
 
-def lookup_parse_leg(ga, gb, n_reads, lookup_s, bases, offsets, threads):
+def write_kmer_text(path, codes, k):
+    """The export file format of jf_occurrences (one k-mer string a line, JellyfishOccurrenceReader.cpp:
+    110-135): 2-bit codes, first base in the top bits, A0 C1 G2 T3."""
+    codes = np.asarray(codes, dtype=np.uint64)
+    shifts = (2 * np.arange(k - 1, -1, -1)).astype(np.uint64)
+    txt = np.empty((len(codes), k + 1), dtype=np.uint8)
+    txt[:, :k] = np.frombuffer(b"ACGT", dtype=np.uint8)[((codes[:, None] >> shifts[None, :]) & np.uint64(3)).astype(np.intp)]
+    txt[:, k] = ord("\n")
+    txt.tofile(path)
+
+
+def categorization_pipeline_leg(paths, sdk, threads, d):
+    """Verdict r04 item 7: the drop-in `categorization` CLI end to end on the C3 reads (Nanosim-like FASTA,
+    both haplotypes, -d) against the C2 [10,25] export as a k-mer text file: its own per-stage "took" lines
+    (src/common/Utils.h:17-35 timeMeasure: index construction and the first connection pass on the GPU,
+    union-find, merging, tails, spectral clustering, enrichment on the host), next to the reference's
+    published ENP75 run on an i5-8250U (writing/Evaluation.txt:75-82) as context only."""
+    import re
+    import subprocess
+    cli = os.path.join(ROOT, "hybrid-genome-assembler_amd", "bin", "categorization")
+    if not os.path.exists(cli):
+        return None
+    kpath = os.path.join(d, f"{K}-mers_{LOWER}_{UPPER}_100%.txt")
+    write_kmer_text(kpath, sdk, K)
+    t0 = time.perf_counter()
+    r = subprocess.run([cli, *paths, "-k", kpath, "-d", "-o", os.path.join(d, "clusters"), "-t", str(threads)],
+                       capture_output=True, text=True, cwd=d, timeout=900)
+    wall = time.perf_counter() - t0
+    stages = {}
+    for line in r.stdout.splitlines():
+        m = re.match(r"(.+) took (\d+)ms$", line.strip())
+        if m:
+            stages[m.group(1)] = stages.get(m.group(1), 0) + int(m.group(2))
+    exported = re.search(r"Exported (\d+) components", r.stdout)
+    return {"argv": f"categorization mg1655_nanosim.fasta uti89_nanosim.fasta -k {os.path.basename(kpath)} -d -t {threads}",
+            "rc": r.returncode, "wall_s": round(wall, 3), "stages_ms": stages,
+            "components": int(exported.group(1)) if exported else None,
+            "stderr_tail": r.stderr[-300:] if r.returncode else None,
+            "published_reference_ENP75_ms": {"Index construction": 49225, "All connections": 4353,
+                                             "Merging into scaffold c.": 8751, "Tail connections": 7281,
+                                             "Spectral clustering": 183, "Merging scaffold c.": 1914,
+                                             "Enrichment connections": 116, "Merging into core c.": 2634,
+                                             "note": "writing/Evaluation.txt:75-82, Intel Core i5-8250U, the "
+                                                     "reference's real ENP75 reads: context, not the same input"}}
+
+
+def lookup_parse_leg(ga, gb, n_reads, lookup_s, bases, offsets, threads, sdk=None):
     """BASELINE.md §3 "reads/s categorized with parsing": the C3 long reads written as Nanosim-like
     FASTA (same generators and seeds as make_c3), read back by categorization's reader
-    (load_records: SequenceRecordIterator, multi-threaded) and the lookup time added."""
+    (load_records: SequenceRecordIterator, multi-threaded) and the lookup time added.  With `sdk`, the
+    whole categorization CLI is then run on the same files (categorization_pipeline_leg)."""
     import shutil
     import tempfile
     d = tempfile.mkdtemp(prefix="hga_c3_")
@@ -385,10 +432,14 @@ def lookup_parse_leg(ga, gb, n_reads, lookup_s, bases, offsets, threads):
         parse_s = time.perf_counter() - t0
         hga.set_host_threads(0)
         same = rec["bases"] == bases and np.array_equal(rec["offsets"], offsets)
-        return {"files": "C3 reads as Nanosim-like FASTA", "bytes": size, "reader_threads": threads,
-                "parse_s": round(parse_s, 4), "same_reads_as_resident": bool(same),
-                "reads_per_s": round(n_reads / (parse_s + lookup_s), 1),
-                "note": "host FASTA parse (through the ctypes mirror) + one hga_lookup_run; upload not included"}
+        del rec
+        out = {"files": "C3 reads as Nanosim-like FASTA", "bytes": size, "reader_threads": threads,
+               "parse_s": round(parse_s, 4), "same_reads_as_resident": bool(same),
+               "reads_per_s": round(n_reads / (parse_s + lookup_s), 1),
+               "note": "host FASTA parse (through the ctypes mirror) + one hga_lookup_run; upload not included"}
+        if sdk is not None:
+            out["pipeline"] = categorization_pipeline_leg(paths, sdk, threads, d)
+        return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -702,8 +753,10 @@ def main():
         result["categorize"]["ms_note"] = ("ms = hga_lookup_run: the per-base encode of the resident ASCII reads "
                                            "(lk_pack) + lookup + CSR outputs; the upload is hga_lookup_set_reads")
         if D.world == 1 and not args.no_ingest:
-            result["categorize"]["with_parsing"] = lookup_parse_leg(ga, gb, s.n_reads, dtl, bases, offsets,
-                                                                    args.cpu_threads)
+            wp = lookup_parse_leg(ga, gb, s.n_reads, dtl, bases, offsets, args.cpu_threads, sdk)
+            if wp.get("pipeline") is not None:
+                result["categorize"]["pipeline"] = wp.pop("pipeline")
+            result["categorize"]["with_parsing"] = wp
         result["categorize"]["connections"] = connections_leg(ctx2, D, reps, args)
         result["categorize"]["hll_auto_k"] = hll_leg(ctx2, D, len(bases), bases, offsets, args)
         ctx2.close()

@@ -126,6 +126,13 @@ __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// dst[i] through a wave-uniform base and a 32-bit lane byte offset (one global_store with an SGPR
+// base, no 64-bit address arithmetic per element); i * sizeof(T) < 2^32.
+template <class T>
+__device__ __forceinline__ void store_at(T* dst, uint32_t i, T v) {
+    *reinterpret_cast<T*>(reinterpret_cast<char*>(dst) + (uint32_t)(i * (uint32_t)sizeof(T))) = v;
+}
+
 // Level-1 blocks: every workgroup takes BLK-element blocks per region from one pool with a
 // single atomic (and a new one only when a block fills), so a tile's region runs are
 // written without any global atomic.  block table entry: start, used, file<<8 | region.
@@ -287,7 +294,9 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
                 rk[j] = ~0u;   // invalid window: staged into this lane's dummy slot (no mask kept live)
                 if ((wm >> j) & 1u) {
                     rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
+#ifndef HGA_B1_NOFHIST
                     atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp)], 1u);
+#endif
                 }
             }
         }
@@ -295,7 +304,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
         lds_barrier();
         if (tid < 64) {   // one wave: scan the <= 64 region counts, place them in the blocks
             const uint32_t c = tid < (int)nb1 ? cnt1[tid] : 0u;
-            const uint32_t inc = wave_incl_scan(c, tid);
+            const uint32_t inc = wave_scan_add_dpp(c);   // wave 0, all lanes active
             const uint32_t room = tid < (int)nb1 ? BLK - bfill[tid] : 0u;
             const bool spill = tid < (int)nb1 && c > room;   // the run spills into a fresh block
             if (tid < (int)nb1) {
@@ -353,7 +362,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
             if (ba < pool_cap) {   // a block past the pool (table exhausted, error bit set) drops its writes
                 E1* __restrict__ dst = out1 + ba;
                 const uint32_t lim = (uint32_t)(pool_cap - ba < na ? pool_cap - ba : na);
-                for (uint32_t jj = lane; jj < lim; jj += 64) dst[jj] = stage[o + jj];
+                for (uint32_t jj = lane; jj < lim; jj += 64) store_at(dst, jj, stage[o + jj]);
             }
             if (len > na) {   // the part past a full block, into the fresh one
                 const uint64_t bb = readfirstlane64(base_b[d]);
@@ -361,7 +370,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
                     E1* __restrict__ dst = out1 + bb;
                     const uint32_t n2 = len - na;
                     const uint32_t lim = (uint32_t)(pool_cap - bb < n2 ? pool_cap - bb : n2);
-                    for (uint32_t jj = lane; jj < lim; jj += 64) dst[jj] = stage[o + na + jj];
+                    for (uint32_t jj = lane; jj < lim; jj += 64) store_at(dst, jj, stage[o + na + jj]);
                 }
             }
         }
@@ -588,9 +597,9 @@ __global__ void __launch_bounds__(NT_R_MAX) kc_rebin(const E1* __restrict__ in1,
     __shared__ uint32_t s_w0;
     __shared__ E stage[CH_R];
     const int tid = threadIdx.x;
-    const uint64_t blk = blockIdx.x;
     const uint32_t nb2 = kp.nb2;
     const uint64_t n_first = (uint64_t)W * kp.nb1;
+    const uint64_t blk = blockIdx.x;
     // first blocks: everything is known from the index, so the element, size and offset loads
     // all go out together; spill blocks (rare) look themselves up
     if (blk >= n_first && blk >= gstat[3]) return;
@@ -628,7 +637,7 @@ __global__ void __launch_bounds__(NT_R_MAX) kc_rebin(const E1* __restrict__ in1,
     uint32_t c2 = 0, inc2 = 0;
     if (tid < NB2_MAX) {   // two waves scan the <= 128 digit counts
         c2 = tid < (int)nb2 ? cnt2[tid] : 0u;
-        inc2 = wave_incl_scan(c2, tid & 63);
+        inc2 = wave_scan_add_dpp(c2);   // whole waves (NB2_MAX is a multiple of 64)
         if (tid == 63) s_w0 = inc2;
     }
     __syncthreads();

@@ -74,14 +74,30 @@ __device__ __forceinline__ void ref_codes(uint32_t b, uint32_t& fc, uint32_t& rc
     rcc = ok ? 3u - c : 0u;
 }
 
+// Load through the global address space.  A pointer the compiler cannot prove global (one read
+// from a struct in memory) is accessed with flat instructions, which count against lgkmcnt as
+// well as vmcnt: every `s_waitcnt lgkmcnt(0)` of an LDS phase would then also drain such a
+// load, so a prefetch would not stay in flight across LDS barriers.
+// (A native vector type: HIP's uint4 is a struct whose copy goes through a generic pointer.)
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+#ifndef HGA_GLOBAL_LOADS
+#define HGA_GLOBAL_LOADS 1   // 0: generic-pointer loads (timing comparison only)
+#endif
+__device__ __forceinline__ uint4 load_global16(const void* p) {
+    if (!HGA_GLOBAL_LOADS) return *reinterpret_cast<const uint4*>(p);
+    const u32x4_t v = *(const __attribute__((address_space(1))) u32x4_t*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // 16 bytes starting at byte index `base` (a multiple of 16) of a stream of length n;
 // bytes outside [0, n) read as 0 (not a base in either semantics).
 __device__ __forceinline__ uint4 load16(const uint8_t* s, int64_t base, uint64_t n) {
-    if (base >= 0 && (uint64_t)base + 16 <= n) return *reinterpret_cast<const uint4*>(s + base);
+    if (base >= 0 && (uint64_t)base + 16 <= n) return load_global16(s + base);
     uint32_t w[4] = {0, 0, 0, 0};
     for (int j = 0; j < 16; ++j) {
         int64_t i = base + j;
-        if (i >= 0 && (uint64_t)i < n) w[j >> 2] |= (uint32_t)s[i] << (8 * (j & 3));
+        if (i >= 0 && (uint64_t)i < n)
+            w[j >> 2] |= (uint32_t)*(const __attribute__((address_space(1))) uint8_t*)(s + i) << (8 * (j & 3));
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
 }

@@ -575,10 +575,16 @@ std::vector<KmerID> ClusteringEngine::accumulate_kmer_ids(const std::vector<Comp
     return all;
 }
 
-// merge_components (:349-422).
+// merge_components (:349-422).  Same statements, flat data structures: a survivor's KmerID union
+// is a mark pass over the dense KmerID range when the members hold many ids (a sort of the
+// concatenation otherwise), and the removal lists are a counting sort of (KmerID, component) pairs
+// by KmerID instead of an ordered map of vectors — on C3, where one component absorbs most reads
+// (~20 M pairs), the map took 17.8 s.  The kmer_component_index update runs over the host threads.
 std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<ComponentList>& components) {
     std::vector<ComponentID> merged_ids;
-    std::map<KmerID, std::vector<ComponentID>> for_removal;
+    const size_t nk = kci_.size();
+    std::vector<uint64_t> pairs;   // KmerID << 32 | component, in the reference's insertion order
+    std::vector<uint8_t> mark;
     for (const ComponentList& ids : components) {
         if (ids.empty()) continue;   // (an empty spectral cluster would dereference ids[0] there)
         if (ids.size() == 1) {
@@ -587,43 +593,86 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
         }
         std::set<int32_t> cats;
         std::vector<uint32_t> contained;
+        size_t total = 0;
         for (ComponentID id : ids) {
             Component& c = index_.at(id);
             contained.insert(contained.end(), c.reads.begin(), c.reads.end());
             c.reads.clear();
             cats.insert(c.categories.begin(), c.categories.end());
+            total += c.kmers.size();
         }
-        std::vector<KmerID> acc = accumulate_kmer_ids(ids);
+        std::vector<KmerID> acc;
+        if (total > nk / 16 + 64) {   // accumulate_kmer_ids as a mark pass (ids < nk)
+            if (mark.empty()) mark.assign(nk, 0);
+            for (ComponentID id : ids)
+                for (KmerID kid : index_.at(id).kmers) mark[kid] = 1;
+            for (size_t kid = 0; kid < nk; ++kid)
+                if (mark[kid]) {
+                    acc.push_back((KmerID)kid);
+                    mark[kid] = 0;
+                }
+        } else {
+            acc = accumulate_kmer_ids(ids);
+        }
         Component& survivor = index_.at(ids[0]);
         survivor.kmers = std::move(acc);
         survivor.categories = cats;
         survivor.reads = contained;
         merged_ids.push_back(ids[0]);
         for (ComponentID id : ids)
-            for (KmerID kid : index_.at(id).kmers) for_removal[kid].push_back(id);
+            for (KmerID kid : index_.at(id).kmers) pairs.push_back((uint64_t)kid << 32 | id);
         pristine_ = false;
     }
+    if (pairs.empty()) return merged_ids;
+    // removal lists: counting sort of the pairs by KmerID
+    std::vector<uint64_t> start(nk + 1, 0);
+    for (uint64_t p : pairs) ++start[(p >> 32) + 1];
+    for (size_t k = 0; k < nk; ++k) start[k + 1] += start[k];
+    std::vector<ComponentID> rem(pairs.size());
+    {
+        std::vector<uint64_t> cur(start.begin(), start.end() - 1);
+        for (uint64_t p : pairs) rem[cur[p >> 32]++] = (ComponentID)p;
+    }
+    pairs.clear();
+    pairs.shrink_to_fit();
     // kmer_component_index update (:395-419), including its early stop: once the removal list
     // is exhausted the rest of the kmer's list is not copied
-    for (auto& kv : for_removal) {
-        std::vector<ComponentID>& removal = kv.second;
-        std::sort(removal.begin(), removal.end());
-        std::vector<ComponentID>& list = kci_[kv.first];
+    auto update = [&](size_t k0, size_t k1) {
         std::vector<ComponentID> updated;
-        size_t i = 0, j = 0;
-        while (i < removal.size() && j < list.size()) {
-            if (removal[i] < list[j]) {
-                ++i;
-            } else if (list[j] < removal[i]) {
-                updated.push_back(list[j]);
-                ++j;
-            } else {
-                ++i;
-                ++j;
+        for (size_t kid = k0; kid < k1; ++kid) {
+            if (start[kid] == start[kid + 1]) continue;
+            ComponentID* rb = rem.data() + start[kid];
+            ComponentID* re = rem.data() + start[kid + 1];
+            std::sort(rb, re);
+            std::vector<ComponentID>& list = kci_[kid];
+            updated.clear();
+            size_t j = 0;
+            for (ComponentID* r = rb; r < re && j < list.size();) {
+                if (*r < list[j]) {
+                    ++r;
+                } else if (list[j] < *r) {
+                    updated.push_back(list[j]);
+                    ++j;
+                } else {
+                    ++r;
+                    ++j;
+                }
             }
+            list.assign(updated.begin(), updated.end());
         }
-        list = std::move(updated);
+    };
+    const int T = std::max(1, std::min<int>(host_threads(), (int)(rem.size() >> 16) + 1));
+    std::vector<std::thread> th;
+    size_t k0 = 0;
+    for (int t = 0; t < T; ++t) {   // kid ranges of about equal pair counts
+        const uint64_t want = (uint64_t)rem.size() * (uint64_t)(t + 1) / (uint64_t)T;
+        const size_t k1 = t + 1 == T ? nk : (size_t)(std::upper_bound(start.begin(), start.end(), want) - start.begin()) - 1;
+        const size_t e = std::max(k0, std::min(k1, nk));
+        if (t + 1 == T) update(k0, nk);
+        else th.emplace_back(update, k0, e);
+        k0 = e;
     }
+    for (auto& x : th) x.join();
     return merged_ids;
 }
 

@@ -32,8 +32,12 @@ print(json.dumps({"ms": round(dt * 1e3, 3), "sel": n, "hist_sum": hs,
                   "k": {x: round(ctx.profile_get(x)[0] / 10, 4) for x in names}}))
 ''' % (ROOT, os.path.join(ROOT, "hybrid-genome-assembler_amd"))
 
-for so in sys.argv[1:]:
+for arg in sys.argv[1:]:   # path.so or path.so@ENV=V,ENV2=V
+    so, _, envs = arg.partition("@")
     env = dict(os.environ, HGA_LIB=so)
+    for kv in filter(None, envs.split(",")):
+        k, _, v = kv.partition("=")
+        env[k] = v
     out = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, timeout=300)
     line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else out.stderr[-500:]
-    print(os.path.basename(so), line, flush=True)
+    print(os.path.basename(so) + ("@" + envs if envs else ""), line, flush=True)
