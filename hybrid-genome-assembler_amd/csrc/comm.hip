@@ -308,38 +308,162 @@ uint64_t count_global_rows(hga_ctx* c) {
 // ---- global answers of the count queries after hga_count_exchange ----------------------------
 
 namespace {
-// A rank's histogram slot for the one-shot gather: [overflow rows, pairs, the first cap pairs].
-constexpr uint64_t HS_CAP = 1024;
-constexpr uint64_t HS_WORDS = 2 + 2 * HS_CAP;
+using proto::HS_CAP;
+using proto::HS_HDR;
+using proto::HS_WORDS;
+
+// A rank's histogram slot for the one-shot gather (proto::merge_hist_slots): [error bits, overflow
+// rows, pairs, the first HS_CAP pairs]; gstat: the counters of an unconsumed count run (its settle
+// bits), or null.
 __global__ void kx_hist_slot(const unsigned long long* __restrict__ ctrl, const unsigned long long* __restrict__ pairs,
+                             const unsigned long long* __restrict__ gstat, uint64_t ncap,
                              unsigned long long* __restrict__ slot) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) {
-        slot[0] = ctrl[0];
-        slot[1] = ctrl[2];
+        slot[0] = (gstat ? (gstat[2] & 7ull) : 0ull) | ((ctrl[1] & 1ull) ? proto::QE_SPEC_THR : 0ull) |
+                  ((ctrl[1] & 2ull) ? proto::QE_OVER : 0ull) | (ctrl[2] > ncap ? proto::QE_COMPACT : 0ull);
+        slot[1] = ctrl[0];
+        slot[2] = ctrl[2];
     }
     const uint64_t n = ctrl[2] < HS_CAP ? ctrl[2] : HS_CAP;
-    for (uint64_t i = t; i < 2 * n; i += (uint64_t)gridDim.x * blockDim.x) slot[2 + i] = pairs[i];
+    for (uint64_t i = t; i < 2 * n; i += (uint64_t)gridDim.x * blockDim.x) slot[HS_HDR + i] = pairs[i];
 }
+
+// The same error on every rank (the lowest failing one's, as its own checks name it).
+[[noreturn]] void throw_query_error(const proto::QueryError& e) {
+    static const struct {
+        uint64_t bit;
+        hga_status code;
+        const char* msg;
+    } order[] = {{proto::QE_POOL, HGA_ERR_OOM, "level-1 block pool exhausted"},
+                 {proto::QE_UNSPLIT, HGA_ERR_INVALID, "a bucket could not be split to fit the LDS table"},
+                 {proto::QE_ROWCAP, HGA_ERR_OOM, "row capacity exceeded"},
+                 {proto::QE_SPEC_THR, HGA_ERR_INVALID, "a row's specificity is above the last threshold"},
+                 {proto::QE_OVER, HGA_ERR_OOM, "histogram overflow list full"},
+                 {proto::QE_COMPACT, HGA_ERR_OOM, "histogram compaction buffer full"}};
+    for (const auto& o : order)
+        if (e.bits & o.bit) throw Error(o.code, "rank " + std::to_string(e.rank) + ": " + o.msg);
+    throw Error(HGA_ERR_INVALID, "rank " + std::to_string(e.rank) + ": count query failed");
+}
+
+// Runs a local query that may fail on this rank with an error the others must learn about: returns
+// its error bits (CountState::last_err) instead of throwing them; other errors propagate.
+template <class Fn>
+uint64_t run_reporting(hga_ctx* c, Fn&& fn) {
+    c->count.last_err = 0;
+    try {
+        fn();
+    } catch (const Error&) {
+        if (!c->count.last_err) throw;
+    }
+    return c->count.last_err;
+}
+
+// ---- code-range re-partition of device lists (proto::repartition) ----
+// pos[o] = entries of the ascending list (codes = key & cmask) below spl[o], o < P - 1.
+__global__ void kx_split_sorted(const uint64_t* __restrict__ keys, uint64_t n, uint64_t cmask,
+                                const uint64_t* __restrict__ spl, uint32_t m, uint64_t* __restrict__ pos) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= m) return;
+    const uint64_t v = spl[o];
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if ((keys[mid] & cmask) < v) lo = mid + 1;
+        else hi = mid;
+    }
+    pos[o] = lo;
+}
+// dst[i] = src[idx[i]] for entries of w u32 words
+__global__ void kx_gather_words(const uint32_t* __restrict__ idx, const uint32_t* __restrict__ src, uint64_t n,
+                                uint32_t w, uint32_t* __restrict__ dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t j = idx[i];
+    for (uint32_t q = 0; q < w; ++q) dst[i * w + q] = src[j * w + q];
+}
+__global__ void kx_iota(uint32_t* v, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (uint32_t)i;
+}
+
+// An ascending device list (keys[n] + n payloads of vb bytes, vb a multiple of 4) for proto::repartition;
+// the rank's code range ends up in `out` (keys, then payloads), ascending.
+struct DevList {
+    hga_ctx* c;
+    int bits;
+    uint64_t n;
+    const uint64_t* k;
+    const void* v;
+    uint32_t vb;
+    DevBuf& out;
+    DevBuf tmp;
+    uint64_t n_out = 0;
+    uint32_t vbytes() const { return vb; }
+    const void* keys() const { return k; }
+    const void* vals() const { return v; }
+    void split(const uint64_t* spl, uint32_t P, uint64_t* per) {
+        std::vector<uint64_t> pos(P + 1, 0);
+        pos[P] = n;
+        if (P > 1) {
+            auto* d = static_cast<uint64_t*>(tmp.ensure(16 * (uint64_t)P + 64));
+            HGA_HIP(hipMemcpyAsync(d, spl, 8ull * (P - 1), hipMemcpyHostToDevice, c->stream));
+            const uint64_t cmask = bits >= 64 ? ~0ull : (1ull << bits) - 1;
+            hipLaunchKernelGGL(kx_split_sorted, dim3((P + 254) / 255), dim3(256), 0, c->stream, k, n, cmask, d, P - 1,
+                               d + P);
+            c->check_launch("kx_split_sorted");
+            HGA_HIP(hipMemcpyAsync(pos.data() + 1, d + P, 8ull * (P - 1), hipMemcpyDeviceToHost, c->stream));
+            c->sync();
+        }
+        for (uint32_t o = 0; o < P; ++o) per[o] = pos[o + 1] - pos[o];
+    }
+    void* recv(uint64_t m) { return out.ensure(std::max<uint64_t>(m, 1) * (8 + vb) + 64); }
+    void finish(const uint64_t*, uint32_t, uint64_t m) {
+        n_out = m;
+        if (m < 2) return;
+        uint64_t* rk = out.as<uint64_t>();
+        auto* rv = reinterpret_cast<uint32_t*>(rk + m);
+        if (vb == 0) {
+            radix_sort_u64(c, rk, nullptr, m, bits, c->count.scratch);
+        } else if (vb == 4) {
+            radix_sort_u64(c, rk, rv, m, bits, c->count.scratch);
+        } else {   // wider payloads: sort (key, index), then gather the payloads
+            const uint32_t w = vb / 4;
+            char* t = static_cast<char*>(tmp.ensure(m * (4 + (uint64_t)vb) + 64));
+            auto* idx = reinterpret_cast<uint32_t*>(t);
+            auto* pv = reinterpret_cast<uint32_t*>(t + m * 4);
+            hipLaunchKernelGGL(kx_iota, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, idx, m);
+            radix_sort_u64(c, rk, idx, m, bits, c->count.scratch);
+            hipLaunchKernelGGL(kx_gather_words, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, idx, rv, m, w, pv);
+            c->check_launch("kx_gather_words");
+            HGA_HIP(hipMemcpyAsync(rv, pv, m * (uint64_t)vb, hipMemcpyDeviceToDevice, c->stream));
+        }
+    }
+};
 }  // namespace
 
 void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out) {
     Comm& m = need_comm(c);
     std::vector<int64_t> local;
     CtxXport x(c);
+    proto::QueryError qe;
     if (!m.on_device()) {
-        count_spec_hist(c, thr, n_thr, local);
-        out = proto::spec_hist_global(x, local);
+        const uint64_t err = run_reporting(c, [&] { count_spec_hist(c, thr, n_thr, local); });
+        out = proto::spec_hist_global(x, local, err, &qe);
+        if (qe.rank >= 0) throw_query_error(qe);
         return;
     }
-    // RCCL: every rank's device pairs gathered inside the local call's one synchronisation; a rank
-    // with an overflow list or more than HS_CAP pairs sends everyone to the general gather
+    // RCCL: every rank's device pairs and error bits gathered inside the local call's one
+    // synchronisation; a rank with an overflow list or more than HS_CAP pairs sends everyone to the
+    // general gather, a rank with an error makes every rank raise it (proto::merge_hist_slots)
     const int P = m.nranks;
     const uint64_t sb = HS_WORDS * 8;
     char* ds = static_cast<char*>(m.stage.ensure(sb * (P + 1) + 16));
     auto* hs = static_cast<unsigned long long*>(m.hstage.ensure(sb * P + 16));
+    const unsigned long long* gst = c->count.pending ? static_cast<const unsigned long long*>(c->count.cursor.p) : nullptr;
+    bool gathered = false;
     const SpecHook hook = [&](const unsigned long long* ctrl, const unsigned long long* pairs) {
-        hipLaunchKernelGGL(kx_hist_slot, dim3(8), dim3(256), 0, c->stream, ctrl, pairs,
+        hipLaunchKernelGGL(kx_hist_slot, dim3(8), dim3(256), 0, c->stream, ctrl, pairs, gst, (uint64_t)1 << 20,
                            reinterpret_cast<unsigned long long*>(ds));
         c->check_launch("kx_hist_slot");
         std::vector<uint64_t> sz(P, sb);
@@ -348,79 +472,144 @@ void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::
         for (int p = 0; p < P; ++p) rp[p] = ds + sb * (p + 1);
         m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
         HGA_HIP(hipMemcpyAsync(hs, ds + sb, sb * P, hipMemcpyDeviceToHost, c->stream));
+        gathered = true;
     };
-    count_spec_hist(c, thr, n_thr, local, &hook);
-    bool fits = true;
-    for (int p = 0; p < P; ++p) fits = fits && hs[p * HS_WORDS] == 0 && hs[p * HS_WORDS + 1] <= HS_CAP;
-    if (!fits) {   // the same decision on every rank (the same gathered words)
-        out = proto::spec_hist_global(x, local);
-        return;
-    }
-    std::map<std::pair<int64_t, int64_t>, int64_t> bins;
-    for (int p = 0; p < P; ++p) {
-        const unsigned long long* sl = hs + p * HS_WORDS;
-        for (uint64_t i = 0; i < sl[1]; ++i) {
-            const uint64_t key = sl[2 + 2 * i];
-            bins[{(int64_t)(key >> 56), (int64_t)(key & ((1ull << 56) - 1))}] += (int64_t)sl[3 + 2 * i];
-        }
-    }
-    out.clear();
-    out.reserve(3 * bins.size());
-    for (const auto& b : bins) {
-        out.push_back(b.first.first);
-        out.push_back(b.first.second);
-        out.push_back(b.second);
+    const uint64_t err = run_reporting(c, [&] { count_spec_hist(c, thr, n_thr, local, &hook); });
+    if (!gathered) HGA_REQUIRE(false, HGA_ERR_STATE, "count_spec_hist failed before its gather");
+    (void)err;   // this rank's bits are in its own slot
+    const proto::SlotMerge r = proto::merge_hist_slots(reinterpret_cast<const uint64_t*>(hs), P, out, &qe);
+    if (r == proto::SlotMerge::error) throw_query_error(qe);
+    if (r == proto::SlotMerge::fallback) {   // the same decision on every rank (the same gathered words)
+        out = proto::spec_hist_global(x, local, 0, &qe);
+        if (qe.rank >= 0) throw_query_error(qe);
     }
 }
 
 void count_select_global(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* nd) {
     Comm& m = need_comm(c);
-    std::vector<uint64_t> mine(2);
-    if (!m.on_device()) {
-        count_select(c, lower, upper, &mine[0], &mine[1]);
-        CtxXport x(c);
-        const std::vector<uint64_t> g = proto::sum_u64(x, mine);
-        *n = g[0];
-        *nd = g[1];
-        return;
-    }
-    // RCCL: the counters' gather rides in the local call's one synchronisation
+    c->count.sel_rep_n = ~0ull;   // a new selection: not re-partitioned yet
+    // an unconsumed count run is settled first, so a failed run is reported in the gathered words
+    const uint64_t serr = run_reporting(c, [&] { count_settle(c); });
     const int P = m.nranks;
-    char* ds = static_cast<char*>(m.stage.ensure(16 * ((uint64_t)P + 1) + 16));
-    auto* hs = static_cast<uint64_t*>(m.hstage.ensure(16 * (uint64_t)P + 16));
-    const SelHook hook = [&](const unsigned long long* stat) {
-        HGA_HIP(hipMemcpyAsync(ds, stat, 16, hipMemcpyDeviceToDevice, c->stream));
-        std::vector<uint64_t> sz(P, 16);
-        std::vector<const void*> sp(P, ds);
-        std::vector<void*> rp(P);
-        for (int p = 0; p < P; ++p) rp[p] = ds + 16 * (p + 1);
-        m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
-        HGA_HIP(hipMemcpyAsync(hs, ds + 16, 16 * (uint64_t)P, hipMemcpyDeviceToHost, c->stream));
-    };
-    count_select(c, lower, upper, &mine[0], &mine[1], &hook);
+    uint64_t mine[3] = {0, 0, serr};
+    std::vector<uint64_t> all(3 * (size_t)P);
+    if (!m.on_device()) {
+        if (!serr) count_select(c, lower, upper, &mine[0], &mine[1]);
+        CtxXport x(c);
+        x.allgather(mine, 24, all.data());
+    } else {
+        // RCCL: the counters' gather rides in the local call's one synchronisation
+        char* ds = static_cast<char*>(m.stage.ensure(24 * ((uint64_t)P + 1) + 16));
+        auto* hs = static_cast<uint64_t*>(m.hstage.ensure(24 * (uint64_t)P + 16));
+        auto gather = [&] {
+            std::vector<uint64_t> sz(P, 24);
+            std::vector<const void*> sp(P, ds);
+            std::vector<void*> rp(P);
+            for (int p = 0; p < P; ++p) rp[p] = ds + 24 * (p + 1);
+            m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+            HGA_HIP(hipMemcpyAsync(hs, ds + 24, 24 * (uint64_t)P, hipMemcpyDeviceToHost, c->stream));
+        };
+        if (serr) {   // take part in the gather with the error word only
+            HGA_HIP(hipMemcpyAsync(ds, mine, 24, hipMemcpyHostToDevice, c->stream));
+            gather();
+            c->sync();
+        } else {
+            const SelHook hook = [&](const unsigned long long* stat) {
+                HGA_HIP(hipMemcpyAsync(ds, stat, 16, hipMemcpyDeviceToDevice, c->stream));
+                HGA_HIP(hipMemsetAsync(ds + 16, 0, 8, c->stream));
+                gather();
+            };
+            count_select(c, lower, upper, &mine[0], &mine[1], &hook);
+        }
+        std::memcpy(all.data(), hs, 24 * (size_t)P);
+    }
+    const proto::QueryError qe = proto::first_error(all.data() + 2, P, 3);
+    if (qe.rank >= 0) throw_query_error(qe);
     *n = *nd = 0;
     for (int p = 0; p < P; ++p) {
-        *n += hs[2 * p];
-        *nd += hs[2 * p + 1];
+        *n += all[3 * (size_t)p];
+        *nd += all[3 * (size_t)p + 1];
     }
 }
 
-// The whole export on every rank (after count_select): keys ascending, flags.
-void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags) {
+// This rank's code range of the global export (proto::repartition of the owners' sorted selections,
+// one all-to-all of the selected keys), kept on the device in count.sel_rep; returns its size.
+uint64_t count_export_repartition(hga_ctx* c) {
     auto& s = c->count;
-    std::vector<uint64_t> k(s.n_sel);
-    std::vector<uint8_t> f(s.n_sel);
-    count_fetch_selected(c, k.data(), f.data());
+    need_comm(c);
+    count_settle(c);
+    if (s.sel_rep_n != ~0ull) return s.sel_rep_n;
     CtxXport x(c);
-    proto::merge_sorted(x, k, f, 1, keys, flags);
+    const bool flag_bit = s.k <= 31;
+    const uint64_t cap = std::max<uint64_t>(s.rows, 1);
+    const char* sb = static_cast<const char*>(s.sel_keys.p);
+    DevList l{c, 2 * s.k, s.n_sel, reinterpret_cast<const uint64_t*>(sb), flag_bit ? nullptr : sb + cap * 8,
+              flag_bit ? 0u : 4u, s.sel_rep, {}};
+    s.sel_rep_n = proto::repartition(l, x, s.k);
+    return s.sel_rep_n;
 }
 
-void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
-    std::vector<uint64_t> k;
-    std::vector<uint32_t> v;
-    count_rows(c, file, k, v);
+// The whole export on every rank (after count_select): the ranks' code ranges concatenated in rank
+// order — ascending, no merge.
+void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags) {
+    auto& s = c->count;
+    const uint64_t n = count_export_repartition(c);
+    const bool flag_bit = s.k <= 31;
+    std::vector<uint64_t> k(n);
+    std::vector<uint8_t> f(n);
+    if (n) {
+        HGA_HIP(hipMemcpyAsync(k.data(), s.sel_rep.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+        std::vector<uint32_t> f32;
+        if (!flag_bit) {
+            f32.resize(n);
+            HGA_HIP(hipMemcpyAsync(f32.data(), s.sel_rep.as<uint64_t>() + n, n * 4, hipMemcpyDeviceToHost, c->stream));
+        }
+        c->sync();
+        for (uint64_t i = 0; i < n; ++i) {
+            f[i] = flag_bit ? (uint8_t)(k[i] >> 63) : (uint8_t)f32[i];
+            if (flag_bit) k[i] &= ~(1ull << 63);
+        }
+    }
     CtxXport x(c);
-    proto::merge_sorted(x, k, v, file < 0 ? c->count.n_files : 1, keys, counts);
+    keys = proto::concat(x, k);
+    flags = proto::concat(x, f);
+}
+
+// The global rows (file < 0) or one file's dump rows: the owners' sorted rows re-partitioned by code
+// range on the device (one all-to-all of the rows), each rank's range fetched, concatenated.
+void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
+    auto& s = c->count;
+    count_settle(c);
+    HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
+    HGA_REQUIRE(file < (int)s.n_files, HGA_ERR_INVALID, "file index out of range");
+    const uint32_t F = s.n_files;
+    DevBuf dk, dc, out;
+    count_rows_device(c, dk, dc);
+    CtxXport x(c);
+    DevList l{c, 2 * s.k, s.rows, dk.as<uint64_t>(), dc.p, 4u * F, out, {}};
+    const uint64_t n = proto::repartition(l, x, s.k);
+    std::vector<uint64_t> k(n);
+    std::vector<uint32_t> v((size_t)n * F);
+    if (n) {
+        HGA_HIP(hipMemcpyAsync(k.data(), out.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+        HGA_HIP(hipMemcpyAsync(v.data(), out.as<uint64_t>() + n, n * 4ull * F, hipMemcpyDeviceToHost, c->stream));
+    }
+    c->sync();
+    std::vector<uint64_t> mk;
+    std::vector<uint32_t> mv;
+    if (file < 0) {
+        mk.swap(k);
+        mv.swap(v);
+    } else {
+        for (uint64_t i = 0; i < n; ++i)
+            if (v[i * F + (uint32_t)file]) {
+                mk.push_back(k[i]);
+                mv.push_back(v[i * F + (uint32_t)file]);
+            }
+    }
+    keys = proto::concat(x, mk);
+    counts = proto::concat(x, mv);
 }
 
 // ---- sharded categorization ------------------------------------------------------------------

@@ -582,12 +582,20 @@ __global__ void __launch_bounds__(NT_3) kc_split3(const E* __restrict__ in, cons
 // ---------------------------------------------------------------- pass B2
 // One workgroup per level-1 block: the next fb2 bits pick the fine bucket (<= 64-way,
 // ranked through LDS so each bucket's run is one coalesced segment).
+#ifndef HGA_NT_REBIN_LD
+#define HGA_NT_REBIN_LD 0   // timing variants: nontemporal element loads / stores in kc_rebin
+#endif
+#ifndef HGA_NT_REBIN_ST
+#define HGA_NT_REBIN_ST 0
+#endif
+#ifndef HGA_SPILL_GRID
+#define HGA_SPILL_GRID 1024   // workgroups of the spill-block launch (grid-stride over gstat[3])
+#endif
 template <class E1, class E>
-__global__ void __launch_bounds__(NT_R_MAX) kc_rebin(const E1* __restrict__ in1, const Blk* __restrict__ table,
-                                                 const unsigned long long* __restrict__ gstat, uint32_t W,
-                                                 KP kp, const uint32_t* __restrict__ nblk,
-                                                 unsigned long long* __restrict__ off,
-                                                 E* __restrict__ out) {
+__device__ __forceinline__ void rebin_block(const uint64_t blk, const E1* __restrict__ in1,
+                                            const Blk* __restrict__ table, uint32_t W, const KP& kp,
+                                            const uint32_t* __restrict__ nblk, unsigned long long* __restrict__ off,
+                                            E* __restrict__ out) {
     constexpr int NT_R = rebin_nt<E>();
     constexpr int IT = CH_R / NT_R;
     static_assert(CH_R >= (int)BLK, "a block must fit one re-bin pass");
@@ -599,14 +607,13 @@ __global__ void __launch_bounds__(NT_R_MAX) kc_rebin(const E1* __restrict__ in1,
     const int tid = threadIdx.x;
     const uint32_t nb2 = kp.nb2;
     const uint64_t n_first = (uint64_t)W * kp.nb1;
-    const uint64_t blk = blockIdx.x;
     // first blocks: everything is known from the index, so the element, size and offset loads
     // all go out together; spill blocks (rare) look themselves up
-    if (blk >= n_first && blk >= gstat[3]) return;
     const E1* __restrict__ src = in1 + blk * BLK;
     E1 v[IT];
 #pragma unroll
-    for (int j = 0; j < IT; ++j) v[j] = src[(uint32_t)j * NT_R + tid];
+    for (int j = 0; j < IT; ++j)
+        v[j] = HGA_NT_REBIN_LD ? __builtin_nontemporal_load(&src[(uint32_t)j * NT_R + tid]) : src[(uint32_t)j * NT_R + tid];
     uint32_t w, d1;
     if (blk < n_first) {
         w = (uint32_t)(blk / kp.nb1);
@@ -660,7 +667,30 @@ __global__ void __launch_bounds__(NT_R_MAX) kc_rebin(const E1* __restrict__ in1,
     for (uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6); d < nb2; d += NT_R / 64) {
         const uint32_t o = off2[d], len = off2[d + 1] - o;
         E* __restrict__ dst = out + base2[d];
-        for (uint32_t jj = (uint32_t)(tid & 63); jj < len; jj += 64) dst[jj] = stage[o + jj];
+        for (uint32_t jj = (uint32_t)(tid & 63); jj < len; jj += 64) {
+            if (HGA_NT_REBIN_ST) __builtin_nontemporal_store(stage[o + jj], &dst[jj]);
+            else dst[jj] = stage[o + jj];
+        }
+    }
+}
+
+// first = true: one workgroup per first block (block blockIdx.x < W * nb1); first = false: the spill
+// blocks [W * nb1, gstat[3]) grid-stride over a small grid (at C2 there are none, and a grid of every
+// possible spill block retired ~36 K empty workgroups)
+template <class E1, class E>
+__global__ void __launch_bounds__(NT_R_MAX) kc_rebin(const E1* __restrict__ in1, const Blk* __restrict__ table,
+                                                 const unsigned long long* __restrict__ gstat, uint32_t W,
+                                                 KP kp, const uint32_t* __restrict__ nblk,
+                                                 unsigned long long* __restrict__ off,
+                                                 E* __restrict__ out, bool first) {
+    if (first) {
+        rebin_block<E1, E>(blockIdx.x, in1, table, W, kp, nblk, off, out);
+        return;
+    }
+    const uint64_t n_first = (uint64_t)W * kp.nb1, used = gstat[3];
+    for (uint64_t blk = n_first + blockIdx.x; blk < used; blk += gridDim.x) {
+        rebin_block<E1, E>(blk, in1, table, W, kp, nblk, off, out);
+        __syncthreads();   // the block's LDS is reused by the next one
     }
 }
 
@@ -1074,6 +1104,9 @@ __global__ void __launch_bounds__(NT_C) kc_count(const E* __restrict__ binned,
 #ifndef HGA_PF_P
 #define HGA_PF_P 6
 #endif
+#ifndef HGA_NT_COUNT_LD
+#define HGA_NT_COUNT_LD 0   // timing variant: nontemporal element loads in kc_count_s
+#endif
 constexpr int NT_P = HGA_NT_P;
 constexpr int PF_P = HGA_PF_P;          // binned elements per thread per batch
 static_assert(PF_P <= 15, "miss counts are scanned as 4-bit values");
@@ -1211,7 +1244,8 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                 if (bi < nfull) {
                     const uint32_t* __restrict__ bp = binned + i0;
 #pragma unroll
-                    for (int q = 0; q < PF_P; ++q) nx[q] = bp[q * NT_P + tid];
+                    for (int q = 0; q < PF_P; ++q)
+                        nx[q] = HGA_NT_COUNT_LD ? __builtin_nontemporal_load(&bp[q * NT_P + tid]) : bp[q * NT_P + tid];
                 } else {
 #pragma unroll
                     for (int q = 0; q < PF_P; ++q) {
@@ -2045,12 +2079,20 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
                            reinterpret_cast<const uint64_t*>(off), d_bf, W, nb, F, fs);
     });
     c->check_launch("kc_fs");
-    // B2: re-bin every level-1 block into the fine buckets
-    const unsigned rebin_grid = (unsigned)std::max<uint64_t>(1, table_cap);   // exits past gstat[3]
+    // B2: re-bin every level-1 block into the fine buckets: the first blocks, then the spill blocks
+    const unsigned spill_grid = (unsigned)std::min<uint64_t>(table_cap - n_first, HGA_SPILL_GRID);
     c->launch("kc_rebin", [&] {
 #define HGA_REBIN(E1T, ET)                                                                                 \
-    hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3(rebin_grid), dim3(rebin_nt<ET>()), 0, c->stream,                    \
-                       static_cast<const E1T*>(binned1), table, gstat, W, kp, nblk, off, static_cast<ET*>(binned))
+    do {                                                                                                   \
+        if (n_first)                                                                                       \
+            hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3((unsigned)n_first), dim3(rebin_nt<ET>()), 0, c->stream, \
+                               static_cast<const E1T*>(binned1), table, gstat, W, kp, nblk, off,            \
+                               static_cast<ET*>(binned), true);                                              \
+        if (spill_grid)                                                                                    \
+            hipLaunchKernelGGL((kc_rebin<E1T, ET>), dim3(spill_grid), dim3(rebin_nt<ET>()), 0, c->stream,  \
+                               static_cast<const E1T*>(binned1), table, gstat, W, kp, nblk, off,            \
+                               static_cast<ET*>(binned), false);                                             \
+    } while (0)
         if (e1_32 && e32) HGA_REBIN(uint32_t, uint32_t);
         else if (e32) HGA_REBIN(uint64_t, uint32_t);
         else if (e1_32) HGA_REBIN(uint32_t, uint64_t);
@@ -2180,6 +2222,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     s.ran = true;
     s.dist = false;
     s.n_sel = 0;
+    s.sel_rep_n = ~0ull;
     s.pending = true;
     if (dumps) count_settle(c);   // the cached rows are merged on the host side now
 }
@@ -2197,6 +2240,7 @@ void count_settle(hga_ctx* c, const unsigned long long* h) {
     }
     s.pending = false;
     if (h[2] & 7ull) s.ran = false;   // a failed run has no rows to consume
+    s.last_err = h[2] & 7ull;         // proto::QE_UNSPLIT / QE_ROWCAP / QE_POOL
     HGA_REQUIRE(!(h[2] & 4ull), HGA_ERR_OOM, "level-1 block pool exhausted");
     HGA_REQUIRE(!(h[2] & 1ull), HGA_ERR_INVALID, "a bucket could not be split to fit the LDS table");
     HGA_REQUIRE(!(h[2] & 2ull), HGA_ERR_OOM, "row capacity exceeded");
@@ -2345,7 +2389,9 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     });
     c->check_launch("kc_hist_compact");
     c->sync();
+    s.last_err = 0;
     if (pend) count_settle(c, hrun);
+    s.last_err = ((hc[1] & 1ull) ? 8ull : 0ull) | ((hc[1] & 2ull) ? 16ull : 0ull) | (hc[2] > ncap ? 32ull : 0ull);
     HGA_REQUIRE(!(hc[1] & 1ull), HGA_ERR_INVALID, "a row's specificity is above the last threshold");
     HGA_REQUIRE(!(hc[1] & 2ull), HGA_ERR_OOM, "histogram overflow list full");
     HGA_REQUIRE(hc[2] <= ncap, HGA_ERR_OOM, "histogram compaction buffer full");
@@ -2453,6 +2499,7 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
         radix_sort_u64(c, out, flag_bit ? nullptr : flag, n, bits, s.scratch);
     }
     s.n_sel = n;
+    s.sel_rep_n = ~0ull;   // a new selection: its code-range re-partition is stale
     *n_out = n;
     *n_discr = hs[1];
 }
@@ -2490,6 +2537,26 @@ void count_fetch_selected(hga_ctx* c, uint64_t* dst, uint8_t* flags) {
         for (uint64_t i = 0; i < s.n_sel; ++i) flags[i] = (uint8_t)f[i];
 }
 
+// The merged rows ascending on the device: keys[rows], counts row-major [rows][F] (enqueued).
+void count_rows_device(hga_ctx* c, DevBuf& keys, DevBuf& counts) {
+    auto& s = c->count;
+    const uint64_t rows = s.rows;
+    const uint32_t F = s.n_files;
+    uint64_t* k = static_cast<uint64_t*>(keys.ensure(std::max<uint64_t>(rows, 1) * 8));
+    uint32_t* cc = static_cast<uint32_t*>(counts.ensure(std::max<uint64_t>(rows, 1) * 4 * F));
+    if (!rows) return;
+    DevBuf tv;
+    uint32_t* v = static_cast<uint32_t*>(tv.ensure(rows * 4));
+    HGA_HIP(hipMemcpyAsync(k, s.rows_key.p, rows * 8, hipMemcpyDeviceToDevice, c->stream));
+    hipLaunchKernelGGL(kc_iota, dim3(blocks_for(rows, 256)), dim3(256), 0, c->stream, v, rows);
+    c->check_launch("kc_iota");
+    radix_sort_u64(c, k, v, rows, 2 * s.k, s.scratch);
+    hipLaunchKernelGGL(kc_gather_rows, dim3(blocks_for(rows, 256)), dim3(256), 0, c->stream, v,
+                       s.rows_cnt.as<uint32_t>(), rows, s.rows_cap, F, cc);
+    c->check_launch("kc_gather_rows");
+    c->sync();   // tv is freed on return
+}
+
 // All merged rows ascending (file < 0), or one file's dump rows (file >= 0).
 void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
     auto& s = c->count;
@@ -2502,17 +2569,10 @@ void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<u
     keys.clear();
     counts.clear();
     if (!rows) return;
-    DevBuf tk, tv, tc;
-    uint64_t* k = static_cast<uint64_t*>(tk.ensure(rows * 8));
-    uint32_t* v = static_cast<uint32_t*>(tv.ensure(rows * 4));
-    uint32_t* cc = static_cast<uint32_t*>(tc.ensure(rows * 4 * F));
-    HGA_HIP(hipMemcpyAsync(k, s.rows_key.p, rows * 8, hipMemcpyDeviceToDevice, c->stream));
-    hipLaunchKernelGGL(kc_iota, dim3(blocks_for(rows, 256)), dim3(256), 0, c->stream, v, rows);
-    c->check_launch("kc_iota");
-    radix_sort_u64(c, k, v, rows, 2 * s.k, s.scratch);
-    hipLaunchKernelGGL(kc_gather_rows, dim3(blocks_for(rows, 256)), dim3(256), 0, c->stream, v,
-                       s.rows_cnt.as<uint32_t>(), rows, s.rows_cap, F, cc);
-    c->check_launch("kc_gather_rows");
+    DevBuf tk, tc;
+    count_rows_device(c, tk, tc);
+    const uint64_t* k = tk.as<uint64_t>();
+    const uint32_t* cc = tc.as<uint32_t>();
     std::vector<uint64_t> hk(rows);
     std::vector<uint32_t> hc(rows * F);
     HGA_HIP(hipMemcpyAsync(hk.data(), k, rows * 8, hipMemcpyDeviceToHost, c->stream));

@@ -167,26 +167,54 @@ uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file, const std::vector
     return n;
 }
 
+// ---- errors of the global count queries ------------------------------------------------------
+// Every rank reports its error bits in the words the query gathers anyway, and every rank decides
+// on the gathered words: all ranks raise the same error, and none enters a collective (a fallback
+// gather) that a failed rank skips.  Bits: the settle bits of an unconsumed count run (1 a bucket
+// could not be split, 2 row capacity, 4 level-1 pool) and the histogram's own (8 a specificity above
+// the last threshold, 16 overflow list full, 32 compaction buffer full).
+enum : uint64_t { QE_UNSPLIT = 1, QE_ROWCAP = 2, QE_POOL = 4, QE_SPEC_THR = 8, QE_OVER = 16, QE_COMPACT = 32 };
+struct QueryError {
+    int rank = -1;   // the lowest failing rank, -1: none
+    uint64_t bits = 0;
+};
+inline QueryError first_error(const uint64_t* words, int P, size_t stride) {
+    QueryError e;
+    for (int p = 0; p < P && e.rank < 0; ++p)
+        if (words[(size_t)p * stride]) {
+            e.rank = p;
+            e.bits = words[(size_t)p * stride];
+        }
+    return e;
+}
+
 // Owners' (threshold index, total, count) triples -> the global histogram, (threshold, total) order.
 // One fixed-size all-gather of [n, up to HIST_CAP triples] per rank; only when some rank has more
 // triples (very wide count ranges) a variable-size all-gather follows.
+// `err` (this rank's error bits, see QueryError) rides in the slot; when any rank reports one, every
+// rank returns an empty histogram with *qe naming the lowest failing rank (no further collective).
 constexpr size_t HIST_CAP = 1024;
-inline std::vector<int64_t> spec_hist_global(Xport& x, const std::vector<int64_t>& local) {
-    const size_t P = (size_t)x.nranks, slot = 1 + 3 * HIST_CAP;
+inline std::vector<int64_t> spec_hist_global(Xport& x, const std::vector<int64_t>& local, uint64_t err = 0,
+                                             QueryError* qe = nullptr) {
+    const size_t P = (size_t)x.nranks, slot = 2 + 3 * HIST_CAP;
     std::vector<int64_t> mine(slot, 0), all(P * slot);
-    const size_t n = local.size() / 3;
-    mine[0] = (int64_t)n;
-    for (size_t i = 0; i < 3 * n && i < 3 * HIST_CAP; ++i) mine[1 + i] = local[i];
+    const size_t n = err ? 0 : local.size() / 3;
+    mine[0] = (int64_t)err;
+    mine[1] = (int64_t)n;
+    for (size_t i = 0; i < 3 * n && i < 3 * HIST_CAP; ++i) mine[2 + i] = local[i];
     x.allgather(mine.data(), slot * 8, all.data());
+    const QueryError e = first_error(reinterpret_cast<const uint64_t*>(all.data()), (int)P, slot);
+    if (qe) *qe = e;
+    if (e.rank >= 0) return {};
     bool fits = true;
-    for (size_t p = 0; p < P; ++p) fits = fits && (size_t)all[p * slot] <= HIST_CAP;
+    for (size_t p = 0; p < P; ++p) fits = fits && (size_t)all[p * slot + 1] <= HIST_CAP;
     std::vector<std::vector<char>> parts;
     if (fits) {
         parts.resize(P);
         for (size_t p = 0; p < P; ++p) {
-            const size_t np = (size_t)all[p * slot];
+            const size_t np = (size_t)all[p * slot + 1];
             parts[p].resize(np * 24);
-            if (np) std::memcpy(parts[p].data(), &all[p * slot + 1], np * 24);
+            if (np) std::memcpy(parts[p].data(), &all[p * slot + 2], np * 24);
         }
     } else {
         parts = x.allgatherv(local.data(), local.size() * 8);
@@ -261,6 +289,77 @@ void merge_sorted(Xport& x, const std::vector<uint64_t>& keys, const std::vector
         out_vals.insert(out_vals.end(), v[p] + i * vw, v[p] + (i + 1) * vw);
         if (at[p] < n[p]) q.push({k[p][at[p]], p});
     }
+}
+
+// Code-range re-partition of per-rank ascending lists.  With hash-bucket owners
+// every owner's export and rows span the whole code space; instead of every rank merging every
+// owner's slice (merge_sorted), the ranks cut their ascending lists at the code-range splitters
+// (owner_splitters: rank o takes the codes [spl[o-1], spl[o])) and swap the pieces in one all-to-all
+// of the list itself — the export, not the rows behind it; each rank orders the P runs it received.
+// The global list is then the ranks' ranges concatenated in rank order (concat), the reference's
+// single ascending pass (JellyfishOccurrenceReader.cpp:110-135).
+// Engine L (engine memory: device memory in the product):
+//   uint32_t vbytes();                            payload bytes per entry (0: keys only)
+//   void split(const uint64_t* spl, uint32_t P, uint64_t* per);   entries per code range (list ascending)
+//   const void* keys(); const void* vals();
+//   void* recv(uint64_t n);                       room for n keys (u64) followed by n payloads
+//   void finish(const uint64_t* n_from, uint32_t P, uint64_t n);  the runs in recv (sender order) ->
+//                                                 the rank's ascending list of n entries
+// Returns the entries of this rank's code range.
+template <class L>
+uint64_t repartition(L& l, Xport& x, int k) {
+    const int P = x.nranks, me = x.rank;
+    const std::vector<uint64_t> spl = owner_splitters(k, P);
+    std::vector<uint64_t> per(P), all((size_t)P * P), rn(P), sb(P), rb(P);
+    l.split(spl.data(), (uint32_t)P, per.data());
+    x.allgather(per.data(), 8ull * (uint64_t)P, all.data());
+    uint64_t n = 0;
+    for (int p = 0; p < P; ++p) n += (rn[p] = all[(size_t)p * P + me]);
+    char* r = static_cast<char*>(l.recv(n));
+    const uint32_t vb = l.vbytes();
+    for (int p = 0; p < P; ++p) {
+        sb[p] = per[p] * 8;
+        rb[p] = rn[p] * 8;
+    }
+    x.alltoallv_eng(l.keys(), sb.data(), r, rb.data());
+    if (vb) {
+        for (int p = 0; p < P; ++p) {
+            sb[p] = per[p] * vb;
+            rb[p] = rn[p] * vb;
+        }
+        x.alltoallv_eng(l.vals(), sb.data(), r + n * 8, rb.data());
+    }
+    l.finish(rn.data(), (uint32_t)P, n);
+    return n;
+}
+
+// The one-shot histogram gather of the device path: rank p's slot holds [error bits, overflow rows,
+// n pairs, the first HS_CAP (threshold << 56 | total, count) pairs].  ok: `out` holds the global
+// (threshold, total, count) triples in (threshold, total) order; fallback: some rank has an overflow
+// list or more than HS_CAP pairs (every rank then takes the general gather); error: *err names it.
+constexpr uint64_t HS_CAP = 1024, HS_HDR = 3, HS_WORDS = HS_HDR + 2 * HS_CAP;
+enum class SlotMerge { ok, fallback, error };
+inline SlotMerge merge_hist_slots(const uint64_t* hs, int P, std::vector<int64_t>& out, QueryError* err) {
+    *err = first_error(hs, P, HS_WORDS);
+    if (err->rank >= 0) return SlotMerge::error;
+    for (int p = 0; p < P; ++p)
+        if (hs[(size_t)p * HS_WORDS + 1] != 0 || hs[(size_t)p * HS_WORDS + 2] > HS_CAP) return SlotMerge::fallback;
+    std::map<std::pair<int64_t, int64_t>, int64_t> bins;
+    for (int p = 0; p < P; ++p) {
+        const uint64_t* sl = hs + (size_t)p * HS_WORDS;
+        for (uint64_t i = 0; i < sl[2]; ++i) {
+            const uint64_t key = sl[HS_HDR + 2 * i];
+            bins[{(int64_t)(key >> 56), (int64_t)(key & ((1ull << 56) - 1))}] += (int64_t)sl[HS_HDR + 2 * i + 1];
+        }
+    }
+    out.clear();
+    out.reserve(3 * bins.size());
+    for (const auto& b : bins) {
+        out.push_back(b.first.first);
+        out.push_back(b.first.second);
+        out.push_back(b.second);
+    }
+    return SlotMerge::ok;
 }
 
 // ---- sharded categorization -------------------------------------------

@@ -139,6 +139,13 @@ struct CountState {
         sel_keys, sel_tmp, sel_wtmp, hist_dense, hist_comp, xch, xch2, nblk, bin_files, blist,
         binned3, file_start3, xsend, xrecv, xdir, xsrc, xslab, xemit, xrbase, xdir_b;
     char xemit_host[64] = {};   // the XbEmit last uploaded to xemit (count.hip)
+    // error bits of the last failed settle / histogram (proto::QE_*), so the global queries can report
+    // them in their gathered words (comm.hip)
+    uint64_t last_err = 0;
+    // the export's code range of this rank after count_export_repartition (comm.hip): keys then
+    // flags (u32, k = 32); sel_rep_n = ~0 until the current selection is re-partitioned
+    DevBuf sel_rep;
+    uint64_t sel_rep_n = ~0ull;
     PinnedBuf xsrc_h;           // the owner merge's run table, staged for upload (exchange.hip)
     PinnedBuf xpack_h;          // count counters + per-owner piece totals of count_xb_pack
     std::vector<uint64_t> l1_exact;   // exact level-1 region sizes after an overflowing attempt
@@ -304,6 +311,10 @@ uint64_t count_global_rows(hga_ctx* c);
 void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::vector<int64_t>& out);
 void count_select_global(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, uint64_t* nd);
 void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags);
+// this rank's code range of the global export on the device (count.sel_rep), its size (comm.hip)
+uint64_t count_export_repartition(hga_ctx* c);
+// the merged rows ascending on the device (count.hip): keys[rows], counts row-major [rows][F]
+void count_rows_device(hga_ctx* c, DevBuf& keys, DevBuf& counts);
 void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);
 void lookup_gather(hga_ctx* c);
 void connections_gather(hga_ctx* c, uint64_t* n);

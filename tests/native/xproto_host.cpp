@@ -220,6 +220,57 @@ struct HostEngine {
     }
 };
 
+// An ascending host list for proto::repartition (vw u32 payload words per entry); checks that every
+// received run is ascending and inside this rank's code range
+struct HostList {
+    int bits = 0;
+    uint32_t vw = 0;
+    std::vector<uint64_t> k;
+    std::vector<uint32_t> v;
+    std::vector<char> buf;
+    std::vector<uint64_t> spl;
+    int me = 0;
+    uint64_t cm() const { return bits >= 64 ? ~0ull : (1ull << bits) - 1; }
+    uint32_t vbytes() const { return 4 * vw; }
+    const void* keys() const { return k.data(); }
+    const void* vals() const { return v.data(); }
+    void split(const uint64_t* s, uint32_t P, uint64_t* per) {
+        spl.assign(s, s + (P - 1));
+        uint64_t prev = 0;
+        for (uint32_t o = 0; o < P; ++o) {
+            const uint64_t e = o + 1 < P ? (uint64_t)(std::lower_bound(k.begin(), k.end(), s[o],
+                                                                       [&](uint64_t a, uint64_t b) { return (a & cm()) < b; }) - k.begin())
+                                         : k.size();
+            per[o] = e - prev;
+            prev = e;
+        }
+    }
+    void* recv(uint64_t n) { buf.assign(n * (8 + 4ull * vw) + 64, 0); return buf.data(); }
+    void finish(const uint64_t* n_from, uint32_t P, uint64_t n) {
+        const uint64_t* rk = reinterpret_cast<const uint64_t*>(buf.data());
+        const uint32_t* rv = reinterpret_cast<const uint32_t*>(rk + n);
+        const uint64_t lo = me ? spl[me - 1] : 0, hi = me + 1 < (int)P ? spl[me] : ~0ull;
+        uint64_t at = 0;
+        for (uint32_t p = 0; p < P; ++p)
+            for (uint64_t i = 0; i < n_from[p]; ++i, ++at) {
+                const uint64_t c = rk[at] & cm();
+                if (c < lo || (me + 1 < (int)P && c >= hi)) throw std::runtime_error("entry outside the code range");
+                if (i && (rk[at - 1] & cm()) >= c) throw std::runtime_error("received run not ascending");
+            }
+        std::vector<uint64_t> idx(n);
+        for (uint64_t i = 0; i < n; ++i) idx[i] = i;
+        std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return (rk[a] & cm()) < (rk[b] & cm()); });
+        std::vector<uint64_t> nk(n);
+        std::vector<uint32_t> nv(n * vw);
+        for (uint64_t i = 0; i < n; ++i) {
+            nk[i] = rk[idx[i]];
+            for (uint32_t q = 0; q < vw; ++q) nv[i * vw + q] = rv[idx[i] * vw + q];
+        }
+        k.swap(nk);
+        v.swap(nv);
+    }
+};
+
 struct Rank {
     HostEngine e;
     HostXport x;
@@ -328,9 +379,18 @@ int64_t xt_select(void* h, int64_t lower, int64_t upper, uint64_t** keys, uint8_
             d += nz == 1;
         }
     }
-    std::vector<uint64_t> gk;
-    std::vector<uint8_t> gf;
-    hga::proto::merge_sorted(r->x, k, f, 1, gk, gf);
+    // the owners' ascending selections re-partitioned by code range (one all-to-all of the export),
+    // the ranks' ranges concatenated — the product's count_fetch_selected_global
+    HostList l;
+    l.bits = 2 * r->e.k_;
+    l.vw = 1;
+    l.me = r->x.rank;
+    l.k = k;
+    l.v.assign(f.begin(), f.end());
+    hga::proto::repartition(l, r->x, r->e.k_);
+    std::vector<uint8_t> lf(l.v.begin(), l.v.end());
+    const std::vector<uint64_t> gk = hga::proto::concat(r->x, l.k);
+    const std::vector<uint8_t> gf = hga::proto::concat(r->x, lf);
     *n_discr = hga::proto::sum_u64(r->x, {d})[0];
     *keys = dup(gk);
     *flags = dup(gf);
@@ -342,12 +402,62 @@ int64_t xt_rows(void* h, uint64_t** keys, uint32_t** counts) {
     auto* r = static_cast<Rank*>(h);
     std::vector<uint32_t> c;
     for (auto& v : r->e.counts) c.insert(c.end(), v.begin(), v.end());
-    std::vector<uint64_t> gk;
-    std::vector<uint32_t> gc;
-    hga::proto::merge_sorted(r->x, r->e.keys, c, r->e.F, gk, gc);
+    HostList l;   // code-range re-partition of the rows, as count_rows_global
+    l.bits = 2 * r->e.k_;
+    l.vw = r->e.F;
+    l.me = r->x.rank;
+    l.k = r->e.keys;
+    l.v = c;
+    hga::proto::repartition(l, r->x, r->e.k_);
+    const std::vector<uint64_t> gk = hga::proto::concat(r->x, l.k);
+    const std::vector<uint32_t> gc = hga::proto::concat(r->x, l.v);
     *keys = dup(gk);
     *counts = dup(gc);
     return (int64_t)gk.size();
+}
+
+// ---- errors and the one-shot histogram gather of the device path, every rank deciding alike ----
+// The general histogram gather with this rank's error bits: returns the triples (0 on an error),
+// *qe_rank / *qe_bits = the lowest failing rank and its bits (-1 / 0: none).
+int64_t xt_spec_hist_err(void* h, const int64_t* local, int64_t n_triples, uint64_t err, int64_t** out,
+                         int* qe_rank, uint64_t* qe_bits) {
+    auto* r = static_cast<Rank*>(h);
+    hga::proto::QueryError qe;
+    const std::vector<int64_t> g =
+        hga::proto::spec_hist_global(r->x, std::vector<int64_t>(local, local + 3 * n_triples), err, &qe);
+    *qe_rank = qe.rank;
+    *qe_bits = qe.bits;
+    *out = dup(g);
+    return (int64_t)g.size() / 3;
+}
+
+// The device path's slot gather (comm.hip count_spec_hist_global) on the host: this rank's slot
+// [err, overflow rows, pairs, (ti << 56 | total, count) pairs], an all-gather of the slots, then
+// proto::merge_hist_slots; a fallback takes the general gather of the same triples.  Returns
+// 0 ok / 1 fallback / 2 error with the triples in *out and the error in *qe_rank / *qe_bits.
+int xt_hist_slots(void* h, uint64_t err, uint64_t n_over, const int64_t* local, int64_t n_triples, int64_t** out,
+                  int64_t* n_out, int* qe_rank, uint64_t* qe_bits) {
+    auto* r = static_cast<Rank*>(h);
+    using namespace hga::proto;
+    std::vector<uint64_t> slot(HS_WORDS, 0), all((size_t)r->x.nranks * HS_WORDS);
+    slot[0] = err;
+    slot[1] = n_over;
+    slot[2] = (uint64_t)n_triples;
+    for (int64_t i = 0; i < n_triples && (uint64_t)i < HS_CAP; ++i) {
+        slot[HS_HDR + 2 * i] = (uint64_t)local[3 * i] << 56 | (uint64_t)local[3 * i + 1];
+        slot[HS_HDR + 2 * i + 1] = (uint64_t)local[3 * i + 2];
+    }
+    r->x.allgather(slot.data(), HS_WORDS * 8, all.data());
+    std::vector<int64_t> g;
+    QueryError qe;
+    const SlotMerge m = merge_hist_slots(all.data(), r->x.nranks, g, &qe);
+    int rc = m == SlotMerge::ok ? 0 : m == SlotMerge::fallback ? 1 : 2;
+    if (m == SlotMerge::fallback) g = spec_hist_global(r->x, std::vector<int64_t>(local, local + 3 * n_triples), 0, &qe);
+    *qe_rank = qe.rank;
+    *qe_bits = qe.bits;
+    *out = dup(g);
+    *n_out = (int64_t)g.size() / 3;
+    return rc;
 }
 
 // ---- sharded categorization: construct_indices output of this rank's reads -> the whole input's

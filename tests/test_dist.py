@@ -166,6 +166,75 @@ def test_histogram_merge_fixed_and_fallback_gathers(tmp_path, sizes):
         assert np.array_equal(np.load(out + f".{rank}.npz")["got"], want)
 
 
+def _rand_triples(rank, n):
+    rng = np.random.default_rng(100 + rank)
+    loc = np.stack([rng.integers(0, 8, n), rng.integers(1, 5000, n), rng.integers(1, 100, n)], 1).astype(np.int64)
+    loc = loc[np.lexsort((loc[:, 1], loc[:, 0]))]
+    _, first = np.unique(loc[:, :2], axis=0, return_index=True)
+    return np.ascontiguousarray(loc[np.sort(first)])
+
+
+def _err_worker(rank, world, port, case, out_path):
+    # case: per rank (error bits, overflow rows, triples); both the general gather (host transport)
+    # and the device path's one-shot slot gather decide on the gathered words, so every rank reaches
+    # the same decision — the same error, or the same fallback — and none waits in a collective that
+    # another rank skipped (comm.hip count_spec_hist_global)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        L = xlib()
+        L.xt_spec_hist_err.restype = C.c_int64
+        L.xt_spec_hist_err.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_uint64, C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
+        L.xt_hist_slots.restype = C.c_int
+        L.xt_hist_slots.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int64, C.POINTER(C.c_void_p),
+                                    C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
+        t = hga_dist.gloo_transport()
+        h = L.xt_create(K, 2, rank, world, C.addressof(t), 1)
+        err, n_over, n = case[rank]
+        loc = _rand_triples(rank, n)
+        p, qr, qb = C.c_void_p(), C.c_int(), C.c_uint64()
+        m = L.xt_spec_hist_err(h, loc.ctypes.data, len(loc), err, C.byref(p), C.byref(qr), C.byref(qb))
+        general = (_take(L, p, 3 * m, np.int64).reshape(-1, 3), qr.value, qb.value)
+        nm = C.c_int64()
+        rc = L.xt_hist_slots(h, err, n_over, loc.ctypes.data, len(loc), C.byref(p), C.byref(nm), C.byref(qr),
+                             C.byref(qb))
+        slots = (rc, _take(L, p, 3 * nm.value, np.int64).reshape(-1, 3), qr.value, qb.value)
+        L.xt_destroy(h)
+        np.savez(out_path + f".{rank}.npz", loc=loc, g_hist=general[0], g_rank=general[1], g_bits=general[2],
+                 s_rc=slots[0], s_hist=slots[1], s_rank=slots[2], s_bits=slots[3])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", [
+    [(0, 0, 300), (0, 0, 500)],                 # all fit: one gather
+    [(0, 5, 300), (0, 0, 500)],                 # rank 0 has an overflow list: every rank falls back
+    [(0, 0, 40), (0, 0, 1500), (0, 0, 7)],      # rank 1 past HS_CAP pairs: every rank falls back
+    [(0, 0, 300), (8, 0, 500)],                 # rank 1 fails (specificity above the last threshold)
+    [(0, 0, 30), (4, 3, 20), (16, 0, 2000)],    # two ranks fail: every rank names the lowest one
+])
+def test_global_histogram_errors_and_fallback_decided_alike(tmp_path, case):
+    world = len(case)
+    out = str(tmp_path / "e")
+    mp.start_processes(_err_worker, args=(world, _free_port(), case, out), nprocs=world, start_method="spawn")
+    errs = [(r, c[0]) for r, c in enumerate(case) if c[0]]
+    acc = {}
+    for rank in range(world):
+        for ti, tot, c in np.load(out + f".{rank}.npz")["loc"]:
+            acc[(int(ti), int(tot))] = acc.get((int(ti), int(tot)), 0) + int(c)
+    want = np.array([[a, b, acc[(a, b)]] for a, b in sorted(acc)], np.int64).reshape(-1, 3)
+    fallback = any(c[1] or c[2] > 1024 for c in case)
+    for rank in range(world):
+        r = np.load(out + f".{rank}.npz")
+        if errs:
+            assert (int(r["g_rank"]), int(r["g_bits"])) == errs[0] and len(r["g_hist"]) == 0
+            assert int(r["s_rc"]) == 2 and (int(r["s_rank"]), int(r["s_bits"])) == errs[0]
+        else:
+            assert int(r["g_rank"]) == -1 and np.array_equal(r["g_hist"], want)
+            assert int(r["s_rc"]) == (1 if fallback else 0) and int(r["s_rank"]) == -1
+            assert np.array_equal(r["s_hist"], want)
+
+
 def test_splitters_and_shards():
     L = xlib()
     for k in (1, 5, 19, 32):
