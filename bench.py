@@ -493,6 +493,12 @@ def ingest_leg(ga, gb, threads):
         shutil.rmtree(d, ignore_errors=True)
 
 
+# launch labels of the owner exchange (exchange.hip / comm.hip): the hash-bucket path (count-kernel
+# emission, gather, owner merge), its generic sender fallback, the wide-row path, the export re-partition
+XCH_KERNELS = ("kx_xb_pack", "kx_xb_gather", "kx_xb_hist", "kx_xb_scatter", "kx_xb_owner_tot", "kx_xb_units",
+               "kx_xb_merge", "kc_xb_dense", "kx_mb_compact", "kx_partition", "kx_merge", "kx_piece_hist",
+               "kx_pack_scatter", "kx_mb_hist", "kx_mb_scatter", "kx_mb_merge")
+
 C4_GENOME, C4_COV = 500_000_000, 30.0 / 8
 
 
@@ -531,13 +537,16 @@ def scale_leg(D, reps=2):
             import hga_dist
             ex4 = hga_dist.OwnerExchange(c4)
         step = (lambda: dist_count_step(ex4)) if ex4 else (lambda: count_step(c4))
+        c4_local_inst = 0
+        if ex4:   # this rank's own instances (the local count), for the conservation invariant
+            c4.count_run(1)
+            c4_local_inst = c4.count_stats().instances
         step()   # warm-up (allocations)
         c4.profile(True)
         c4.profile_reset()
         step()
         names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_split3", "kc_count", "kc_spec_hist", "kc_select",
-                 "kx_piece_hist", "kx_pack_scatter", "kx_mb_hist", "kx_mb_scatter", "kx_mb_merge", "kx_mb_compact",
-                 "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
+                 *XCH_KERNELS, "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
         ker = {nm: round(c4.profile_get(nm)[0], 3) for nm in names if c4.profile_get(nm)[1]}
         c4.profile(False)
         D.barrier()
@@ -549,6 +558,25 @@ def scale_leg(D, reps=2):
         D.barrier()
         ms = D.max((time.perf_counter() - t0) / reps * 1e3)
         st = c4.count_stats()   # global after the exchange
+        export = None
+        if ex4:   # the full export of the last step in code order on every rank (re-partition + gather)
+            D.barrier()
+            t1 = time.perf_counter()
+            keys, flags = ex4.select(LOWER, UPPER)
+            D.barrier()
+            exp_ms = D.max((time.perf_counter() - t1) * 1e3)
+            k64 = keys.astype(np.uint64)
+            # size-independent invariants of the exchanged C4 result (its rows are not checked against
+            # the oracle at this size: parity unpinned here, the C2 shards carry the N > 1 parity check)
+            inv = {"export_ascending": bool(len(k64) < 2 or bool(np.all(k64[1:] > k64[:-1]))),
+                   "export_count_matches_select": int(len(keys)) == int(n_sel),
+                   "discriminative_matches_flags": int(flags.sum()) == int(n_disc),
+                   "global_instances_equal_sum_of_ranks": int(st.instances) == int(D.sum(float(c4_local_inst)))}
+            export = {"ms": round(exp_ms, 2), "keys": int(len(keys)),
+                      "note": "hga_count_select + hga_count_fetch_selected after the exchange: the owners' sorted "
+                              "selections re-partitioned by code range (one all-to-all), every rank's range "
+                              "gathered to every rank in rank order",
+                      "invariants": inv, "parity": "unpinned at C4 size (invariants only)"}
         return {"workload": f"C4 (configs[3]): {D.world} of the 8 rank shards of ART-like 30x reads of a 2 x 500 Mbp "
                             "diploid (d=0.005), k=19, 2 files per shard; step = count_run + "
                             + ("hga_count_exchange (owner all-to-all) + " if ex4 else "")
@@ -557,7 +585,8 @@ def scale_leg(D, reps=2):
                 "instances": int(st.instances), "distinct_rows": int(st.distinct_rows),
                 "buckets": int(st.buckets), "max_split": int(st.max_split), "selected": int(n_sel),
                 "discriminative": int(n_disc), "ms_per_step": round(ms, 2),
-                "k_mers_per_s": round(st.instances / (ms * 1e-3), 1), "kernels_ms_rank0": ker}
+                "k_mers_per_s": round(st.instances / (ms * 1e-3), 1), "kernels_ms_rank0": ker,
+                **({"export": export} if export else {})}
     finally:
         c4.close()
 
@@ -636,8 +665,7 @@ def main():
     stats = {"bytes": st.bytes, "instances": st.instances, "rows": st.distinct_rows, "files": 2}
     # 1) untimed profiled pass: per-kernel breakdown (events around every launch)
     names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
-             "kx_partition", "kx_piece_hist", "kx_pack_scatter", "kx_merge", "kx_mb_hist", "kx_mb_scatter",
-             "kx_mb_merge", "kx_mb_compact", "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
+             *XCH_KERNELS, "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
     ctx.profile(True)
     ctx.profile_reset()
     for _ in range(args.steps):
@@ -696,6 +724,16 @@ def main():
                               "achieved": round(pipe_gbs, 1), "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)},
         "kernels_ms_per_step": {k: round(v["ms_per_step"], 4) for k, v in kernels.items()},
     }
+    if ex:   # the full export of the last timed step in code order on every rank
+        D.barrier()
+        t1 = time.perf_counter()
+        ek, ef = ex.select(LOWER, UPPER)
+        D.barrier()
+        result["export"] = {"ms": round(D.max((time.perf_counter() - t1) * 1e3), 3), "keys": int(len(ek)),
+                            "discriminative": int(ef.sum()),
+                            "note": "select + fetch after the exchange: owners' sorted selections re-partitioned by "
+                                    "code range (one all-to-all of the export), ranges gathered in rank order"}
+        del ek, ef
     if ex and not args.no_check:   # the state of the last timed step: the exchanged global count
         result["parity"] = dist_parity(ctx, D, min(16 * D.world, os.cpu_count() or 16))
 

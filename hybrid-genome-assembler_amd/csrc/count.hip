@@ -2439,9 +2439,10 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     uint32_t* flag = reinterpret_cast<uint32_t*>(sb + cap * 8);
     const bool flag_bit = s.k <= 31;   // the discriminative flag rides in key bit 63
     const int bits = 2 * s.k;
-    // export sort: one MSD pass over the span the kept keys actually occupy (an owner's range on a
-    // multi-GPU run, the whole code space on one) + per-segment LDS sorts (sort_export_u64) when the
-    // flag rides in the key; kc_select counts the kept keys by the top 12 bits of the code
+    // export sort: one MSD pass over the span the kept keys actually occupy (the whole code space:
+    // hash-bucket owners' keys also cover every code; the re-partition by code range comes after,
+    // comm.hip count_export_repartition) + per-segment LDS sorts (sort_export_u64) when the flag rides
+    // in the key; kc_select counts the kept keys by the top 12 bits of the code
     const bool msd = flag_bit && bits >= 16 && s.rows >= (1u << 15);
     const uint64_t chunks = blocks_for(std::max<uint64_t>(s.rows, 1), NT_H * SEL_R);
     if (!s.sel_grid) {   // one resident round of workgroups: a second, partial round would run alone

@@ -1,10 +1,13 @@
 """Multi-GPU counting from Python: a thin caller of the C ABI's communicator.
 
-SURVEY.md §8(e): every rank counts its contiguous shard of every file; the merged rows are
-range-partitioned by canonical code and exchanged once (all-to-all over xGMI); each owner sums
-what it received and applies the per-file `--bc` drop (src/occurrences/run_jellyfish.sh:3-6).  All of
-that runs inside libhga (include/hga.h: hga_comm_init / hga_comm_init_host, hga_count_exchange); the
-count queries of the ctx then answer for the whole input (JellyfishOccurrenceReader.cpp:63-135).
+SURVEY.md §8(e): every rank counts its contiguous shard of every file with min 1; the rows travel once
+(all-to-all over xGMI) to hash-bucket owners — owner o holds a range of the counting hash's top bits,
+the pieces come out of the count kernel already grouped by bucket; each owner sums what
+it received and applies the per-file `--bc` drop (src/occurrences/run_jellyfish.sh:3-6).  The count
+queries of the ctx then answer for the whole input (JellyfishOccurrenceReader.cpp:63-135): the
+histogram is the owners' bins summed; the export, rows and dumps are re-partitioned by canonical-code
+range (one all-to-all of the export itself) and come out as the ranks' ranges in rank order.  All of
+that runs inside libhga (include/hga.h: hga_comm_init / hga_comm_init_host, hga_count_exchange).
 
 This module only sets the communicator up from a torch.distributed process group:
   backend "nccl" (RCCL): the library's own RCCL communicator over xGMI, its unique id broadcast

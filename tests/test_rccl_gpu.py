@@ -76,18 +76,22 @@ def test_rccl_one_rank_lookup_and_connections_gather(monkeypatch, self_p2p):
 
 def _heavy_streams():
     """make_streams plus one k-mer repeated past 65536 instances in a file: its bucket goes to the
-    generic count kernel (count.hip kc_count), which does not emit exchange pieces."""
+    generic count kernel (count.hip kc_count), which emits its exchange pieces as kc_count_s does
+    (the XbEmit branch), so the exchange still takes the count_xb_pack fast path."""
     a, b = make_streams()
     return [a + b"\n".join([b"A" * 60] * 1800) + b"\n", b]
 
 
-@pytest.mark.parametrize("heavy", [False, True])
+@pytest.mark.parametrize("heavy,generic", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("k", [13, 19])
-def test_local_queries_of_an_exchange_count(monkeypatch, k, heavy):
+def test_local_queries_of_an_exchange_count(monkeypatch, k, heavy, generic):
     """With a communicator attached, count_run(ctx, 1) writes exchange pieces instead of dense rows
-    (count.hip XbEmit); local queries before the exchange rebuild the rows from them (kc_xb_dense),
-    and the exchange of a count with a generic-kernel bucket bins its rows itself."""
+    (count.hip XbEmit, both count kernels); local queries before the exchange rebuild the rows from them
+    (kc_xb_dense).  generic: HGA_XB_GENERIC turns the emission off, so the sender bins its dense rows
+    itself (exchange.hip kx_xb_hist / kx_xb_scatter, the path of cached dump rows)."""
     monkeypatch.setenv("HGA_FB_MIN", "10")   # buckets fine enough for the emission
+    if generic:
+        monkeypatch.setenv("HGA_XB_GENERIC", "1")
     streams = _heavy_streams() if heavy else make_streams()
     ref1 = oracle.count_pipeline(streams, k, 3, 40, min_count=1)
     ref2 = oracle.count_pipeline(streams, k, 3, 40)
