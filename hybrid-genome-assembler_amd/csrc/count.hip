@@ -33,6 +33,9 @@
 #include "hga_internal.hpp"
 #include "kmer_dev.hpp"
 
+#ifndef HGA_B1_NOFB
+#define HGA_B1_NOFB 0   // timing comparison: kc_bin1 without the compile-time fine-bucket bits
+#endif
 #ifndef HGA_B1_BRANCHFREE
 #define HGA_B1_BRANCHFREE 0   // 1: kc_bin1 ranks every window (invalid ones into per-lane dummy counters)
 #endif
@@ -179,7 +182,9 @@ struct BinFile {
 // K > 0: k known at compile time (the usual k of a run): the window mask, the run-of-k validity
 // doubling and the mix's mask and shift fold to constants — with a runtime k those uniform values
 // spill out of the SGPR file (v_readlane per use) and runs_of is a chain of uniform selects.
-template <class E1, int K = 0>
+// FB > 0 (with K): the fine-bucket bits known at compile time too (C2-sized inputs: 12), so region and
+// bucket are constant shifts of the mixed key (no 64-bit shift by a uniform register per window).
+template <class E1, int K = 0, int FB = 0>
 __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __restrict__ files, uint32_t F,
                                                 uint64_t st_pos, KP kp,
                                                 Blk* __restrict__ table, uint64_t table_cap,
@@ -280,7 +285,9 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
         for (int j = 0; j < P_B; ++j) {
             const uint64_t h = mix_fwd(frame_canon<P_B>(f, j, wmask), mx);
             // (k < 32: h < 4^k, so a shift by the full width 2k already gives region / bucket 0)
-            dd[j] = K && K < 32 ? (uint32_t)(h >> kp.r1bits) : region_of(h, kp);
+            constexpr int R1B = 2 * K - (FB < MAX_FB1 ? FB : MAX_FB1), RB = 2 * K - FB;
+            const uint32_t r1s = K && FB ? (uint32_t)R1B : kp.r1bits, rbs = K && FB ? (uint32_t)RB : kp.rbits;
+            dd[j] = K && K < 32 ? (uint32_t)(h >> r1s) : region_of(h, kp);
             // (u32 elements of a k with 2k - MAX_FB1 >= 32: r1bits == 32, the truncation is the mask)
             constexpr bool trunc = K && sizeof(E1) == 4 && 2 * K - MAX_FB1 >= 32;
             ee[j] = trunc ? (E1)h : (E1)(h & kp.r1mask);
@@ -294,9 +301,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
                 rk[j] = ~0u;   // invalid window: staged into this lane's dummy slot (no mask kept live)
                 if ((wm >> j) & 1u) {
                     rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
-#ifndef HGA_B1_NOFHIST
-                    atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp)], 1u);
-#endif
+                    atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> rbs) : bucket_of(h, kp)], 1u);
                 }
             }
         }
@@ -2053,16 +2058,17 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     // B1: level-1 binning of every file into pool blocks + per-workgroup fine histograms
     if (W) {
         c->launch("kc_bin1", [&] {
-#define HGA_BIN1(E1T, KK)                                                                                   \
-    hipLaunchKernelGGL((kc_bin1<E1T, KK>), dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table, table_cap, \
+#define HGA_BIN1(E1T, KK, FBB)                                                                              \
+    hipLaunchKernelGGL((kc_bin1<E1T, KK, FBB>), dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table, table_cap, \
                        pool_cap, static_cast<E1T*>(binned1), wcnt, nblk, gstat)
             // compile-time k for the k of the configs (C1-C4: 19; C5: 15, 17, 19, 21)
-            if (e1_32 && kp.k == 19) HGA_BIN1(uint32_t, 19);
-            else if (e1_32 && kp.k == 17) HGA_BIN1(uint32_t, 17);
-            else if (e1_32 && kp.k == 15) HGA_BIN1(uint32_t, 15);
-            else if (e1_32) HGA_BIN1(uint32_t, 0);
-            else if (kp.k == 21) HGA_BIN1(uint64_t, 21);
-            else HGA_BIN1(uint64_t, 0);
+            if (e1_32 && kp.k == 19 && kp.fb == 12 && !HGA_B1_NOFB) HGA_BIN1(uint32_t, 19, 12);
+            else if (e1_32 && kp.k == 19) HGA_BIN1(uint32_t, 19, 0);
+            else if (e1_32 && kp.k == 17) HGA_BIN1(uint32_t, 17, 0);
+            else if (e1_32 && kp.k == 15) HGA_BIN1(uint32_t, 15, 0);
+            else if (e1_32) HGA_BIN1(uint32_t, 0, 0);
+            else if (kp.k == 21) HGA_BIN1(uint64_t, 21, 0);
+            else HGA_BIN1(uint64_t, 0, 0);
 #undef HGA_BIN1
         });
         c->check_launch("kc_bin1");

@@ -30,6 +30,7 @@
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
+#include <memory>
 #include <vector>
 
 namespace {
@@ -232,19 +233,22 @@ int64_t or_count_stream_mt(const char* s, uint64_t n, int k, uint32_t min_count,
 // --- A3 + A4, multi-threaded over all files: merged rows of the whole count stage ----------
 // The same result as or_count_stream per file followed by or_merge, computed by range
 // partitioning (so no heap merge is needed): threads extract every canonical k-mer of their
-// slice of a file (cut at separator bytes) into P code-range partitions; then, one partition at
-// a time (threads take partitions from a shared counter), each file's codes are sorted and
-// run-length counted (count < min_count dropped: `--bc`, run_jellyfish.sh:3-6) and the F sorted
-// per-file lists are merged into rows (counts[f] = 0 where file f lacks the k-mer,
-// JellyfishOccurrenceReader.cpp:63-86).  Partitions are ascending code ranges, so their rows
-// concatenate in ascending order.  Output: keys[rows], counts[rows * F] row-major.
+// slice of a file (cut at separator bytes) and count them per code-range partition; a prefix sum
+// gives every (partition, thread) its place in one array per file, and a second extraction pass
+// scatters the codes there (no per-thread bins: threads x partitions vectors did not scale to 256
+// threads).  Then, one partition at a time (threads take partitions from a shared counter), each
+// file's codes are sorted and run-length counted (count < min_count dropped: `--bc`,
+// run_jellyfish.sh:3-6) and the F sorted per-file lists are merged into rows (counts[f] = 0 where
+// file f lacks the k-mer, JellyfishOccurrenceReader.cpp:63-86).  Partitions are ascending code
+// ranges, so their rows concatenate in ascending order.  Output: keys[rows], counts[rows * F]
+// row-major.
 int64_t or_count_files_mt(int F, const char* const* s, const uint64_t* n, int k, uint32_t min_count,
                           int threads, uint64_t** keys, uint32_t** counts) {
     if (k > 32 || k < 1 || F < 1) return -1;
     if (threads < 1) threads = 1;
     const int nb = 2 * k;
     const int tb = nb < 16 ? nb : 16;              // top bits that pick the partition
-    const int P = nb <= 8 ? 1 : 512;
+    const int P = nb <= 8 ? 1 : (nb <= 12 ? 64 : 4096);
     // canonical = min(fwd, rc) of uniform codes has mass 1 - (1 - x)^2 below x: equal-mass
     // ranges, aligned to the top tb bits (any ascending ranges give the same rows)
     std::vector<uint16_t> part_of(1u << tb);
@@ -254,9 +258,9 @@ int64_t or_count_files_mt(int F, const char* const* s, const uint64_t* n, int k,
         part_of[t] = (uint16_t)std::min(p, P - 1);
     }
     const int shift = nb - tb;
-    // bins[f][t][p]
-    std::vector<std::vector<std::vector<std::vector<uint64_t>>>> bins(
-        F, std::vector<std::vector<std::vector<uint64_t>>>(threads, std::vector<std::vector<uint64_t>>(P)));
+    // codes[f]: file f's codes grouped by partition; start[f][p] = partition p's first
+    std::vector<std::unique_ptr<uint64_t[]>> codes(F);
+    std::vector<std::vector<uint64_t>> start(F, std::vector<uint64_t>(P + 1, 0));
     for (int f = 0; f < F; ++f) {
         std::vector<uint64_t> cut(threads + 1, 0);
         cut[threads] = n[f];
@@ -266,12 +270,35 @@ int64_t or_count_files_mt(int F, const char* const* s, const uint64_t* n, int k,
             while (c < n[f] && jf_code((unsigned char)s[f][c]) >= 0) ++c;
             cut[t] = c;
         }
+        std::vector<uint64_t> cnt((size_t)threads * P, 0);   // [t][p]
+        {
+            std::vector<std::thread> th;
+            for (int t = 0; t < threads; ++t)
+                th.emplace_back([&, f, t] {
+                    uint64_t* C = cnt.data() + (size_t)t * P;
+                    for_each_jf_kmer(s[f] + cut[t], cut[t + 1] - cut[t], k,
+                                     [&](uint64_t c, uint64_t) { ++C[part_of[c >> shift]]; });
+                });
+            for (auto& x : th) x.join();
+        }
+        uint64_t run = 0;   // partition-major, threads in order
+        for (int p = 0; p < P; ++p) {
+            start[f][p] = run;
+            for (int t = 0; t < threads; ++t) {
+                const uint64_t c = cnt[(size_t)t * P + p];
+                cnt[(size_t)t * P + p] = run;
+                run += c;
+            }
+        }
+        start[f][P] = run;
+        codes[f].reset(new uint64_t[std::max<uint64_t>(run, 1)]);
+        uint64_t* out = codes[f].get();
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t)
             th.emplace_back([&, f, t] {
-                auto& B = bins[f][t];
+                uint64_t* O = cnt.data() + (size_t)t * P;
                 for_each_jf_kmer(s[f] + cut[t], cut[t + 1] - cut[t], k,
-                                 [&](uint64_t c, uint64_t) { B[part_of[c >> shift]].push_back(c); });
+                                 [&](uint64_t c, uint64_t) { out[O[part_of[c >> shift]]++] = c; });
             });
         for (auto& x : th) x.join();
     }
@@ -282,22 +309,17 @@ int64_t or_count_files_mt(int F, const char* const* s, const uint64_t* n, int k,
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t)
             th.emplace_back([&] {
-                std::vector<uint64_t> v;
                 std::vector<std::vector<std::pair<uint64_t, uint32_t>>> runs(F);
                 for (int p; (p = next.fetch_add(1)) < P;) {
                     for (int f = 0; f < F; ++f) {
-                        v.clear();
-                        for (int t2 = 0; t2 < threads; ++t2) {
-                            auto& b = bins[f][t2][p];
-                            v.insert(v.end(), b.begin(), b.end());
-                            std::vector<uint64_t>().swap(b);
-                        }
-                        std::sort(v.begin(), v.end());
+                        uint64_t* v = codes[f].get() + start[f][p];
+                        const size_t m = start[f][p + 1] - start[f][p];
+                        std::sort(v, v + m);
                         auto& r = runs[f];
                         r.clear();
-                        for (size_t i = 0; i < v.size();) {
+                        for (size_t i = 0; i < m;) {
                             size_t j = i + 1;
-                            while (j < v.size() && v[j] == v[i]) ++j;
+                            while (j < m && v[j] == v[i]) ++j;
                             if (j - i >= min_count) r.push_back({v[i], (uint32_t)(j - i)});
                             i = j;
                         }
@@ -325,6 +347,7 @@ int64_t or_count_files_mt(int F, const char* const* s, const uint64_t* n, int k,
             });
         for (auto& x : th) x.join();
     }
+    codes.clear();
     size_t total = 0;
     for (auto& x : pk) total += x.size();
     uint64_t* ok = (uint64_t*)std::malloc(std::max<size_t>(1, total * 8));
