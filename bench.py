@@ -665,7 +665,7 @@ def main():
     stats = {"bytes": st.bytes, "instances": st.instances, "rows": st.distinct_rows, "files": 2}
     # 1) untimed profiled pass: per-kernel breakdown (events around every launch)
     names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select",
-             *XCH_KERNELS, "radix_upsweep", "radix_downsweep", "radix_segsort", "scan")
+             *XCH_KERNELS, "radix_upsweep", "radix_downsweep", "bx_colscan", "bx_scatter", "radix_segsort", "scan")
     ctx.profile(True)
     ctx.profile_reset()
     for _ in range(args.steps):

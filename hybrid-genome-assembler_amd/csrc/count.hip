@@ -1886,6 +1886,159 @@ __global__ void __launch_bounds__(256) kc_sel_span(const uint32_t* __restrict__ 
     publish(sum);
 }
 
+// ---- bucketed export sort (moderate exports, flag in key bit 63): the kept keys go straight from
+// kc_select's per-workgroup regions to their 12-bit digit segments — deterministic offsets from the
+// per-workgroup digit counts (column scan), LDS-ranked inside a workgroup — and every segment of at
+// most BX_MAX keys is sorted by one wave in registers (bitonic, 64 x R keys).  Replaces the compaction,
+// the MSD onesweep pass and the 256 one-workgroup LDS segment sorts (C2: 0.16 -> ~0.09 ms); exports
+// with a larger segment keep that path (sort_export_u64).
+constexpr uint32_t BX_MAX = 1024;
+// One 1024-thread workgroup: dbase[d] = exclusive scan of the digit totals hist[d]; stat[0] / [1] =
+// kept / discriminative keys (the per-workgroup counts wcnt), stat[2] = the largest digit total;
+// stat[0..3] also into the host's mapped staging hstat.
+__global__ void __launch_bounds__(1024) kc_bx_prep(const uint32_t* __restrict__ hist, const unsigned long long* __restrict__ wcnt,
+                                                   uint32_t grid, uint32_t* __restrict__ dbase,
+                                                   unsigned long long* __restrict__ stat,
+                                                   unsigned long long* __restrict__ hstat) {
+    __shared__ uint32_t ws[1024 / 64 + 1];
+    __shared__ unsigned long long red[3][16];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t h[4], sum = 0, mx = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        h[q] = hist[4 * t + q];
+        sum += h[q];
+        mx = max(mx, h[q]);
+    }
+    uint32_t tot;
+    uint32_t o = block_excl_scan<1024>(sum, ws, &tot);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        dbase[4 * t + q] = o;
+        o += h[q];
+    }
+    unsigned long long k = 0, d = 0, m = mx;
+    for (uint32_t i = t; i < grid; i += 1024) {
+        k += wcnt[2 * i];
+        d += wcnt[2 * i + 1];
+    }
+#pragma unroll
+    for (int s2 = 32; s2; s2 >>= 1) {
+        k += __shfl_xor(k, s2, 64);
+        d += __shfl_xor(d, s2, 64);
+        m = max(m, (unsigned long long)__shfl_xor(m, s2, 64));
+    }
+    if (lane == 0) {
+        red[0][wave] = k;
+        red[1][wave] = d;
+        red[2][wave] = m;
+    }
+    __syncthreads();
+    if (t < 4) {
+        unsigned long long v = 0;
+        for (int w = 0; w < 16; ++w) v = t == 2 ? max(v, red[2][w]) : v + (t < 2 ? red[t][w] : 0ull);
+        stat[t] = v;
+        hstat[t] = v;
+    }
+}
+// off[w][d] = dbase[d] + sum over workgroups w' < w of their digit-d counts (rows[w'][d]); one
+// workgroup per 16 digits, 16 row groups of threads.
+__global__ void __launch_bounds__(256) kc_bx_colscan(const uint32_t* __restrict__ rows, uint32_t n_rows,
+                                                     const uint32_t* __restrict__ dbase, uint32_t* __restrict__ off) {
+    __shared__ uint32_t part[16][17];
+    const uint32_t dl = threadIdx.x & 15, rg = threadIdx.x >> 4, d = blockIdx.x * 16 + dl;
+    const uint32_t per = (n_rows + 15) / 16, r0 = rg * per, r1 = min(n_rows, r0 + per);
+    uint32_t s2 = 0;
+    for (uint32_t r = r0; r < r1; ++r) s2 += rows[(uint64_t)r * SEL_HB + d];
+    part[rg][dl] = s2;
+    __syncthreads();
+    uint32_t base = dbase[d];
+    for (uint32_t g = 0; g < rg; ++g) base += part[g][dl];
+    for (uint32_t r = r0; r < r1; ++r) {
+        off[(uint64_t)r * SEL_HB + d] = base;
+        base += rows[(uint64_t)r * SEL_HB + d];
+    }
+}
+// Workgroup w of kc_select's grid: its kept keys from its region to their digit segments (ranks
+// inside the workgroup by LDS atomics; a segment is fully sorted afterwards and keys are unique, so
+// the order inside it does not matter).
+__global__ void __launch_bounds__(256) kc_bx_scatter(const uint64_t* __restrict__ wkeys, uint64_t region,
+                                                     const unsigned long long* __restrict__ wcnt,
+                                                     const uint32_t* __restrict__ off, int hshift,
+                                                     uint64_t* __restrict__ out) {
+    __shared__ uint32_t cur[SEL_HB];
+    const uint32_t w = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < SEL_HB; i += 256) cur[i] = off[(uint64_t)w * SEL_HB + i];
+    __syncthreads();
+    const uint64_t n = wcnt[2 * w];
+    const uint64_t* __restrict__ src = wkeys + (uint64_t)w * region;
+    for (uint64_t j = threadIdx.x; j < n; j += 256) {
+        const uint64_t key = src[j];
+        const uint32_t pos = atomicAdd(&cur[(uint32_t)(key >> hshift) & (SEL_HB - 1)], 1u);
+        out[pos] = key;
+    }
+}
+// One wave per digit segment of at most BX_MAX keys: bitonic sort in registers by the code (the flag
+// in bit 63 moved below it: codes are unique, the flag never decides), padding sorts last.
+template <int R>
+__device__ __forceinline__ void bx_sort_seg(uint64_t* __restrict__ keys, uint32_t start, uint32_t len, uint32_t lane,
+                                            int bits) {
+    const uint64_t cm = bits >= 63 ? ~0ull >> 1 : (1ull << bits) - 1;
+    uint64_t v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint32_t i = lane * R + u;
+        const uint64_t k = i < len ? keys[start + i] : 0ull;
+        v[u] = i < len ? ((k & cm) << 1) | (k >> 63) : ~0ull;
+    }
+    bitonic_stage<R, 2>(v, lane);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint32_t i = lane * R + u;
+        if (i < len) keys[start + i] = (v[u] >> 1) | ((v[u] & 1ull) << 63);
+    }
+}
+// The same with u32 sort keys when the code bits below the digit and the flag fit (2k - 12 + 1 <= 32,
+// k <= 21): (low code bits << 1 | flag), the digit restored on the way out — half the registers and
+// compare-exchange work of the u64 form.
+template <int R>
+__device__ __forceinline__ void bx_sort_seg32(uint64_t* __restrict__ keys, uint32_t start, uint32_t len, uint32_t lane,
+                                              int bits, uint64_t dig) {
+    const int lb = bits - 12;   // code bits below the digit
+    const uint64_t lm = (1ull << lb) - 1;
+    uint32_t v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint32_t i = lane * R + u;
+        const uint64_t k = i < len ? keys[start + i] : 0ull;
+        v[u] = i < len ? (uint32_t)(((k & lm) << 1) | (k >> 63)) : ~0u;
+    }
+    bitonic_stage<R, 2>(v, lane);
+    const uint64_t hi = dig << lb;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint32_t i = lane * R + u;
+        if (i < len) keys[start + i] = hi | (uint64_t)(v[u] >> 1) | ((uint64_t)(v[u] & 1u) << 63);
+    }
+}
+__global__ void __launch_bounds__(256) kc_bx_wsort(uint64_t* __restrict__ keys, const uint32_t* __restrict__ hist,
+                                                   const uint32_t* __restrict__ dbase, int bits) {
+    const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t len = hist[d], st = dbase[d];
+    if (len <= 1) return;
+    if (bits - 12 + 1 <= 32) {
+        if (len <= 64) bx_sort_seg32<1>(keys, st, len, lane, bits, d);
+        else if (len <= 256) bx_sort_seg32<4>(keys, st, len, lane, bits, d);
+        else if (len <= 512) bx_sort_seg32<8>(keys, st, len, lane, bits, d);
+        else bx_sort_seg32<16>(keys, st, len, lane, bits, d);   // len <= BX_MAX (checked by the host)
+        return;
+    }
+    if (len <= 64) bx_sort_seg<1>(keys, st, len, lane, bits);
+    else if (len <= 256) bx_sort_seg<4>(keys, st, len, lane, bits);
+    else if (len <= 512) bx_sort_seg<8>(keys, st, len, lane, bits);
+    else bx_sort_seg<16>(keys, st, len, lane, bits);   // len <= BX_MAX (checked by the host)
+}
+
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
@@ -2455,13 +2608,18 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
         int nb = 0;      // (C4 shard: 1024 workgroups at 3 per CU took two rounds)
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kc_select, NT_H, 0) != hipSuccess || nb < 1) nb = 1;
         s.sel_grid = (uint32_t)std::min<uint64_t>((uint64_t)nb * c->num_cu, HGA_SEL_GRID);
+        if (const char* e = std::getenv("HGA_SEL_GRID_X")) s.sel_grid = std::max(1, std::atoi(e));   // tuning
     }
     const uint32_t cpw = (uint32_t)blocks_for(chunks, s.sel_grid);   // chunks per workgroup
     const unsigned grid = (unsigned)blocks_for(chunks, cpw);
     const uint64_t region = (uint64_t)cpw * NT_H * SEL_R;
     const size_t hb = (size_t)SEL_HB * 4;
-    char* tb = static_cast<char*>(s.sel_tmp.ensure(64 + hb + 1024 + (size_t)grid * 16 + (msd ? (size_t)grid * hb : 0)));
-    auto* wcnt = reinterpret_cast<unsigned long long*>(tb + 64 + hb + 1024 + (msd ? (size_t)grid * hb : 0));
+    // [stat 64 | dhist | dig256 1 KB | dhist_rows (msd) | wcnt | dbase (msd) | off (msd)]
+    const size_t rows_b = msd ? (size_t)grid * hb : 0;
+    char* tb = static_cast<char*>(s.sel_tmp.ensure(64 + hb + 1024 + rows_b + (size_t)grid * 16 + (msd ? hb + rows_b : 0)));
+    auto* wcnt = reinterpret_cast<unsigned long long*>(tb + 64 + hb + 1024 + rows_b);
+    uint32_t* bx_dbase = msd ? reinterpret_cast<uint32_t*>(tb + 64 + hb + 1024 + rows_b + (size_t)grid * 16) : nullptr;
+    uint32_t* bx_off = msd ? bx_dbase + SEL_HB : nullptr;
     char* wt = static_cast<char*>(s.sel_wtmp.ensure((size_t)grid * region * (flag_bit ? 8 : 12) + 64));
     uint64_t* wkeys = reinterpret_cast<uint64_t*>(wt);
     uint32_t* wflag = reinterpret_cast<uint32_t*>(wt + (size_t)grid * region * 8);
@@ -2478,30 +2636,62 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
             hipLaunchKernelGGL(kc_select, dim3(grid), dim3(NT_H), 0, c->stream, s.rows_key.as<uint64_t>(),
                                s.rows_cnt.as<uint32_t>(), s.rows, s.rows_cap, s.n_files, lower, upper, wkeys, wflag,
                                flag_bit, cpw, wcnt, dhist_rows, bits - 12, stat, msd ? dhist : nullptr);
-            hipLaunchKernelGGL(kc_sel_compact, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys,
-                               (const uint32_t*)wflag, region, (const unsigned long long*)wcnt, grid, out, flag,
-                               flag_bit, stat);
-            if (msd) {
+            if (msd) {   // the digit totals, their scan, the counts and the largest digit (kc_bx_prep)
                 hipLaunchKernelGGL(kc_dhist_reduce, dim3(SEL_HB / 256, (grid + 31) / 32), dim3(256), 0, c->stream,
                                    dhist_rows, grid, dhist);
-                hipLaunchKernelGGL(kc_sel_span, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)dhist,
-                                   reinterpret_cast<uint32_t*>(stat + 4), dig256, (const unsigned long long*)stat,
-                                   c->pinned_sel.dev(hs), c->pinned_sel.dev(h256));
+                hipLaunchKernelGGL(kc_bx_prep, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)dhist,
+                                   (const unsigned long long*)wcnt, grid, bx_dbase, stat, c->pinned_sel.dev(hs));
+            } else {
+                hipLaunchKernelGGL(kc_sel_compact, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys,
+                                   (const uint32_t*)wflag, region, (const unsigned long long*)wcnt, grid, out, flag,
+                                   flag_bit, stat);
             }
         });
         c->check_launch("kc_select");
     }
-    // one synchronisation: counts, the MSD digit span and its 256 digit counts together (kc_sel_span
-    // writes them into the mapped staging; without it, one copy)
+    // one synchronisation for the counts (kc_bx_prep writes them into the mapped staging; else a copy)
     if (!(s.rows && msd)) HGA_HIP(hipMemcpyAsync(hs, stat, 64, hipMemcpyDeviceToHost, c->stream));
     if (before_sync) (*before_sync)(stat);
     c->sync();
     const uint64_t n = hs[0];
-    if (msd && n > 1) {
-        // digit = (code >> shift) - dbase over the occupied 12-bit bins [lo, hi], <= 256 digits
+    const bool bx = msd && n > 1 && hs[2] <= BX_MAX && !std::getenv("HGA_BX_OFF");
+    if (bx) {   // bucketed export sort: digit segments straight from the workgroup regions, one wave each
+        c->launch("bx_colscan", [&] {
+            hipLaunchKernelGGL(kc_bx_colscan, dim3(SEL_HB / 16), dim3(256), 0, c->stream, (const uint32_t*)dhist_rows,
+                               grid, (const uint32_t*)bx_dbase, bx_off);
+        });
+        c->launch("bx_scatter", [&] {
+            hipLaunchKernelGGL(kc_bx_scatter, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys, region,
+                               (const unsigned long long*)wcnt, (const uint32_t*)bx_off, bits - 12, out);
+        });
+        c->launch("radix_segsort", [&] {
+            hipLaunchKernelGGL(kc_bx_wsort, dim3(SEL_HB / 4), dim3(256), 0, c->stream, out, (const uint32_t*)dhist,
+                               (const uint32_t*)bx_dbase, bits);
+        });
+        c->check_launch("kc_bx_wsort");
+    } else if (msd && n > 1) {
+        // compaction, then the MSD pass: digit = (code >> shift) - dbase over the occupied 12-bit bins
+        // [lo, hi], <= 256 digits (kc_sel_span: span into stat + 4, the 256 digit counts into dig256)
+        c->launch("kc_select", [&] {
+            hipLaunchKernelGGL(kc_sel_compact, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys,
+                               (const uint32_t*)wflag, region, (const unsigned long long*)wcnt, grid, out, flag,
+                               flag_bit, stat);
+            hipLaunchKernelGGL(kc_sel_span, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)dhist,
+                               reinterpret_cast<uint32_t*>(stat + 4), dig256, (const unsigned long long*)stat,
+                               c->pinned_sel.dev(hs), c->pinned_sel.dev(h256));
+        });
+        c->check_launch("kc_sel_span");
+        c->sync();
         const uint32_t* span = reinterpret_cast<const uint32_t*>(hs + 4);   // written at stat + 4
         const int shift = bits - 12 + (int)span[2];
         sort_export_u64(c, out, n, shift, span[3], dig256, h256, s.scratch);
+    } else if (msd && n == 1) {
+        c->launch("kc_select", [&] {
+            hipLaunchKernelGGL(kc_sel_compact, dim3(grid), dim3(256), 0, c->stream, (const uint64_t*)wkeys,
+                               (const uint32_t*)wflag, region, (const unsigned long long*)wcnt, grid, out, flag,
+                               flag_bit, stat);
+        });
+        c->check_launch("kc_sel_compact");
     } else {
         radix_sort_u64(c, out, flag_bit ? nullptr : flag, n, bits, s.scratch);
     }

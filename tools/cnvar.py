@@ -30,7 +30,11 @@ names = ("cn_wave", "cn_local", "cn_global", "cn_sort", "radix_upsweep", "radix_
 print(json.dumps({"ms": round(dt * 1e3, 3), "n": int(n), "checksum": cs,
                   "k": {m: round(c2.profile_get(m)[0] / 5, 4) for m in names}}))
 ''' % (ROOT, os.path.join(ROOT, "hybrid-genome-assembler_amd"))
-for so in sys.argv[1:]:
-    out = subprocess.run([sys.executable, "-c", CODE], env=dict(os.environ, HGA_LIB=so), capture_output=True,
-                         text=True, timeout=300)
-    print(os.path.basename(so), (out.stdout.strip().splitlines() or [out.stderr[-400:]])[-1], flush=True)
+for arg in sys.argv[1:]:   # path.so or path.so@ENV=V,ENV2=V
+    so, _, envs = arg.partition("@")
+    env = dict(os.environ, HGA_LIB=so)
+    for kv in filter(None, envs.split(",")):
+        env[kv.partition("=")[0]] = kv.partition("=")[2]
+    out = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, timeout=300)
+    print(os.path.basename(so) + ("@" + envs if envs else ""), (out.stdout.strip().splitlines() or [out.stderr[-400:]])[-1],
+          flush=True)

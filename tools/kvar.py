@@ -23,7 +23,7 @@ ctx.profile(True); ctx.profile_reset()
 import time; ctx.sync(); t0 = time.perf_counter()
 for _ in range(10): n = step()
 ctx.sync(); dt = (time.perf_counter() - t0) / 10
-names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select", "radix_upsweep", "radix_downsweep", "radix_segsort")
+names = ("kc_init", "kc_bin1", "kc_layout", "kc_rebin", "kc_count", "kc_spec_hist", "kc_select", "radix_upsweep", "radix_downsweep", "bx_colscan", "bx_scatter", "radix_segsort")
 try:
     hs = int(ctx.spec_hist(bench.THRESHOLDS)[:, 2].sum())
 except hga.HgaError:
