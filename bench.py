@@ -476,18 +476,27 @@ def ingest_leg(ga, gb, threads):
         cli = os.path.join(ROOT, "hybrid-genome-assembler_amd", "bin", "jf_occurrences")
         if os.path.exists(cli):
             import subprocess
-            env = dict(os.environ, HGA_PLOT_CMD="cat > /dev/null")
+            env = dict(os.environ, HGA_PLOT_CMD="cat > /dev/null", HGA_TIMING="1")
             t0 = time.perf_counter()
             r = subprocess.run([cli, *paths, "-k", str(K)], input=f"{LOWER} {UPPER} 1\n", text=True,
                                capture_output=True, cwd=d, env=env, timeout=300)
             dt = time.perf_counter() - t0
             exp = os.path.join(d, f"{K}-mers_{LOWER}_{UPPER}_100%.txt")
+            phases = {}
+            for line in r.stderr.splitlines():   # "hga-timing <phase> <ms>" (HGA_TIMING=1)
+                f = line.split()
+                if len(f) == 3 and f[0] == "hga-timing":
+                    phases[f[1]] = float(f[2])
             out["cli_jf_occurrences"] = {
                 "argv": f"jf_occurrences mg1655.fq uti89.fq -k {K}  (stdin: {LOWER} {UPPER} 1)",
-                "rc": r.returncode, "wall_s": round(dt, 3),
+                "rc": r.returncode, "wall_s": round(dt, 3), "phases_ms": phases,
+                "dump_bytes": sum(os.path.getsize(p + f"_{K}-mers_sorted") for p in paths
+                                  if os.path.exists(p + f"_{K}-mers_sorted")),
                 "exported_lines": sum(1 for _ in open(exp)) if r.returncode == 0 and os.path.exists(exp) else None,
-                "note": "one process: HIP init, FASTQ ingest, upload, count, the two per-file sorted dump "
-                        "caches written as text, histogram wire string, export file"}
+                "note": "one process: HIP init (on a thread, overlapped with the FASTQ ingest), ingest, upload, "
+                        "count, the two per-file sorted dump caches written as text (on a thread, overlapped "
+                        "with the histogram, plot and export), histogram wire string, export file; phases_ms "
+                        "from the CLI's HGA_TIMING=1 lines (main-thread wall time between marks)"}
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)

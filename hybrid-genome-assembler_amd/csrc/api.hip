@@ -266,10 +266,13 @@ hga_status hga_count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n
 hga_status hga_count_rows(hga_ctx* c, uint64_t** keys, uint32_t** counts, uint64_t* rows) {
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(keys && counts && rows, HGA_ERR_INVALID, "null pointer");
+        if (!c->count.dist) {   // sorted on the device, copied straight into the returned buffers
+            hga::count_rows_to(c, keys, counts, rows);
+            return HGA_OK;
+        }
         std::vector<uint64_t> k;
         std::vector<uint32_t> v;
-        if (c->count.dist) hga::count_rows_global(c, -1, k, v);
-        else hga::count_rows(c, -1, k, v);
+        hga::count_rows_global(c, -1, k, v);
         *keys = host_dup(k.data(), k.size());
         *counts = host_dup(v.data(), v.size());
         *rows = k.size();

@@ -2754,6 +2754,39 @@ void count_rows_device(hga_ctx* c, DevBuf& keys, DevBuf& counts) {
     c->sync();   // tv is freed on return
 }
 
+// All merged rows ascending into malloc'ed buffers (hga_count_rows): keys[rows], counts[rows][F].
+void count_rows_to(hga_ctx* c, uint64_t** keys, uint32_t** counts, uint64_t* n_rows) {
+    auto& s = c->count;
+    count_settle(c);
+    HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    count_dense(c);
+    const uint64_t rows = s.rows;
+    const uint32_t F = s.n_files;
+    auto* hk = static_cast<uint64_t*>(std::malloc(std::max<uint64_t>(rows, 1) * 8));
+    auto* hc = static_cast<uint32_t*>(std::malloc(std::max<uint64_t>(rows, 1) * 4ull * F));
+    if (!hk || !hc) {
+        std::free(hk);
+        std::free(hc);
+        throw std::bad_alloc();
+    }
+    try {
+        if (rows) {
+            DevBuf tk, tc;
+            count_rows_device(c, tk, tc);
+            HGA_HIP(hipMemcpyAsync(hk, tk.p, rows * 8, hipMemcpyDeviceToHost, c->stream));
+            HGA_HIP(hipMemcpyAsync(hc, tc.p, rows * 4ull * F, hipMemcpyDeviceToHost, c->stream));
+            c->sync();
+        }
+    } catch (...) {
+        std::free(hk);
+        std::free(hc);
+        throw;
+    }
+    *keys = hk;
+    *counts = hc;
+    *n_rows = rows;
+}
+
 // All merged rows ascending (file < 0), or one file's dump rows (file >= 0).
 void count_rows(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
     auto& s = c->count;

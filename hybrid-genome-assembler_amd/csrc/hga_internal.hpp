@@ -313,6 +313,8 @@ void count_select_global(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n, 
 void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags);
 // this rank's code range of the global export on the device (count.sel_rep), its size (comm.hip)
 uint64_t count_export_repartition(hga_ctx* c);
+// all merged rows ascending into malloc'ed buffers (hga_count_rows, count.hip)
+void count_rows_to(hga_ctx* c, uint64_t** keys, uint32_t** counts, uint64_t* n_rows);
 // the merged rows ascending on the device (count.hip): keys[rows], counts row-major [rows][F]
 void count_rows_device(hga_ctx* c, DevBuf& keys, DevBuf& counts);
 void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);

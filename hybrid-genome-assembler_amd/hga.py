@@ -127,6 +127,7 @@ HOST_SYMBOLS = {
     "hgh_fmt_double": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
     "hgh_hll_estimate": (C.c_double, [_u8p, C.c_int]),
     "hgh_set_threads": (None, [C.c_int]),
+    "hgh_write_kmer_dump": (C.c_int, [C.c_char_p, C.c_int, _u64p, _u32p, C.c_uint64]),
 }
 
 
@@ -520,6 +521,13 @@ def write_art_fastq(genome: bytes, name: str, n_reads: int, read_len: int, seed:
 
 def write_nanosim_fasta(genome: bytes, name: str, n_reads: int, seed: int, path: str):
     _hck(host().hgh_write_nanosim_fasta(genome, len(genome), name.encode(), n_reads, seed, path.encode()))
+
+
+def write_kmer_dump(path: str, k: int, keys, counts):
+    """The jf_occurrences dump cache writer ("KMER COUNT" lines, host/seqio.cpp write_kmer_dump)."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    counts = np.ascontiguousarray(counts, dtype=np.uint32)
+    _hck(host().hgh_write_kmer_dump(path.encode(), k, keys.ctypes.data_as(_u64p), counts.ctypes.data_as(_u32p), len(keys)))
 
 
 def set_host_threads(n: int):

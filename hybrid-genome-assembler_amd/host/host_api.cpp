@@ -45,6 +45,11 @@ void export_batch(const hgah::ReadBatch& b, char** seq, uint64_t* seq_len, char*
 extern "C" {
 
 const char* hgh_last_error(void) { return g_err.c_str(); }
+
+// The dump cache writer of jf_occurrences (seqio.cpp write_kmer_dump), for the tests.
+int hgh_write_kmer_dump(const char* path, int k, const uint64_t* keys, const uint32_t* counts, uint64_t n) {
+    return guard([&] { hgah::write_kmer_dump(path, k, keys, counts, n); });
+}
 void hgh_free(void* p) { std::free(p); }
 
 int hgh_gen_genome(uint64_t len, uint64_t seed, char** out) {

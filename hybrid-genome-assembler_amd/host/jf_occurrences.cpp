@@ -20,7 +20,12 @@
 // Without -k, k is chosen as the reference does (:40-44, KmerAnalysis.cpp:41-56): HyperLogLog
 // estimates for k = 11, 13, ... filled on the GPU (hga_hll_registers), printed per k.
 //
-// HGA_DEVICE selects the GPU (default 0); HGA_PLOT_CMD overrides the plot command.
+// HGA_DEVICE selects the GPU (default 0); HGA_PLOT_CMD overrides the plot command; HGA_TIMING=1 prints
+// the wall time of each phase to stderr ("hga-timing <phase> <ms>"; stdout stays the reference's).
+//
+// Overlap (same outputs): the HIP / device set-up runs on a thread while the read files are parsed,
+// and the dump caches are formatted and written on a thread while the histogram, the plot, the prompt
+// and the export proceed (joined before exit).
 //
 // --gpus N (extension, default 1): N ranks in this process, one per GPU (ranks.h), each counting a
 // contiguous share of every file's reads with min 1; hga_count_exchange moves the rows to their owner
@@ -32,10 +37,12 @@
 #include <filesystem>
 #include <iostream>
 #include <map>
+#include <memory>
 #include <random>
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "args.h"
@@ -65,6 +72,24 @@ int run_command_with_input(const std::string& cmd, const std::string& in) {
     if (pclose(p) != 0) std::fprintf(stderr, "Could not run more or other error.\n");
     return EXIT_SUCCESS;
 }
+
+// Phase timer for HGA_TIMING=1.
+struct PhaseTimer {
+    bool on = false;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+    void mark(const char* phase) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "hga-timing %s %.2f\n", phase,
+                     std::chrono::duration<double, std::milli>(now - last).count());
+        last = now;
+    }
+    void total() {
+        if (on)
+            std::fprintf(stderr, "hga-timing total %.2f\n",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
 
 using KmerSpecificity = std::map<double, std::map<int, int>>;
 
@@ -117,54 +142,128 @@ int main(int argc, char* argv[]) {
     }
     if (read_paths.empty()) throw std::invalid_argument("You need to specify paths to read files");
 
+    PhaseTimer tm;
+    if (const char* te = std::getenv("HGA_TIMING")) tm.on = std::string(te) == "1";
     const char* dev_env = std::getenv("HGA_DEVICE");
-    hgah::Ranks ranks(gpus, dev_env ? std::atoi(dev_env) : 0);
-    hga_ctx* ctx = ranks.ctx[0];
-    const int P = ranks.size();
+    // device set-up (HIP init, contexts) on a thread while the files are read, when k is given
+    std::unique_ptr<hgah::Ranks> ranks_p;
+    std::exception_ptr init_err;
+    std::thread init_th([&] {
+        try {
+            ranks_p = std::make_unique<hgah::Ranks>(gpus, dev_env ? std::atoi(dev_env) : 0);
+        } catch (...) {
+            init_err = std::current_exception();
+        }
+    });
+    auto join_init = [&] {
+        if (init_th.joinable()) init_th.join();
+        if (init_err) std::rethrow_exception(init_err);
+    };
     if (!ap.has("k-size")) {   // :40-44 — SequenceRecordIterator(read_paths, true) + get_unique_k_length
         const hgah::RecordSet rs = hgah::load_records(read_paths, true, false);
-        check(hga_lookup_set_reads(ctx, rs.bases.data(), rs.offsets.data(), rs.size(), 1), "hga_lookup_set_reads");
-        k = hgah::unique_k_length(ctx, std::cout).first;
+        join_init();
+        hga_ctx* c0 = ranks_p->ctx[0];
+        check(hga_lookup_set_reads(c0, rs.bases.data(), rs.offsets.data(), rs.size(), 1), "hga_lookup_set_reads");
+        k = hgah::unique_k_length(c0, std::cout).first;
     }
-    for (auto* c : ranks.ctx) check(hga_count_begin(c, k, (uint32_t)read_paths.size()), "hga_count_begin");
+    // dump caches (JellyfishOccurrenceReader.cpp:19-24) and the other files' bases
+    std::vector<std::vector<uint64_t>> cache_k(read_paths.size());
+    std::vector<std::vector<uint32_t>> cache_c(read_paths.size());
+    std::vector<hgah::Bytes> streams(read_paths.size());
+    std::vector<bool> cached(read_paths.size(), false);
     std::vector<uint32_t> counted;
     for (uint32_t f = 0; f < read_paths.size(); ++f) {
         const std::string cache = hgah::dump_cache_path(read_paths[f], k);
         if (std::filesystem::exists(cache)) {   // the dump's rows enter once, on rank 0
-            std::vector<uint64_t> dk;
-            std::vector<uint32_t> dc;
-            hgah::read_kmer_dump(cache, k, dk, dc);
-            check(hga_count_add_rows(ctx, f, dk.data(), dc.data(), dk.size()), "hga_count_add_rows");
+            hgah::read_kmer_dump(cache, k, cache_k[f], cache_c[f]);
+            cached[f] = true;
             continue;
         }
-        const hgah::Bytes s = hgah::jf_stream(read_paths[f]);
-        for (int r = 0; r < P; ++r) {
-            const auto [a, b] = hgah::shard_of(s.data(), s.size(), r, P);
-            check(hga_count_add(ranks.ctx[r], f, s.data() + a, b - a), "hga_count_add");
-        }
+        streams[f] = hgah::jf_stream(read_paths[f]);
         counted.push_back(f);
     }
+    tm.mark("read_files");
+    join_init();
+    tm.mark("device_init_wait");
+    hgah::Ranks& ranks = *ranks_p;
+    hga_ctx* ctx = ranks.ctx[0];
+    const int P = ranks.size();
+    for (auto* c : ranks.ctx) check(hga_count_begin(c, k, (uint32_t)read_paths.size()), "hga_count_begin");
+    for (uint32_t f = 0; f < read_paths.size(); ++f) {
+        if (cached[f]) {
+            check(hga_count_add_rows(ctx, f, cache_k[f].data(), cache_c[f].data(), cache_k[f].size()),
+                  "hga_count_add_rows");
+            std::vector<uint64_t>().swap(cache_k[f]);
+            std::vector<uint32_t>().swap(cache_c[f]);
+            continue;
+        }
+        const hgah::Bytes& sb = streams[f];
+        for (int r = 0; r < P; ++r) {
+            const auto [a, b] = hgah::shard_of(sb.data(), sb.size(), r, P);
+            check(hga_count_add(ranks.ctx[r], f, sb.data() + a, b - a), "hga_count_add");
+        }
+        streams[f] = hgah::Bytes();   // freed once uploaded
+    }
+    tm.mark("upload");
     if (P == 1) {
         check(hga_count_run(ctx, 2), "hga_count_run");   // jellyfish --bc: per-file singletons dropped
+        if (tm.on) {   // (the count is asynchronous; the stats wait for it)
+            hga_count_stats st;
+            check(hga_count_get_stats(ctx, &st), "hga_count_get_stats");
+            tm.mark("count");
+        }
     } else {
         ranks.each([](int, hga_ctx* c) {
             check(hga_count_run(c, 1), "hga_count_run");   // no drop before the global sum
             check(hga_count_exchange(c, 2), "hga_count_exchange");
         });
     }
+    // the dumps come off the device here; they are formatted and written on a thread meanwhile
+    struct DumpJob {
+        std::string path;
+        uint32_t file = 0;
+        std::vector<uint64_t*> k;   // one rank's dump of `file` (--gpus N), or null: the merged rows
+        std::vector<uint32_t*> c;
+        uint64_t n = 0;
+    };
+    std::vector<DumpJob> dumps;
+    uint64_t* all_k = nullptr;   // one GPU: every dump from one fetch of the merged rows
+    uint32_t* all_c = nullptr;
+    uint64_t all_n = 0;
+    const uint32_t F = (uint32_t)read_paths.size();
     const char* cache_env = std::getenv("HGA_DUMP_CACHE");
-    if (!(cache_env && std::string(cache_env) == "0"))
+    if (!(cache_env && std::string(cache_env) == "0") && !counted.empty()) {
+        if (P == 1) check(hga_count_rows(ctx, &all_k, &all_c, &all_n), "hga_count_rows");
         for (uint32_t f : counted) {
-            std::vector<uint64_t*> dk(P, nullptr);
-            std::vector<uint32_t*> dc(P, nullptr);
-            std::vector<uint64_t> n_d(P, 0);
-            ranks.each([&](int r, hga_ctx* c) { check(hga_count_dump(c, f, &dk[r], &dc[r], &n_d[r]), "hga_count_dump"); });
-            hgah::write_kmer_dump(hgah::dump_cache_path(read_paths[f], k), k, dk[0], dc[0], n_d[0]);
-            for (int r = 0; r < P; ++r) {
-                hga_free(dk[r]);
-                hga_free(dc[r]);
+            DumpJob j;
+            j.path = hgah::dump_cache_path(read_paths[f], k);
+            j.file = f;
+            if (P > 1) {
+                j.k.assign(P, nullptr);
+                j.c.assign(P, nullptr);
+                std::vector<uint64_t> n_d(P, 0);
+                ranks.each([&](int r, hga_ctx* c) { check(hga_count_dump(c, f, &j.k[r], &j.c[r], &n_d[r]), "hga_count_dump"); });
+                j.n = n_d[0];
             }
+            dumps.push_back(std::move(j));
         }
+    }
+    tm.mark("count_and_dump_fetch");
+    std::exception_ptr dump_err;
+    std::thread dump_th([&] {
+        try {
+            for (auto& j : dumps) {
+                if (j.k.empty()) hgah::write_kmer_dump_rows(j.path, k, all_k, all_c, F, j.file, all_n);
+                else hgah::write_kmer_dump(j.path, k, j.k[0], j.c[0], j.n);
+            }
+        } catch (...) {
+            dump_err = std::current_exception();
+        }
+    });
+    struct DumpJoin {   // joined on every way out of main, the outputs complete before exit
+        std::thread& t;
+        ~DumpJoin() { if (t.joinable()) t.join(); }
+    } dump_join{dump_th};
 
     const std::set<double> thresholds = {70, 85, 90, 95, 99, 100, 100.01};
     const std::vector<double> thr(thresholds.begin(), thresholds.end());
@@ -182,14 +281,17 @@ int main(int argc, char* argv[]) {
         spec[thr[(size_t)tri[3 * i]]][(int)tri[3 * i + 1]] += (int)tri[3 * i + 2];
     hga_free(tri);
     std::map<int, KmerSpecificity> spec_map = {{k, spec}};
+    tm.mark("spec_hist");
     const char* plot_env = std::getenv("HGA_PLOT_CMD");
     const std::string plot_cmd = plot_env ? plot_env : "python scripts/plotting.py --plot kmer_histogram_with_spec";
     std::cout << run_command_with_input(plot_cmd, plot_wire(spec_map, 200)) << std::endl;
+    tm.mark("plot");
 
     int lower = 0, upper = 0;
     double percent = 0;
     std::cout << "Enter lower and upper bounds for exported kmers as well as percentage\n";
     std::cin >> lower >> upper >> percent;
+    tm.mark("prompt");
     if (output_path.empty())
         output_path = std::to_string(k) + "-mers_" + std::to_string(lower) + "_" + std::to_string(upper) + "_" +
                       hgah::fmt_double(percent * 100) + "%.txt";
@@ -229,7 +331,19 @@ int main(int argc, char* argv[]) {
     std::fclose(out);
     hga_free(keys);
     hga_free(disc);
+    tm.mark("select_and_export");
     std::cout << discriminative << " out of " << exported << " exported kmers are discriminative";
     std::cout.flush();
+    dump_th.join();
+    for (auto& j : dumps)
+        for (size_t r = 0; r < j.k.size(); ++r) {
+            hga_free(j.k[r]);
+            hga_free(j.c[r]);
+        }
+    hga_free(all_k);
+    hga_free(all_c);
+    tm.mark("dump_write_wait");
+    tm.total();
+    if (dump_err) std::rethrow_exception(dump_err);
     return 0;
 }

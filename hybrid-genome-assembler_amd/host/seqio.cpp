@@ -8,6 +8,9 @@
 #include <fstream>
 #include <regex>
 #include <stdexcept>
+#include <algorithm>
+#include <atomic>
+#include <thread>
 
 namespace hgah {
 
@@ -348,26 +351,54 @@ void read_kmer_dump(const std::string& path, int k, std::vector<uint64_t>& keys,
 }
 
 void write_kmer_dump(const std::string& path, int k, const uint64_t* keys, const uint32_t* counts, uint64_t n) {
+    write_kmer_dump_rows(path, k, keys, counts, 1, 0, n);
+}
+
+void write_kmer_dump_rows(const std::string& path, int k, const uint64_t* keys, const uint32_t* counts, uint32_t F,
+                          uint32_t file, uint64_t n) {
     std::FILE* f = std::fopen(path.c_str(), "wb");
     if (!f) throw std::runtime_error("cannot write " + path);
-    std::vector<char> buf;
-    buf.reserve(1 << 20);
-    char num[16];
-    for (uint64_t i = 0; i < n; ++i) {
-        const size_t at = buf.size();
-        buf.resize(at + (size_t)k);
-        kmer_to_chars(keys[i], k, buf.data() + at);
-        buf.push_back(' ');
-        auto r = std::to_chars(num, num + sizeof(num), counts[i]);
-        buf.insert(buf.end(), num, r.ptr);
-        buf.push_back('\n');
-        if (buf.size() > (1u << 20)) {
-            std::fwrite(buf.data(), 1, buf.size(), f);
-            buf.clear();
+    // "KMER COUNT\n" lines formatted by host_threads() threads, chunk by chunk in row order, each
+    // chunk's text written as soon as it and its predecessors are done
+    const uint64_t CH = 1u << 18;   // rows per chunk
+    const uint64_t nch = (n + CH - 1) / CH;
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), nch));
+    std::vector<std::vector<char>> text(nch);
+    std::vector<std::atomic<int>> done(nch);
+    for (auto& d : done) d.store(0);
+    std::atomic<uint64_t> next{0};
+    auto work = [&] {
+        char num[16];
+        for (uint64_t c; (c = next.fetch_add(1)) < nch;) {
+            const uint64_t a = c * CH, b = std::min(n, a + CH);
+            std::vector<char>& buf = text[c];
+            buf.resize((b - a) * ((size_t)k + 12));
+            char* o = buf.data();
+            for (uint64_t i = a; i < b; ++i) {
+                const uint32_t cnt = counts[i * F + file];
+                if (!cnt) continue;   // a row of the merged table without this file
+                kmer_to_chars(keys[i], k, o);
+                o += k;
+                *o++ = ' ';
+                auto r = std::to_chars(num, num + sizeof(num), cnt);
+                for (const char* q = num; q < r.ptr; ++q) *o++ = *q;
+                *o++ = '\n';
+            }
+            buf.resize((size_t)(o - buf.data()));
+            done[c].store(1, std::memory_order_release);
         }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work);
+    bool ok = true;
+    if (T == 1) work();
+    for (uint64_t c = 0; c < nch; ++c) {   // the writer: chunks in order as they complete
+        while (!done[c].load(std::memory_order_acquire)) std::this_thread::yield();
+        ok = ok && std::fwrite(text[c].data(), 1, text[c].size(), f) == text[c].size();
+        std::vector<char>().swap(text[c]);
     }
-    std::fwrite(buf.data(), 1, buf.size(), f);
-    if (std::fclose(f) != 0) throw std::runtime_error("cannot write " + path);
+    for (auto& x : th) x.join();
+    if (std::fclose(f) != 0 || !ok) throw std::runtime_error("cannot write " + path);
 }
 
 }  // namespace hgah

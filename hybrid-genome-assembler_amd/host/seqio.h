@@ -106,6 +106,9 @@ uint64_t line_canonical(const char* s, size_t len);
 // whose k-mer is not k bases of ACGT throws.  write_kmer_dump writes rows in the given order.
 void read_kmer_dump(const std::string& path, int k, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts);
 void write_kmer_dump(const std::string& path, int k, const uint64_t* keys, const uint32_t* counts, uint64_t n);
+// The same from the merged rows (counts row-major [n][F]): the rows with a count in `file`.
+void write_kmer_dump_rows(const std::string& path, int k, const uint64_t* keys, const uint32_t* counts, uint32_t F,
+                          uint32_t file, uint64_t n);
 std::string dump_cache_path(const std::string& reads, int k);   // "{reads}_{k}-mers_sorted"
 
 }  // namespace hgah

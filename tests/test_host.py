@@ -114,3 +114,33 @@ def test_cli_argument_errors():
     out = subprocess.run([os.path.join(BIN, "jf_occurrences"), "--bogus", "x"], capture_output=True, text=True,
                          timeout=60)
     assert out.returncode != 0 and "unrecognised option" in out.stderr
+
+
+@pytest.mark.parametrize("n,threads", [(0, 1), (7, 1), (300_000, 1), (300_000, 5), (1_100_000, 16)])
+def test_dump_writer_matches_restatement(tmp_path, n, threads):
+    """write_kmer_dump (the dump cache of run_jellyfish.sh:5-6: "KMER COUNT" lines, LC_ALL=C order as
+    given) formats chunks on several threads and writes them in order: byte-identical to a plain
+    restatement for any thread count, including several chunks of 2^18 rows."""
+    rng = np.random.default_rng(n + threads)
+    k = 19
+    keys = np.sort(rng.integers(0, 4 ** k, n, dtype=np.uint64))
+    counts = rng.integers(1, 1 << 20, n, dtype=np.uint64).astype(np.uint32)
+    import hga as hga_mod
+    hga_mod.set_host_threads(threads)
+    try:
+        p = tmp_path / "d.txt"
+        hga_mod.write_kmer_dump(str(p), k, keys, counts)
+    finally:
+        hga_mod.set_host_threads(0)
+    got = p.read_text()
+    lines = got.splitlines(keepends=True)
+    assert len(lines) == n
+
+    def kstr(c):
+        return "".join("ACGT"[(int(c) >> (2 * (k - 1 - i))) & 3] for i in range(k))
+    want = "".join(f"{kstr(c)} {int(v)}\n" for c, v in zip(keys[:2000], counts[:2000]))
+    assert "".join(lines[:2000]) == want
+    idx = rng.integers(0, max(n, 1), 200) if n else []
+    for i in idx:
+        kstr = "".join("ACGT"[(int(keys[i]) >> (2 * (k - 1 - j))) & 3] for j in range(k))
+        assert lines[i] == f"{kstr} {int(counts[i])}\n"
