@@ -2215,7 +2215,7 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     hipLaunchKernelGGL((kc_bin1<E1T, KK, FBB>), dim3(W), dim3(NT_B), 0, c->stream, d_bf, F, st_pos, kp, table, table_cap, \
                        pool_cap, static_cast<E1T*>(binned1), wcnt, nblk, gstat)
             // compile-time k for the k of the configs (C1-C4: 19; C5: 15, 17, 19, 21)
-            if (e1_32 && kp.k == 19 && kp.fb == 12 && !HGA_B1_NOFB) HGA_BIN1(uint32_t, 19, 12);
+            if (e1_32 && kp.k == 19 && kp.fb == MAX_FB && !HGA_B1_NOFB) HGA_BIN1(uint32_t, 19, MAX_FB);
             else if (e1_32 && kp.k == 19) HGA_BIN1(uint32_t, 19, 0);
             else if (e1_32 && kp.k == 17) HGA_BIN1(uint32_t, 17, 0);
             else if (e1_32 && kp.k == 15) HGA_BIN1(uint32_t, 15, 0);
