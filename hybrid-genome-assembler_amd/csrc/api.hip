@@ -3,6 +3,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "hga_internal.hpp"
@@ -12,6 +13,8 @@ thread_local std::string g_err;
 
 template <class F>
 hga_status guard(F&& f) {
+    // a body that returns a value on one path would fall off its end on the others (undefined)
+    static_assert(std::is_void<decltype(f())>::value, "guarded bodies return nothing");
     try {
         g_err.clear();
         f();
@@ -246,6 +249,7 @@ hga_status hga_count_pack_bits(hga_ctx* c, int* bits) {
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(bits, HGA_ERR_INVALID, "null pointer");
         HGA_REQUIRE(c->count.begun, HGA_ERR_STATE, "hga_count_begin not called");
+        hga::count_settle(c);   // (a failed count reports here)
         *bits = hga::count_pack_bits(c);
     });
 }
@@ -266,16 +270,17 @@ hga_status hga_count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n
 hga_status hga_count_rows(hga_ctx* c, uint64_t** keys, uint32_t** counts, uint64_t* rows) {
     HGA_CTX_GUARD(c, {
         HGA_REQUIRE(keys && counts && rows, HGA_ERR_INVALID, "null pointer");
+        // (no early return: the guarded lambda returns void on every path)
         if (!c->count.dist) {   // sorted on the device, copied straight into the returned buffers
             hga::count_rows_to(c, keys, counts, rows);
-            return HGA_OK;
+        } else {
+            std::vector<uint64_t> k;
+            std::vector<uint32_t> v;
+            hga::count_rows_global(c, -1, k, v);
+            *keys = host_dup(k.data(), k.size());
+            *counts = host_dup(v.data(), v.size());
+            *rows = k.size();
         }
-        std::vector<uint64_t> k;
-        std::vector<uint32_t> v;
-        hga::count_rows_global(c, -1, k, v);
-        *keys = host_dup(k.data(), k.size());
-        *counts = host_dup(v.data(), v.size());
-        *rows = k.size();
     });
 }
 

@@ -222,9 +222,14 @@ struct CtxXport : proto::Xport {
     }
 };
 
+[[noreturn]] void throw_query_error(const proto::QueryError& e);
+
 // ... and its rows on the device (exchange.hip kernels).
 struct DevEngine {
     hga_ctx* c;
+    // extra[0] of the exchange is the rank's instance count: with the count not settled yet, the fused
+    // head gathers it from the device counters
+    bool extra0_instances = false;
     int k() const { return c->count.k; }
     uint32_t n_files() const { return c->count.n_files; }
     uint64_t rows() const { return c->count.rows; }
@@ -232,6 +237,63 @@ struct DevEngine {
     void* send_buf(uint64_t bytes) { return c->count.xsend.ensure(bytes + 64); }
     void* recv_buf(uint64_t bytes) { return c->count.xrecv.ensure(bytes + 64); }
     int xb_pack(uint32_t P, uint64_t* per) { return count_xb_pack(c, P, per); }
+    // Fused head over an on-device communicator (the count kernels wrote the pieces): the per-owner
+    // totals, R, the extras and this rank's count error bits are all-gathered straight from device
+    // memory and the count's counters read back in the same host round trip (instead of one each for
+    // the settle, xb_pack and the all-gather).  Errors are decided on the gathered bits, so every rank
+    // raises the lowest failing rank's and none enters the piece all-to-all alone.
+    bool xb_pack_gather(uint32_t P, std::vector<uint64_t>& per, std::vector<uint64_t>& all, int& R) {
+        Comm& m = *c->comm;
+        auto& s = c->count;
+        if (!m.on_device() || !(s.xb_on && s.xb_P == P)) return false;
+        const size_t W = per.size(), Wg = W + 1;   // + the error word
+        const uint64_t B = 8 * (uint64_t)Wg;
+        char* ds = static_cast<char*>(m.stage.ensure(B * (P + 1) + 16));
+        char* hs = static_cast<char*>(m.hstage.ensure(B * (P + 1) + 64 + 16));
+        auto* hp = reinterpret_cast<unsigned long long*>(hs + B * (P + 1));   // the count's counters
+        const bool pend = s.pending;
+        if (!count_xb_pack_begin(c, P, reinterpret_cast<uint64_t*>(ds))) return false;
+        R = s.xb_R;
+        per[P] = (uint64_t)R;
+        std::memcpy(hs + 8 * P, per.data() + P, 8 * (W - P));
+        HGA_HIP(hipMemcpyAsync(ds + 8 * P, hs + 8 * P, 8 * (W - P), hipMemcpyHostToDevice, c->stream));
+        if (pend) {   // settle bits (gstat[2]) and, if asked, instances (gstat[4]) from the device
+            HGA_HIP(hipMemcpyAsync(ds + 8 * W, static_cast<char*>(s.cursor.p) + 16, 8, hipMemcpyDeviceToDevice,
+                                   c->stream));
+            if (extra0_instances && W > (size_t)P + 1)
+                HGA_HIP(hipMemcpyAsync(ds + 8 * (P + 1), static_cast<char*>(s.cursor.p) + 32, 8,
+                                       hipMemcpyDeviceToDevice, c->stream));
+            HGA_HIP(hipMemcpyAsync(hp, s.cursor.p, 64, hipMemcpyDeviceToHost, c->stream));
+        } else {
+            HGA_HIP(hipMemsetAsync(ds + 8 * W, 0, 8, c->stream));
+        }
+        std::vector<uint64_t> sz(P, B);
+        std::vector<const void*> sp(P, ds);
+        std::vector<void*> rp(P);
+        for (uint32_t p = 0; p < P; ++p) rp[p] = ds + B * (p + 1);
+        m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+        HGA_HIP(hipMemcpyAsync(hs + B, ds + B, B * P, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        const uint64_t* g = reinterpret_cast<const uint64_t*>(hs + B);
+        std::vector<uint64_t> bits(P);
+        for (uint32_t p = 0; p < P; ++p) bits[p] = g[(size_t)p * Wg + W] & 7ull;
+        const proto::QueryError qe = proto::first_error(bits.data(), (int)P, 1);
+        if (qe.rank >= 0) {
+            if (pend) {   // this rank's run is consumed as failed (as count_settle would)
+                s.pending = false;
+                s.last_err = hp[2] & 7ull;
+                if (s.last_err) s.ran = false;
+            }
+            throw_query_error(qe);
+        }
+        if (pend) count_settle(c, hp);
+        all.assign((size_t)P * W, 0);
+        for (uint32_t p = 0; p < P; ++p)
+            for (size_t i = 0; i < W; ++i) all[(size_t)p * W + i] = g[(size_t)p * Wg + i];
+        for (uint32_t o = 0; o < P; ++o) per[o] = all[(size_t)m.rank * W + o];
+        count_xb_pack_finish(c, P, per.data());
+        return true;
+    }
     const void* xb_pieces() const { return c->count.xsend.p; }
     const void* xb_dir() const { return c->count.xdir.p; }
     void xb_merge(const uint64_t* in, const uint64_t* self, const uint64_t* n_from, const uint64_t* dir_in,
@@ -251,8 +313,11 @@ struct DevEngine {
 
 void count_exchange(hga_ctx* c, uint32_t min_per_file) {
     auto& s = c->count;
-    need_comm(c);
-    count_settle(c);
+    Comm& m = need_comm(c);
+    // an unsettled count whose kernels wrote the pieces is settled by the fused exchange head
+    // (DevEngine::xb_pack_gather), in the round trip of its all-gather
+    const bool fused = m.on_device() && s.pending && s.xb_on && s.xb_P == (uint32_t)m.nranks;
+    if (!fused) count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run(ctx, 1) first");
     HGA_REQUIRE(s.min_per_file == 1, HGA_ERR_STATE, "the local count must keep singletons: hga_count_run(ctx, 1)");
     HGA_REQUIRE(min_per_file >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
@@ -261,12 +326,12 @@ void count_exchange(hga_ctx* c, uint32_t min_per_file) {
     std::vector<uint64_t> mine{s.instances, 0}, g;
     for (auto l : s.seq_len) mine[1] += l;
     DevEngine e{c};
+    e.extra0_instances = fused;
     proto::count_exchange(e, x, min_per_file, mine, &g);
     s.g_instances = g[0];
     s.g_bytes = g[1];
     // the global row count once, here, so hga_count_get_stats stays local (not a collective); over
     // RCCL it is only enqueued (pinned staging both ways) and summed when get_stats asks for it
-    Comm& m = *c->comm;
     const int P = x.nranks;
     if (m.on_device()) {
         uint64_t* hs = static_cast<uint64_t*>(s.g_rows_h.ensure(8 * ((uint64_t)P + 1)));

@@ -895,9 +895,9 @@ __global__ void __launch_bounds__(MG_NT) kx_xb_merge(const uint64_t* __restrict_
 }  // namespace
 
 // Bits per file count in the packed form (0 = not packable: use the wide exchange).
+// (k and the file count only: no settle, so the exchange's fused head can still take an unsettled count)
 int count_pack_bits(hga_ctx* c) {
     auto& s = c->count;
-    count_settle(c);
     const int kb = 2 * s.k;
     const int cb = s.n_files ? (64 - kb) / (int)s.n_files : 0;
     return (s.n_files <= 8 && cb >= 4) ? (cb > 32 ? 32 : cb) : 0;
@@ -1050,44 +1050,62 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
 // Sender: this rank's rows as pieces in bucket order in `xsend`, the per-bucket counts in `xdir`,
 // pieces per owner in per_owner[P]; returns the bucket resolution R (about 1024 pieces per owner
 // bucket if every rank holds as many rows as this one, within [EB0, min(2k, XB_MAXR)]).
+// Fast path, first half (enqueued, no host round trip): the count kernels' per-bucket piece counts
+// scanned into the gather offsets and the per-owner totals written to d_per (P words, device or
+// mapped memory).  False (nothing enqueued): the count kernels did not write the pieces.
+// Owners hold whole count buckets (count_run checked fb >= EB0).
+bool count_xb_pack_begin(hga_ctx* c, uint32_t P, uint64_t* d_per) {
+    auto& s = c->count;
+    HGA_REQUIRE(P >= 1 && P <= XB_MAXP, HGA_ERR_INVALID, "at most 1024 ranks");
+    if (!(s.xb_on && s.xb_P == P)) return false;
+    const int eb0 = std::min(10, 2 * s.k);
+    const int fbc = s.xb_R - (int)s.xb_x;
+    const uint64_t nbc = s.xb_nbc;
+    uint64_t* S = static_cast<uint64_t*>(s.xch.ensure((nbc + 1) * 8 + 64));
+    HGA_HIP(hipMemcpyAsync(S, s.xdir_b.p, nbc * 8, hipMemcpyDeviceToDevice, c->stream));
+    HGA_HIP(hipMemsetAsync(S + nbc, 0, 8, c->stream));
+    exclusive_scan_u64(c, S, nbc + 1, s.scratch);
+    c->launch("kx_xb_pack", [&] {
+        hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream, S, P, eb0, fbc, d_per);
+    });
+    c->check_launch("kx_xb_owner_tot");
+    return true;
+}
+
+// Second half, once the count is settled and this rank's per-owner totals are on the host: the
+// pieces gathered into owner order (xb_pieces) with their directory (xb_dir).  Returns R.
+int count_xb_pack_finish(hga_ctx* c, uint32_t P, const uint64_t* per_owner) {
+    auto& s = c->count;
+    HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
+    HGA_REQUIRE(s.xb_on && s.xb_P == P, HGA_ERR_STATE, "the count did not emit exchange pieces");
+    const int R = s.xb_R;
+    uint64_t total = 0;
+    for (uint32_t o = 0; o < P; ++o) total += per_owner[o];
+    HGA_REQUIRE(total < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per rank");
+    uint64_t* out = static_cast<uint64_t*>(s.xsend.ensure(std::max<uint64_t>(total, 1) * 8 + 64));
+    uint64_t* dir = static_cast<uint64_t*>(s.xdir.ensure((8ull << R) + 64));
+    c->launch("kx_xb_gather", [&] {
+        hipLaunchKernelGGL(kx_xb_gather, dim3((unsigned)s.xb_nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(),
+                           s.xb_fs, s.n_files, s.xb_x, 2 * s.k - R, s.xch.as<uint64_t>(), out, dir);
+    });
+    c->check_launch("kx_xb_gather");
+    return R;
+}
+
 int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner) {
     auto& s = c->count;
     HGA_REQUIRE(P >= 1 && P <= XB_MAXP, HGA_ERR_INVALID, "at most 1024 ranks");
     const int eb0 = std::min(10, 2 * s.k);
-    if (s.xb_on && s.xb_P == P) {   // the count kernels wrote the pieces
-        // one host round trip: the count's counters and the per-owner totals come back together;
-        // owners hold whole count buckets (count_run checked fb >= EB0)
-        const int R = s.xb_R, fbc = s.xb_R - (int)s.xb_x;
-        const uint64_t nbc = s.xb_nbc;
-        char* w = static_cast<char*>(s.xch.ensure((nbc + 1) * 8 + 64));
-        uint64_t* S = reinterpret_cast<uint64_t*>(w);
-        auto* hp = static_cast<unsigned long long*>(s.xpack_h.ensure(8 * (8 + (uint64_t)P)));
-        HGA_HIP(hipMemcpyAsync(S, s.xdir_b.p, nbc * 8, hipMemcpyDeviceToDevice, c->stream));
-        HGA_HIP(hipMemsetAsync(S + nbc, 0, 8, c->stream));
-        exclusive_scan_u64(c, S, nbc + 1, s.scratch);
-        c->launch("kx_xb_pack", [&] {
-            hipLaunchKernelGGL(kx_xb_owner_tot, dim3(kx_blocks(P, 256)), dim3(256), 0, c->stream, S, P, eb0, fbc,
-                               reinterpret_cast<uint64_t*>(s.xpack_h.dev(hp + 8)));
-        });
-        c->check_launch("kx_xb_owner_tot");
+    // the count kernels wrote the pieces: one host round trip, the count's counters and the
+    // per-owner totals come back together
+    auto* hp = static_cast<unsigned long long*>(s.xpack_h.ensure(8 * (8 + (uint64_t)P)));
+    if (count_xb_pack_begin(c, P, reinterpret_cast<uint64_t*>(s.xpack_h.dev(hp + 8)))) {
         const bool pend = s.pending;
         if (pend) HGA_HIP(hipMemcpyAsync(hp, s.cursor.p, 64, hipMemcpyDeviceToHost, c->stream));
         c->sync();
         if (pend) count_settle(c, hp);
-        HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
-        if (s.xb_on) {
-            uint64_t total = 0;
-            for (uint32_t o = 0; o < P; ++o) total += (per_owner[o] = hp[8 + o]);
-            HGA_REQUIRE(total < (1ull << 32), HGA_ERR_INVALID, "at most 2^32-1 pieces per rank");
-            uint64_t* out = static_cast<uint64_t*>(s.xsend.ensure(std::max<uint64_t>(total, 1) * 8 + 64));
-            uint64_t* dir = static_cast<uint64_t*>(s.xdir.ensure((8ull << R) + 64));
-            c->launch("kx_xb_gather", [&] {
-                hipLaunchKernelGGL(kx_xb_gather, dim3((unsigned)nbc), dim3(256), 0, c->stream, s.xslab.as<uint64_t>(),
-                                   s.xb_fs, s.n_files, s.xb_x, 2 * s.k - R, S, out, dir);
-            });
-            c->check_launch("kx_xb_gather");
-            return R;
-        }
+        for (uint32_t o = 0; o < P; ++o) per_owner[o] = hp[8 + o];
+        return count_xb_pack_finish(c, P, per_owner);
     }
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");

@@ -77,6 +77,11 @@ inline uint32_t xb_owner_of_cell(uint64_t c, int P, int eb0) { return (uint32_t)
 //     int xb_pack(uint32_t P, uint64_t* per_owner);
 //         orders the pieces by bucket (owner-major) in engine memory xb_pieces() and counts them per
 //         bucket in xb_dir() (u64, 2^R entries); returns R; per_owner[o] = pieces for owner o
+//     bool xb_pack_gather(uint32_t P, std::vector<uint64_t>& per, std::vector<uint64_t>& all, int& R);
+//         optional fused form of xb_pack + the piece-count all-gather below (an engine whose transport
+//         gathers its device words directly): per = this rank's W words with the extras filled, out:
+//         per[0, P] and `all` (P x W, rank-major) as recv_counts leaves them; false: not taken (the
+//         engine did nothing), xb_pack + allgather follow
 //     const void* xb_pieces(); const void* xb_dir();
 //     void xb_merge(const uint64_t* in, const uint64_t* self, const uint64_t* n_from, const uint64_t* dir_in,
 //                   const int* r_from, uint32_t P, uint32_t me, uint32_t min);
@@ -97,8 +102,7 @@ uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file, const std::vector
     const size_t X = extra.size(), W = (size_t)P + 1 + X;
     std::vector<uint64_t> per(W), all((size_t)P * W), rn(P), sb(P), rb(P);
     for (size_t i = 0; i < X; ++i) per[P + 1 + i] = extra[i];
-    auto recv_counts = [&] {
-        x.allgather(per.data(), 8 * (uint64_t)W, all.data());
+    auto digest = [&] {   // `all` gathered: pieces per sender for this owner, the extras' sums
         uint64_t n = 0;
         for (int p = 0; p < P; ++p) n += (rn[p] = all[(size_t)p * W + me]);
         if (extra_sum) {
@@ -108,11 +112,21 @@ uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file, const std::vector
         }
         return n;
     };
+    auto recv_counts = [&] {
+        x.allgather(per.data(), 8 * (uint64_t)W, all.data());
+        return digest();
+    };
     if (e.pack_bits() > 0) {   // one u64 piece per row (a count past the piece width: several pieces)
         const int eb0 = xb_base_bits(e.k());
-        const int R = e.xb_pack((uint32_t)P, per.data());
-        per[P] = (uint64_t)R;
-        const uint64_t n = recv_counts();
+        int R = 0;
+        uint64_t n;
+        if (e.xb_pack_gather((uint32_t)P, per, all, R)) {
+            n = digest();
+        } else {
+            R = e.xb_pack((uint32_t)P, per.data());
+            per[P] = (uint64_t)R;
+            n = recv_counts();
+        }
         std::vector<int> rf(P);
         uint64_t nd = 0;   // directory entries this owner receives
         for (int p = 0; p < P; ++p) {

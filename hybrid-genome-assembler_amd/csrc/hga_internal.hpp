@@ -295,6 +295,11 @@ void count_merge_packed(hga_ctx* c, const uint64_t* pieces, uint64_t n, uint32_t
 // bucket order in `xsend` and its per-bucket counts in `xdir` (returns the resolution R), and the
 // owner's merge of every sender's runs of its buckets
 int count_xb_pack(hga_ctx* c, uint32_t P, uint64_t* per_owner);
+// its fast path in two halves (count kernels that wrote the pieces): begin enqueues the per-owner
+// totals into d_per (false: not applicable, nothing enqueued); finish gathers the pieces once the
+// count is settled and the totals are on the host
+bool count_xb_pack_begin(hga_ctx* c, uint32_t P, uint64_t* d_per);
+int count_xb_pack_finish(hga_ctx* c, uint32_t P, const uint64_t* per_owner);
 void count_xb_merge(hga_ctx* c, const uint64_t* in, const uint64_t* self, const uint64_t* n_from, const uint64_t* dir_in,
                     const int* r_from, uint32_t P, uint32_t me, uint32_t min_c);
 

@@ -123,6 +123,7 @@ struct HostEngine {
     }
     // pieces of every row, by hash bucket at resolution R; R differs between ranks on purpose (the
     // owners merge at the coarsest one)
+    bool xb_pack_gather(uint32_t, std::vector<uint64_t>&, std::vector<uint64_t>&, int&) { return false; }
     int xb_pack(uint32_t P, uint64_t* per) {
         const int eb0 = hga::proto::xb_base_bits(k_);
         const int R = std::min(2 * k_, eb0 + rank_ % 3);

@@ -27,8 +27,8 @@ XLIB = os.path.join(HERE, "native", "_build", "libxproto_host.so")
 
 
 def xlib():
-    if not os.path.exists(XLIB):
-        subprocess.run(["make", "-s", "-C", os.path.join(HERE, "native")], check=True)
+    # (make rebuilds it when its sources or the protocol header changed)
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "native")], check=True)
     L = C.CDLL(XLIB)
     L.xt_create.restype = C.c_void_p
     L.xt_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]

@@ -37,6 +37,8 @@ def test_rccl_one_rank_count_exchange(monkeypatch, self_p2p, k, emit):
         ctx.count_run(1)
         ctx.count_exchange(2)
         assert ctx.count_stats().distinct_rows == len(ref["keys"])   # the enqueued row-count gather
+        # (with emission the instances ride the fused exchange head from the device counters)
+        assert ctx.count_stats().instances == sum(oracle.count_instances(x, k) for x in streams)
         assert np.array_equal(ctx.spec_hist(THR), ref["hist"])
         keys, flags, nd = ctx.select(3, 40)
         assert np.array_equal(keys, ref["selected"]) and nd == ref["n_discr"]
@@ -44,6 +46,30 @@ def test_rccl_one_rank_count_exchange(monkeypatch, self_p2p, k, emit):
         assert np.array_equal(rk, ref["keys"]) and np.array_equal(rc, ref["counts"])
         d0 = ctx.dump(0)
         assert np.array_equal(d0[0], ref["dumps"][0][0]) and np.array_equal(d0[1], ref["dumps"][0][1])
+        ctx.comm_destroy()
+
+
+def test_rccl_fused_exchange_head_reports_count_errors(monkeypatch):
+    """A count that failed on the device (row capacity, HGA_ROW_CAP) and was never settled: the fused
+    exchange head (comm.hip DevEngine::xb_pack_gather) decides on the gathered error bits and raises
+    the failing rank's error by name; the context stays usable for a new count."""
+    monkeypatch.setenv("HGA_FB_MIN", "10")
+    streams = make_streams()
+    with hga.Ctx(0) as ctx:
+        ctx.comm_init(hga.comm_unique_id(), 0, 1)
+        ctx.count_begin(13, len(streams))
+        for f, s in enumerate(streams):
+            ctx.count_add(f, s)
+        monkeypatch.setenv("HGA_ROW_CAP", "64")
+        ctx.count_run(1)
+        with pytest.raises(hga.HgaError, match="rank 0: row capacity exceeded"):
+            ctx.count_exchange(2)
+        monkeypatch.delenv("HGA_ROW_CAP")
+        ref = oracle.count_pipeline(streams, 13, 3, 40)
+        ctx.count_run(1)
+        ctx.count_exchange(2)
+        keys, flags, nd = ctx.select(3, 40)
+        assert np.array_equal(keys, ref["selected"]) and nd == ref["n_discr"]
         ctx.comm_destroy()
 
 
