@@ -184,6 +184,7 @@ struct LookupState {
     int k = 0, km = 0;
     uint32_t n_sdk = 0;
     uint64_t slots = 0, fwords = 0, pk_words = 0;   // slots = table buckets
+    uint32_t idb = 0;   // packed table entries: KmerID bits (0: 64-B buckets)
     DevBuf tab_key, tab_id, filter, packed, valid, starts, word_read, win_kid;
     uint64_t n_reads = 0, n_bases = 0;
     uint32_t first_read_id = 1;

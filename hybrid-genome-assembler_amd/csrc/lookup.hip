@@ -127,6 +127,18 @@ __device__ __forceinline__ uint64_t end_word(uint32_t minh, uint32_t x, uint64_t
     return ((((uint64_t)minh) << 2) | (x >> 30)) & fmask;
 }
 
+// Packed layout (2k bits of key + the KmerID bits fit 64: the SDK sets of C3-C5): 32-B buckets of
+// four u64 entries key << idb | KmerID, so a probe reads half a 64-B line instead of a whole one.
+// An empty entry is ~0 (its key field, all ones, is the all-T code, which is never canonical).
+constexpr int PBKT = 4;
+struct alignas(32) PBucket {
+    uint64_t e[PBKT];
+};
+static_assert(sizeof(PBucket) == 32, "half a line per packed bucket");
+#ifndef HGA_LK_PACKED
+#define HGA_LK_PACKED 1   // 0: always the 64-B layout
+#endif
+
 __global__ void lk_fill(Bucket* __restrict__ t, uint64_t nbk) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nbk * BKT) return;
@@ -134,7 +146,7 @@ __global__ void lk_fill(Bucket* __restrict__ t, uint64_t nbk) {
 }
 
 __global__ void lk_build(const uint64_t* __restrict__ keys, uint32_t n, Bucket* __restrict__ t, uint64_t nbk,
-                         uint32_t* __restrict__ filt, uint64_t fmask, int k, int km) {
+                         uint32_t* __restrict__ filt, uint64_t fmask, int k, int km, uint32_t idb) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t key = keys[i];
@@ -148,6 +160,17 @@ __global__ void lk_build(const uint64_t* __restrict__ keys, uint32_t n, Bucket* 
         atomicOr(&filt[filter_word(key_minimizer(key, k, km), h, fmask)], bloom_bits(h));
     }
     uint64_t b = bucket_of(h, nbk);
+    if (idb) {   // packed buckets
+        PBucket* pt = reinterpret_cast<PBucket*>(t);
+        const unsigned long long ent = (key << idb) | i;
+        while (true) {
+            for (int s = 0; s < PBKT; ++s) {
+                const unsigned long long old = atomicCAS((unsigned long long*)&pt[b].e[s], ~0ull, ent);
+                if (old == ~0ull || (old >> idb) == key) return;
+            }
+            b = b + 1 == nbk ? 0 : b + 1;
+        }
+    }
     while (true) {
         for (int s = 0; s < BKT; ++s) {
             const unsigned long long old = atomicCAS((unsigned long long*)&t[b].key[s],
@@ -194,11 +217,46 @@ __device__ __forceinline__ int line_find(const Line& l, uint64_t key, uint32_t& 
     id = v;
     return found ? 1 : (empty ? 0 : -1);
 }
+// Packed bucket: two 16-B loads, four entries.
+struct PLine {
+    uint4 v[2];
+};
+__device__ __forceinline__ PLine load_pline(const PBucket* __restrict__ t, uint64_t b) {
+    const uint4* p = reinterpret_cast<const uint4*>(t + b);
+    PLine l;
+    l.v[0] = p[0];
+    l.v[1] = p[1];
+    return l;
+}
+__device__ __forceinline__ int pline_find(const PLine& l, uint64_t key, uint32_t idb, uint32_t& id) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(l.v);
+    bool found = false, empty = false;
+    uint32_t v = 0;
+#pragma unroll
+    for (int s = 0; s < PBKT; ++s) {
+        const uint64_t e = ((uint64_t)w[2 * s + 1] << 32) | w[2 * s];
+        const bool hit = (e >> idb) == key;
+        v = hit ? (uint32_t)(idb >= 32 ? e : (e & ((1ull << idb) - 1))) : v;   // KmerIDs < 2^32
+        found |= hit;
+        empty |= e == ~0ull;
+    }
+    id = v;
+    return found ? 1 : (empty ? 0 : -1);
+}
+// One bucket of either layout: 1 found (id set), 0 absent, -1 full without the key.
+template <bool PK>
+__device__ __forceinline__ int bucket_find(const void* __restrict__ t, uint64_t b, uint64_t key, uint32_t idb,
+                                           uint32_t& id) {
+    if constexpr (PK) return pline_find(load_pline(static_cast<const PBucket*>(t), b), key, idb, id);
+    else return line_find(load_line(static_cast<const Bucket*>(t), b), key, id);
+}
 // Full probe from bucket b: KmerID or -1.
-__device__ __forceinline__ int64_t lk_probe(const Bucket* __restrict__ t, uint64_t nbk, uint64_t key, uint64_t b) {
+template <bool PK>
+__device__ __forceinline__ int64_t lk_probe(const void* __restrict__ t, uint64_t nbk, uint32_t idb, uint64_t key,
+                                            uint64_t b) {
     while (true) {
         uint32_t id;
-        const int r = line_find(load_line(t, b), key, id);
+        const int r = bucket_find<PK>(t, b, key, idb, id);
         if (r > 0) return id;
         if (r == 0) return -1;
         b = b + 1 == nbk ? 0 : b + 1;
@@ -221,9 +279,10 @@ __global__ void __launch_bounds__(256) lk_read_map(const uint64_t* __restrict__ 
 }
 
 struct LkTab {
-    const Bucket* t;
+    const void* t;          // Bucket[nbk], or PBucket[nbk] when idb > 0
     const uint32_t* filt;
     uint64_t nbk, fmask;
+    uint32_t idb;           // packed layout: KmerID bits of an entry (0: the 64-B layout)
 };
 
 // Canonical code of the window ending at p0+j (j compile-time after unrolling).
@@ -256,7 +315,7 @@ __device__ __forceinline__ uint64_t lk_canon_rt(const Frame<LK_P>& f, int j, uin
 
 // K > 0: k known at compile time (masks and the m-mer / k-mer widths fold, narrowing the 64-bit
 // hash multiplies); K == 0: any k.
-template <bool EMIT, int KM, int K = 0>
+template <bool EMIT, int KM, int K = 0, bool PK = false>
 __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk, const uint16_t* __restrict__ vd,
                                                 const unsigned int* __restrict__ sb, uint64_t nbases,
                                                 const uint64_t* __restrict__ offs, uint64_t nreads, int k_rt,
@@ -372,14 +431,23 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
             const bool l0 = i0 < nq, l1 = i1 < nq;
             const uint64_t k0 = l0 ? qkey[wave][i0] : 0ull, k1 = l1 ? qkey[wave][i1] : 0ull;
             const uint64_t b0 = bucket_of(tab_hash(k0), tab.nbk), b1 = bucket_of(tab_hash(k1), tab.nbk);
-            Line L0, L1;
-            if (l0) L0 = load_line(tab.t, b0);
-            if (l1) L1 = load_line(tab.t, b1);
+            using LineK = std::conditional_t<PK, PLine, Line>;
+            LineK L0, L1;
+            auto load_k = [&](uint64_t b) {
+                if constexpr (PK) return load_pline(static_cast<const PBucket*>(tab.t), b);
+                else return load_line(static_cast<const Bucket*>(tab.t), b);
+            };
+            auto find_k = [&](const LineK& l, uint64_t key, uint32_t& id) {
+                if constexpr (PK) return pline_find(l, key, tab.idb, id);
+                else return line_find(l, key, id);
+            };
+            if (l0) L0 = load_k(b0);
+            if (l1) L1 = load_k(b1);
             if (l0) {
                 uint32_t id;
-                int r = line_find(L0, k0, id);
+                int r = find_k(L0, k0, id);
                 if (r < 0) {
-                    const int64_t x = lk_probe(tab.t, tab.nbk, k0, b0 + 1 == tab.nbk ? 0 : b0 + 1);
+                    const int64_t x = lk_probe<PK>(tab.t, tab.nbk, tab.idb, k0, b0 + 1 == tab.nbk ? 0 : b0 + 1);
                     r = x >= 0;
                     id = (uint32_t)x;
                 }
@@ -391,9 +459,9 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
             }
             if (l1) {
                 uint32_t id;
-                int r = line_find(L1, k1, id);
+                int r = find_k(L1, k1, id);
                 if (r < 0) {
-                    const int64_t x = lk_probe(tab.t, tab.nbk, k1, b1 + 1 == tab.nbk ? 0 : b1 + 1);
+                    const int64_t x = lk_probe<PK>(tab.t, tab.nbk, tab.idb, k1, b1 + 1 == tab.nbk ? 0 : b1 + 1);
                     r = x >= 0;
                     id = (uint32_t)x;
                 }
@@ -411,7 +479,7 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
             const int j = __builtin_ctz(ovf);
             ovf &= ovf - 1u;
             const uint64_t key = lk_canon_rt(f, j, mask);
-            const int64_t x = lk_probe(tab.t, tab.nbk, key, bucket_of(tab_hash(key), tab.nbk));
+            const int64_t x = lk_probe<PK>(tab.t, tab.nbk, tab.idb, key, bucket_of(tab_hash(key), tab.nbk));
             if (x >= 0) {
                 hits |= 1u << j;
                 win_kid[gt * LK_P + j] = (uint32_t)x;
@@ -857,26 +925,36 @@ bool segment_sort(hga_ctx* c, const uint64_t* hptr, uint64_t nseg, uint64_t maxl
 void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n) {
     HGA_REQUIRE(k >= 1 && k <= 32, HGA_ERR_INVALID, "k must be in [1,32]");
     auto& L = c->lookup;
-    const uint64_t nbk = std::max<uint64_t>(64, ((uint64_t)HGA_LK_SLOTS10 * n / 10 + BKT - 1) / BKT);   // slot load 10 / HGA_LK_SLOTS10
+    // packed 32-B buckets when a key and its KmerID fit one u64 (HGA_LK_WIDE: test hook for the 64-B layout)
+    const int nbits_id = bits_for(std::max<uint32_t>(n, 1));
+    const uint32_t idb = HGA_LK_PACKED && 2 * k + nbits_id <= 64 && !std::getenv("HGA_LK_WIDE") ? 64u - 2u * (uint32_t)k
+                                                                                                   : 0u;
+    const int bkt = idb ? PBKT : BKT;
+    const uint64_t nbk = std::max<uint64_t>(64, ((uint64_t)HGA_LK_SLOTS10 * n / 10 + bkt - 1) / bkt);   // slot load 10 / HGA_LK_SLOTS10
     uint64_t fw = 1024;
     while (fw * 64 < (uint64_t)HGA_FBITS2 * n) fw <<= 1;   // >= HGA_FBITS2/2 filter bits per key
     L.slots = nbk;   // buckets
+    L.idb = idb;
     L.fwords = fw;
     L.k = k;
     L.km = lk_km_for(k);
     L.n_sdk = n;
-    Bucket* tb = static_cast<Bucket*>(L.tab_key.ensure(nbk * sizeof(Bucket)));
+    Bucket* tb = static_cast<Bucket*>(L.tab_key.ensure(nbk * (idb ? sizeof(PBucket) : sizeof(Bucket))));
     auto* filt = static_cast<uint32_t*>(L.filter.ensure(fw * 4));
     DevBuf tmp;
     uint64_t* dk = static_cast<uint64_t*>(tmp.ensure(std::max<uint64_t>(n, 1) * 8));
     if (n) HGA_HIP(hipMemcpyAsync(dk, keys, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(lk_fill, dim3(blocks_for(nbk * BKT, 256)), dim3(256), 0, c->stream, tb, nbk);
-    c->check_launch("lk_fill");
+    if (idb) {
+        HGA_HIP(hipMemsetAsync(tb, 0xFF, nbk * sizeof(PBucket), c->stream));
+    } else {
+        hipLaunchKernelGGL(lk_fill, dim3(blocks_for(nbk * BKT, 256)), dim3(256), 0, c->stream, tb, nbk);
+        c->check_launch("lk_fill");
+    }
     HGA_HIP(hipMemsetAsync(filt, 0, fw * 4, c->stream));
     if (n) {
         c->launch("lk_build", [&] {
             hipLaunchKernelGGL(lk_build, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, dk, n, tb, nbk, filt,
-                               fw - 1, k, L.km);
+                               fw - 1, k, L.km, idb);
         });
         c->check_launch("lk_build");
     }
@@ -970,14 +1048,19 @@ void lookup_run(hga_ctx* c) {
     const uint16_t* vd = L.valid.as<uint16_t>();
     const unsigned int* sb = L.starts.as<unsigned int>();
     const uint64_t* offs = L.offsets.as<uint64_t>();
-    LkTab tab{L.tab_key.as<Bucket>(), L.filter.as<uint32_t>(), L.slots, L.fwords - 1};
+    LkTab tab{L.tab_key.p, L.filter.as<uint32_t>(), L.slots, L.fwords - 1, L.idb};
     uint64_t H = 0;
     if (n_tiles) {
         c->launch("lk_count", [&] {
-#define HGA_LK_SCAN(KMV, KK)                                                                                 \
-    hipLaunchKernelGGL((lk_scan<false, KMV, KK>), dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, sb, \
-                       nb, offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, (uint32_t*)nullptr,      \
+#define HGA_LK_SCAN2(KMV, KK, PKV)                                                                           \
+    hipLaunchKernelGGL((lk_scan<false, KMV, KK, PKV>), dim3((unsigned)n_tiles), dim3(LK_T), 0, c->stream, pk, vd, \
+                       sb, nb, offs, n, k, L.word_read.as<uint32_t>(), tab, hm, wkid, tile, (uint32_t*)nullptr,  \
                        (uint32_t*)nullptr, (uint32_t*)nullptr)
+#define HGA_LK_SCAN(KMV, KK)                       \
+    do {                                           \
+        if (L.idb) HGA_LK_SCAN2(KMV, KK, true);    \
+        else HGA_LK_SCAN2(KMV, KK, false);         \
+    } while (0)
             if (L.km == LK_KM && k == 19) HGA_LK_SCAN(LK_KM, 19);   // compile-time k for the usual SDK k
             else if (L.km == LK_KM && k == 21) HGA_LK_SCAN(LK_KM, 21);
             else if (L.km == LK_KM) HGA_LK_SCAN(LK_KM, 0);
@@ -986,6 +1069,7 @@ void lookup_run(hga_ctx* c) {
             else if (L.km == 4) HGA_LK_SCAN(4, 15);
             else HGA_LK_SCAN(0, 0);
 #undef HGA_LK_SCAN
+#undef HGA_LK_SCAN2
         });
         c->check_launch("lk_count");
         HGA_HIP(hipMemsetAsync(tile + n_tiles, 0, 8, c->stream));

@@ -50,8 +50,13 @@ def random_case(seed, n_reads, maxlen, k, alphabet, n_sdk):
     return bases, offsets, sdk
 
 
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("k", [1, 3, 11, 19, 21, 31, 32])
-def test_lookup_random_vs_oracle(gpu_ctx, k):
+def test_lookup_random_vs_oracle(gpu_ctx, monkeypatch, k, wide):
+    """wide: the 64-B table buckets (HGA_LK_WIDE) where a key and its KmerID would pack into the
+    32-B ones (lookup.hip PBucket; k = 32 always takes the 64-B layout)."""
+    if wide:
+        monkeypatch.setenv("HGA_LK_WIDE", "1")
     bases, offsets, sdk = random_case(k, 700, 200, k, "ACGTACGTACGTNa", 3000)
     assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 7), oracle.construct_indices(bases, offsets, k, sdk, 7))
 
