@@ -120,8 +120,15 @@ __device__ __forceinline__ uint32_t key_minimizer(uint64_t x, int k, int km, uin
 __device__ __forceinline__ uint32_t end_mix(uint32_t e) {
     return (e ^ (e >> 16)) * 0x9E3779B1u;
 }
-__device__ __forceinline__ uint32_t end_bits(uint32_t x) {   // bits 15..29: three bits of the word
-    return (1u << ((x >> 15) & 31)) | (1u << ((x >> 20) & 31)) | (1u << ((x >> 25) & 31));
+#ifndef HGA_LK_FBITS
+#define HGA_LK_FBITS 3
+#endif
+static_assert(HGA_LK_FBITS >= 1 && HGA_LK_FBITS <= 6, "bit fields of the filter hash below its 2 word-select bits");
+__device__ __forceinline__ uint32_t end_bits(uint32_t x) {   // HGA_LK_FBITS bits of the word (5-bit fields from bit 25 down)
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < HGA_LK_FBITS; ++i) m |= 1u << ((x >> (25 - 5 * i)) & 31);
+    return m;
 }
 __device__ __forceinline__ uint64_t end_word(uint32_t minh, uint32_t x, uint64_t fmask) {
     return ((((uint64_t)minh) << 2) | (x >> 30)) & fmask;
