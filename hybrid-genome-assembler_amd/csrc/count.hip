@@ -136,6 +136,39 @@ __device__ __forceinline__ void store_at(T* dst, uint32_t i, T v) {
     *reinterpret_cast<T*>(reinterpret_cast<char*>(dst) + (uint32_t)(i * (uint32_t)sizeof(T))) = v;
 }
 
+#ifndef HGA_B1_BUFST
+#define HGA_B1_BUFST 1   // kc_bin1's flush through buffer stores (0: global stores, 64-bit lane addresses)
+#endif
+// dst[0, n) = src[0, n) by one wave (dst wave-uniform): buffer stores off a descriptor built from the
+// run's uniform base, so each store takes a 32-bit lane offset instead of 64-bit address arithmetic
+// (the descriptor's record count is the run's length: a lane past it stores nothing)
+template <class T>
+__device__ __forceinline__ void store_run(T* dst, uint32_t n, const T* src, uint32_t lane) {
+    if (!HGA_B1_BUFST) {
+        for (uint32_t jj = lane; jj < n; jj += 64) store_at(dst, jj, src[jj]);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(n * (uint32_t)sizeof(T)), 0x00020000);
+    // four elements per lane and round, read and stored unpredicated: src has 256 readable elements past
+    // any run (the caller's padding) and the descriptor drops the stores past n
+    for (uint32_t j0 = 0; j0 < n; j0 += 256) {
+        T v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src[j0 + 64u * (uint32_t)u + lane];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t jj = j0 + 64u * (uint32_t)u + lane;
+            if constexpr (sizeof(T) == 4) {
+                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v[u], rs, (int)(jj * 4u), 0, 0);
+            } else {
+                typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{(uint32_t)v[u], (uint32_t)((uint64_t)v[u] >> 32)}, rs,
+                                                      (int)(jj * 8u), 0, 0);
+            }
+        }
+    }
+}
+
 // Level-1 blocks: every workgroup takes BLK-element blocks per region from one pool with a
 // single atomic (and a new one only when a block fills), so a tile's region runs are
 // written without any global atomic.  block table entry: start, used, file<<8 | region.
@@ -145,6 +178,7 @@ struct Blk {
     uint32_t tag;
 };
 constexpr uint32_t BLK = TP_B;   // >= a tile, so a tile's run spans at most two blocks
+static_assert(BLK < 65536, "kc_bin1 packs a block count and a run offset in 16 bits each");
 
 // gstat: [0] row cursor, [1] max split, [2] error bits (1 unsplittable, 2 row capacity,
 // 4 level-1 pool exhausted), [3] blocks used, [4] instances.
@@ -198,9 +232,10 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
     __shared__ uint32_t bent[NB1_MAX];               // its table entry
     __shared__ uint32_t nchain[NB1_MAX];             // blocks this workgroup used per region
     __shared__ unsigned long long base_a[NB1_MAX], base_b[NB1_MAX];
-    __shared__ uint32_t take_a[NB1_MAX];
+    __shared__ uint2 fl_n[NB1_MAX];                  // flush: elements into the current / the fresh block
     __shared__ uint32_t fhist[MAX_NB + (HGA_B1_BRANCHFREE ? 64 : 0)];
-    __shared__ E1 stage[TP_B + 64];   // + one dummy slot per lane for invalid windows
+    // + one dummy slot per lane for invalid windows, + 256 readable past any run (store_run's rounds)
+    __shared__ E1 stage[TP_B + 64 + 256];
     __shared__ uint32_t ws[NT_B / 64 + 1];
     // packed words [t0/16 - 2, t0/16 + 512) of this tile and the next (code | valid << 32)
     __shared__ uint64_t lpw[2][TP_B / 16 + 2];
@@ -316,10 +351,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
                 off1[tid] = inc - c;
                 cnt1[tid] = 0;
                 base_a[tid] = bstart[tid] + bfill[tid];
-                if (!spill) {
-                    take_a[tid] = c;
-                    bfill[tid] += c;
-                }
+                if (!spill) bfill[tid] += c;
             }
             // ONE returning atomic per workgroup and tile for all spilling runs: regions fill in
             // lockstep, so at a C4 shard every lane of every workgroup spills in the same tiles (one
@@ -331,7 +363,6 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
                 if (tid == l0) e0 = atomicAdd(&gstat[3], (unsigned long long)__popcll(sm));
                 e0 = __shfl(e0, l0, 64);
                 if (spill) {
-                    take_a[tid] = room;
                     if (bent[tid] != 0xFFFFFFFFu) table[bent[tid]].used = BLK;
                     unsigned long long st;
                     bent[tid] = claim_block(e0 + (unsigned long long)__popcll(sm & ((1ull << tid) - 1ull)), gstat,
@@ -343,6 +374,13 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
                 }
             }
             if (tid == 63) off1[nb1] = inc;
+            if (tid < (int)nb1) {   // the flush's two pieces per region, clipped to the pool here once
+                const uint32_t na = spill ? room : c, nb = c - na;
+                const uint64_t ba = base_a[tid], bb = spill ? base_b[tid] : 0ull;
+                // y: the fresh block's count | its first element's run offset << 16 (both <= BLK < 2^16)
+                fl_n[tid] = make_uint2(ba < pool_cap ? (uint32_t)min<uint64_t>(pool_cap - ba, na) : 0u,
+                                       (nb && bb < pool_cap ? (uint32_t)min<uint64_t>(pool_cap - bb, nb) : 0u) | na << 16);
+            }
         }
         lds_barrier();
         {   // all 16 run offsets read first (no wait per element), then the writes
@@ -358,26 +396,13 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
         // (run values made wave-uniform: scalar base addresses, 32-bit lane offsets, no per-element
         // 64-bit select / bound check)
         const uint32_t lane = (uint32_t)(tid & 63);
+        // (a piece past the pool — table exhausted, error bit set — was clipped to nothing by wave 0)
         for (uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6); d < nb1; d += NT_B / 64) {
             const uint32_t o = __builtin_amdgcn_readfirstlane(off1[d]);
-            const uint32_t len = __builtin_amdgcn_readfirstlane(off1[d + 1]) - o;
-            const uint32_t ta = __builtin_amdgcn_readfirstlane(take_a[d]);
-            const uint32_t na = len < ta ? len : ta;
-            const uint64_t ba = readfirstlane64(base_a[d]);
-            if (ba < pool_cap) {   // a block past the pool (table exhausted, error bit set) drops its writes
-                E1* __restrict__ dst = out1 + ba;
-                const uint32_t lim = (uint32_t)(pool_cap - ba < na ? pool_cap - ba : na);
-                for (uint32_t jj = lane; jj < lim; jj += 64) store_at(dst, jj, stage[o + jj]);
-            }
-            if (len > na) {   // the part past a full block, into the fresh one
-                const uint64_t bb = readfirstlane64(base_b[d]);
-                if (bb < pool_cap) {
-                    E1* __restrict__ dst = out1 + bb;
-                    const uint32_t n2 = len - na;
-                    const uint32_t lim = (uint32_t)(pool_cap - bb < n2 ? pool_cap - bb : n2);
-                    for (uint32_t jj = lane; jj < lim; jj += 64) store_at(dst, jj, stage[o + na + jj]);
-                }
-            }
+            const uint2 n2 = fl_n[d];
+            const uint32_t na = __builtin_amdgcn_readfirstlane(n2.x), y = __builtin_amdgcn_readfirstlane(n2.y);
+            if (na) store_run(out1 + readfirstlane64(base_a[d]), na, stage + o, lane);
+            if (y & 0xFFFFu) store_run(out1 + readfirstlane64(base_b[d]), y & 0xFFFFu, stage + o + (y >> 16), lane);
         }
         lds_barrier();
     }
