@@ -227,6 +227,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
                                                 unsigned long long* __restrict__ gstat) {
     __shared__ uint32_t cnt1[NB1_MAX + (HGA_B1_BRANCHFREE ? 64 : 0)];
     __shared__ uint32_t off1[NB1_MAX + 1];
+    __shared__ uint32_t offb[NB1_MAX];               // the same run offsets in bytes of the stage
     __shared__ unsigned long long bstart[NB1_MAX];   // current block of each region
     __shared__ uint32_t bfill[NB1_MAX];              // elements already in it
     __shared__ uint32_t bent[NB1_MAX];               // its table entry
@@ -322,33 +323,37 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
             // (k < 32: h < 4^k, so a shift by the full width 2k already gives region / bucket 0)
             constexpr int R1B = 2 * K - (FB < MAX_FB1 ? FB : MAX_FB1), RB = 2 * K - FB;
             const uint32_t r1s = K && FB ? (uint32_t)R1B : kp.r1bits, rbs = K && FB ? (uint32_t)RB : kp.rbits;
-            dd[j] = K && K < 32 ? (uint32_t)(h >> r1s) : region_of(h, kp);
+            // Byte units: the region counters count sizeof(E1) per element, so a rank is the element's
+            // byte offset in its stage run and dd the region's byte offset in the counter / run-offset
+            // arrays (the stage needs no index scaling).  An invalid window is staged into this lane's
+            // dummy slot TP_B + lane: "region" 0 (whose run offset is 0) with that rank.
+            const bool ok = (wm >> j) & 1u;
+            const uint32_t reg = K && K < 32 ? (uint32_t)(h >> r1s) : region_of(h, kp);
+            dd[j] = ok ? reg * 4u : 0u;
             // (u32 elements of a k with 2k - MAX_FB1 >= 32: r1bits == 32, the truncation is the mask)
             constexpr bool trunc = K && sizeof(E1) == 4 && 2 * K - MAX_FB1 >= 32;
             ee[j] = trunc ? (E1)h : (E1)(h & kp.r1mask);
+            rk[j] = ((uint32_t)TP_B + (uint32_t)(tid & 63)) * (uint32_t)sizeof(E1);
             if (HGA_B1_BRANCHFREE) {   // invalid windows count into this lane's dummy counters
-                const bool ok = (wm >> j) & 1u;
-                const uint32_t r = atomicAdd(&cnt1[ok ? dd[j] : NB1_MAX + (uint32_t)(tid & 63)], 1u);
+                const uint32_t r = atomicAdd(&cnt1[ok ? reg : NB1_MAX + (uint32_t)(tid & 63)], (uint32_t)sizeof(E1));
                 atomicAdd(&fhist[ok ? (K && K < 32 ? (uint32_t)(h >> kp.rbits) : bucket_of(h, kp))
                                     : MAX_NB + (uint32_t)(tid & 63)], 1u);
-                rk[j] = ok ? r : ~0u;
-            } else {
-                rk[j] = ~0u;   // invalid window: staged into this lane's dummy slot (no mask kept live)
-                if ((wm >> j) & 1u) {
-                    rk[j] = atomicAdd(&cnt1[dd[j]], 1u);
-                    atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> rbs) : bucket_of(h, kp)], 1u);
-                }
+                if (ok) rk[j] = r;
+            } else if (ok) {
+                rk[j] = atomicAdd(&cnt1[reg], (uint32_t)sizeof(E1));
+                atomicAdd(&fhist[K && K < 32 ? (uint32_t)(h >> rbs) : bucket_of(h, kp)], 1u);
             }
         }
         inst += __popc(wm);
         lds_barrier();
         if (tid < 64) {   // one wave: scan the <= 64 region counts, place them in the blocks
-            const uint32_t c = tid < (int)nb1 ? cnt1[tid] : 0u;
+            const uint32_t c = tid < (int)nb1 ? cnt1[tid] / (uint32_t)sizeof(E1) : 0u;   // (byte units)
             const uint32_t inc = wave_scan_add_dpp(c);   // wave 0, all lanes active
             const uint32_t room = tid < (int)nb1 ? BLK - bfill[tid] : 0u;
             const bool spill = tid < (int)nb1 && c > room;   // the run spills into a fresh block
             if (tid < (int)nb1) {
                 off1[tid] = inc - c;
+                offb[tid] = (inc - c) * (uint32_t)sizeof(E1);
                 cnt1[tid] = 0;
                 base_a[tid] = bstart[tid] + bfill[tid];
                 if (!spill) bfill[tid] += c;
@@ -386,10 +391,10 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
         {   // all 16 run offsets read first (no wait per element), then the writes
             uint32_t o1[P_B];
 #pragma unroll
-            for (int j = 0; j < P_B; ++j) o1[j] = off1[dd[j]];
+            for (int j = 0; j < P_B; ++j) o1[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(offb) + dd[j]);
 #pragma unroll
-            for (int j = 0; j < P_B; ++j)
-                stage[rk[j] != ~0u ? o1[j] + rk[j] : (uint32_t)TP_B + (uint32_t)(tid & 63)] = ee[j];
+            for (int j = 0; j < P_B; ++j)   // (offb[0] == 0)
+                *reinterpret_cast<E1*>(reinterpret_cast<char*>(stage) + o1[j] + rk[j]) = ee[j];
         }
         lds_barrier();
         // flush: one wave per region run (region-uniform bases, lanes on consecutive elements)
