@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(NT_B, HGA_B1_WAVES) kc_bin1(const BinFile* __r
         }
 #pragma unroll
         for (int j = 0; j < P_B; ++j) {
-            const uint64_t h = mix_fwd(frame_canon<P_B>(f, j, wmask), mx);
+            const uint64_t h = mix_fwd_k<K>(frame_canon<P_B>(f, j, wmask), mx);
             // (k < 32: h < 4^k, so a shift by the full width 2k already gives region / bucket 0)
             constexpr int R1B = 2 * K - (FB < MAX_FB1 ? FB : MAX_FB1), RB = 2 * K - FB;
             const uint32_t r1s = K && FB ? (uint32_t)R1B : kp.r1bits, rbs = K && FB ? (uint32_t)RB : kp.rbits;

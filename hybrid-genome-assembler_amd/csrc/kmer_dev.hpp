@@ -42,6 +42,33 @@ inline uint64_t inv_odd_u64(uint64_t a) {  // a * x == 1 mod 2^64 (Newton)
 // then needs one 32x32->64 multiply-add and one low multiply instead of three quarter-rate
 // multiplies (x_lo * c_hi vanishes mod 2^38).  Any odd constant gives a bijection.
 constexpr uint64_t kMixC1 = 0x9E3779C07F4A7C15ull;
+// mix_fwd for a compile-time 16 < K <= 19 with kMixC1 (what make_mix(K) gives): x * c1 mod 2^(2K) as the
+// low words' 32x32->64 product plus the high word's contribution, of which only the low 2K - 32 bits
+// count — a small multiply by c1 mod 64 (c1's high word, a multiple of 64, contributes nothing below
+// 2^38) — one 64-bit multiply-add instead of two.  Equal to mix_fwd.
+#ifndef HGA_MIX_K
+#define HGA_MIX_K 1
+#endif
+template <int K>
+__device__ __forceinline__ uint64_t mix_fwd_k(uint64_t x, const Mix& m) {
+    if constexpr (HGA_MIX_K && K > 16 && K <= 19) {
+        static_assert((kMixC1 >> 32) % 64 == 0, "c1's high word must vanish below 2^38");
+        constexpr uint32_t CL = (uint32_t)kMixC1;
+        const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+        // one v_mad_u64_u32 with the small product as the high word of its addend (written out: the
+        // compiler otherwise re-derives the 64-bit product and issues two)
+        const uint64_t add = (uint64_t)(xh * (CL & 63u)) << 32;
+        uint64_t p;
+        uint64_t carry;
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(p), "=s"(carry) : "v"(xl), "s"(CL), "v"(add));
+        (void)carry;
+        const uint64_t y = p & ((1ull << (2 * K)) - 1);
+        return y ^ (y >> ((2 * K + 1) / 2));
+    } else {
+        return mix_fwd(x, m);
+    }
+}
+
 inline Mix make_mix(int k) {
     Mix m;
     m.n = 2u * (uint32_t)k;
