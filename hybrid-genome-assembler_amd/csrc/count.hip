@@ -1188,6 +1188,20 @@ __device__ __forceinline__ void match_s(const KGrp kg, uint32_t r, int& w, int& 
     }
 }
 
+// The slot of r in a loaded group, -1 if absent (keys are unique in the table: at most one match).
+__device__ __forceinline__ int match_hit_s(const KGrp kg, uint32_t r) {
+    uint32_t k[GS_S];
+    if constexpr (GS_S == 4) {
+        k[0] = kg.x; k[1] = kg.y; k[2] = reinterpret_cast<const uint4&>(kg).z; k[3] = reinterpret_cast<const uint4&>(kg).w;
+    } else {
+        k[0] = kg.x; k[1] = kg.y;
+    }
+    int w = k[0] == r ? 0 : -1;
+#pragma unroll
+    for (int t = 1; t < GS_S; ++t) w = k[t] == r ? t : w;
+    return w;
+}
+
 // Settle key r (+inc) from its home group; false if MAXPROBE_P groups were full.
 __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t r, uint32_t inc) {
     uint32_t g = r & (G_S - 1);
@@ -1214,6 +1228,11 @@ __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t
 }
 
 
+// LAZY: the batch only finds existing keys (a hit is one add); a key not in its home group goes
+// through the miss queue, which claims new keys with all lanes busy — cheaper where most instances
+// repeat a key (C2: ~12 instances per distinct key and bucket, kc_count_s 0.47 -> 0.39 ms); otherwise
+// the home group's first empty slot is claimed inline (C4 rank shard: ~5 per key, 9.7 vs 10.0 ms).
+template <bool LAZY>
 __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t* __restrict__ binned,
                                                       const uint64_t* __restrict__ fs, uint32_t F,
                                                       uint32_t min_count, KP kp, uint64_t* __restrict__ out_key,
@@ -1321,7 +1340,12 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
 #pragma unroll
                 for (int q = 0; q < PF_P; ++q) {
                     int w, e0;
-                    match_s(kg[q], rv[q], w, e0);
+                    if (LAZY) {   // new keys go through the miss queue (claimed there, all lanes busy)
+                        w = match_hit_s(kg[q], rv[q]);
+                        e0 = -1;
+                    } else {
+                        match_s(kg[q], rv[q], w, e0);
+                    }
                     const bool live = rv[q] != 0xFFFFFFFFu;
                     slot[q] = (rv[q] & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
                     {   // every lane adds: a hit to its slot, anything else to its own dummy word
@@ -2383,9 +2407,17 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
     if (packed && e32) {
         uint32_t* blist = static_cast<uint32_t*>(s.blist.ensure((size_t)nbc * 4));
         c->launch("kc_count", [&] {
-            hipLaunchKernelGGL(kc_count_s, dim3(nbc), dim3(NT_P), 0, c->stream,
-                               static_cast<const uint32_t*>(binned), fs, F, min_per_file, kp, s.rows_key.as<uint64_t>(),
-                               s.rows_cnt.as<uint32_t>(), cap, gstat, blist, d_xe);
+            // instances per count bucket: >= 32 K (C2-sized) -> the lazy claim (HGA_CS_LAZY=0/1 forces)
+            const char* le = std::getenv("HGA_CS_LAZY");
+            const bool lazy = le ? std::atoi(le) != 0 : (total_bytes >> kp.fb) >= 32768;
+            if (lazy)
+                hipLaunchKernelGGL(kc_count_s<true>, dim3(nbc), dim3(NT_P), 0, c->stream,
+                                   static_cast<const uint32_t*>(binned), fs, F, min_per_file, kp,
+                                   s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, blist, d_xe);
+            else
+                hipLaunchKernelGGL(kc_count_s<false>, dim3(nbc), dim3(NT_P), 0, c->stream,
+                                   static_cast<const uint32_t*>(binned), fs, F, min_per_file, kp,
+                                   s.rows_key.as<uint64_t>(), s.rows_cnt.as<uint32_t>(), cap, gstat, blist, d_xe);
             // buckets with a per-file run >= 65536 (listed in blist, count in gstat[5])
             hipLaunchKernelGGL(kc_count<uint32_t>, dim3(std::min<uint32_t>(nbc, (uint32_t)c->num_cu)), dim3(NT_C), 0,
                                c->stream, static_cast<const uint32_t*>(binned), fs, F, T, maxload, min_per_file, kp,

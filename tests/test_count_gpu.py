@@ -99,6 +99,23 @@ def test_count_edge_inputs(gpu_ctx):
         assert_same(run_gpu(gpu_ctx, streams, 4, 1, 10 ** 9, min_count=1), o)
 
 
+@pytest.mark.parametrize("lazy", ["0", "1"])
+def test_count_claim_modes(gpu_ctx, hga_mod, monkeypatch, lazy):
+    """kc_count_s with new keys claimed inline (0) or through the miss queue (1), forced either way
+    (count_run picks by instances per bucket): random, all-distinct (table splits) and heavy inputs."""
+    monkeypatch.setenv("HGA_CS_LAZY", lazy)
+    streams = random_streams(19, 2, 400, 120, "ACGTACGTACGTNacgt")
+    assert_same(run_gpu(gpu_ctx, streams, 19, 2, 6), oracle.count_pipeline(streams, 19, 2, 6))
+    g = hga_mod.gen_genome(3_000_000, 77)
+    streams = [g[:1_500_000], g[1_500_000:]]
+    r = run_gpu(gpu_ctx, streams, 25, 1, 5, min_count=1)
+    assert_same(r, oracle.count_pipeline(streams, 25, 1, 5, min_count=1))
+    assert r["stats"].max_split > 1
+    streams = [b"A" * 5000 + b"\n" + b"ACGT" * 3000, b"A" * 10]
+    assert_same(run_gpu(gpu_ctx, streams, 13, 1, 10 ** 9, min_count=1),
+                oracle.count_pipeline(streams, 13, 1, 10 ** 9, min_count=1))
+
+
 def test_count_split_buckets_all_distinct(gpu_ctx, hga_mod):
     # coverage-1 random reads: every k-mer distinct -> buckets exceed the LDS table and
     # must be split into sub-ranges
