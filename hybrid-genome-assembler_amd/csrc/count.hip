@@ -1188,8 +1188,9 @@ __device__ __forceinline__ void match_s(const KGrp kg, uint32_t r, int& w, int& 
     }
 }
 
-// The slot of r in a loaded group, -1 if absent (keys are unique in the table: at most one match).
-__device__ __forceinline__ int match_hit_s(const KGrp kg, uint32_t r) {
+// The byte offset of r in a loaded group (4 x its slot), -1 if absent (keys are unique in the table:
+// at most one match).
+__device__ __forceinline__ int match_hit4_s(const KGrp kg, uint32_t r) {
     uint32_t k[GS_S];
     if constexpr (GS_S == 4) {
         k[0] = kg.x; k[1] = kg.y; k[2] = reinterpret_cast<const uint4&>(kg).z; k[3] = reinterpret_cast<const uint4&>(kg).w;
@@ -1198,7 +1199,7 @@ __device__ __forceinline__ int match_hit_s(const KGrp kg, uint32_t r) {
     }
     int w = k[0] == r ? 0 : -1;
 #pragma unroll
-    for (int t = 1; t < GS_S; ++t) w = k[t] == r ? t : w;
+    for (int t = 1; t < GS_S; ++t) w = k[t] == r ? 4 * t : w;
     return w;
 }
 
@@ -1334,18 +1335,31 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                     }
                 }
                 KGrp kg[PF_P];
-#pragma unroll
-                for (int q = 0; q < PF_P; ++q) kg[q] = read_keys_s(tkey, rv[q] & (G_S - 1));
-                uint32_t claim = 0, miss = 0, slot[PF_P];
+                uint32_t ga[PF_P];   // byte offset of each home group (keys; counts at the same offset)
 #pragma unroll
                 for (int q = 0; q < PF_P; ++q) {
-                    int w, e0;
-                    if (LAZY) {   // new keys go through the miss queue (claimed there, all lanes busy)
-                        w = match_hit_s(kg[q], rv[q]);
-                        e0 = -1;
-                    } else {
-                        match_s(kg[q], rv[q], w, e0);
+                    ga[q] = (rv[q] & (G_S - 1)) * (GS_S * 4u);
+                    kg[q] = *reinterpret_cast<const KGrp*>(reinterpret_cast<const char*>(tkey) + ga[q]);
+                }
+                uint32_t claim = 0, miss = 0, slot[PF_P];
+                if constexpr (LAZY) {   // new keys go through the miss queue (claimed there, all lanes busy)
+                    // byte addresses: the group's key offset, + the match's byte offset = its count word
+                    // (tkey and tcnt share the layout); a lane without a hit adds to its dummy word
+#pragma unroll
+                    for (int q = 0; q < PF_P; ++q) {
+                        const int w4 = match_hit4_s(kg[q], rv[q]);
+                        const bool live = rv[q] != 0xFFFFFFFFu;
+                        const bool hit = live && w4 >= 0;
+                        atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tcnt) +
+                                                              (hit ? ga[q] + (uint32_t)w4 : (T_S + lane) * 4u)),
+                                  inc);
+                        miss |= (live && !hit) ? 1u << q : 0u;
                     }
+                }
+#pragma unroll
+                for (int q = 0; q < PF_P && !LAZY; ++q) {
+                    int w, e0;
+                    match_s(kg[q], rv[q], w, e0);
                     const bool live = rv[q] != 0xFFFFFFFFu;
                     slot[q] = (rv[q] & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
                     {   // every lane adds: a hit to its slot, anything else to its own dummy word
