@@ -1712,7 +1712,7 @@ __global__ void kc_spec_publish(unsigned long long* __restrict__ ctrl, const uns
 }
 
 #ifndef HGA_SEL_GRID
-#define HGA_SEL_GRID 1024u   // kc_select workgroups (each takes a contiguous range of chunks)
+#define HGA_SEL_GRID 1024u   // kc_select workgroups at most (each takes a contiguous range of chunks)
 #endif
 constexpr int SEL_R = 16;   // rows per thread: chunks of NT_H * SEL_R = 4096 rows
 constexpr uint32_t SEL_HB = 4096;   // top-12-bit histogram of the kept keys (the export sort's MSD pass)
@@ -2686,7 +2686,11 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
         s.sel_grid = (uint32_t)std::min<uint64_t>((uint64_t)nb * c->num_cu, HGA_SEL_GRID);
         if (const char* e = std::getenv("HGA_SEL_GRID_X")) s.sel_grid = std::max(1, std::atoi(e));   // tuning
     }
-    const uint32_t cpw = (uint32_t)blocks_for(chunks, s.sel_grid);   // chunks per workgroup
+    // below 32 M rows half the grid: the export sort's column scan runs over every workgroup's digit
+    // histogram (C2: -0.005 ms; a C4 shard's 515 M rows keep the whole grid, 1.65 vs 1.93 ms)
+    const uint32_t sel_grid = s.rows < (1ull << 25) && !std::getenv("HGA_SEL_GRID_X") ? std::min(s.sel_grid, 512u)
+                                                                                        : s.sel_grid;
+    const uint32_t cpw = (uint32_t)blocks_for(chunks, sel_grid);   // chunks per workgroup
     const unsigned grid = (unsigned)blocks_for(chunks, cpw);
     const uint64_t region = (uint64_t)cpw * NT_H * SEL_R;
     const size_t hb = (size_t)SEL_HB * 4;
