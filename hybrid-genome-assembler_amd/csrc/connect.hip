@@ -420,6 +420,9 @@ constexpr uint32_t CNW_CAP = HGA_CNW_CAP;
 constexpr uint32_t CNW_W = 512;            // pairs per owner-map window
 constexpr int CNW_U = CNW_W / 64;
 constexpr int CNW_WAVES = HGA_CNW_WAVES;
+#ifndef HGA_CN_HOME
+#define HGA_CN_HOME 1   // cn_wave: home-slot hits first, the rest through a per-wave queue (0: per-lane inserts)
+#endif
 #ifndef HGA_CNW_GRAB
 #define HGA_CNW_GRAB 2
 #endif
@@ -431,10 +434,12 @@ constexpr int CNW_WAVES = HGA_CNW_WAVES;
 #endif
 constexpr uint32_t CNW_GRAB = HGA_CNW_GRAB;   // pivots per work-counter atomic
 
+constexpr uint32_t CNW_Q = 128;   // per-wave queue of a window's candidates not found at their home slot
 struct CnWaveLds {
     uint64_t tab[CNW_CAP];
     uint64_t base[64];             // per hit of the chunk: kci offset of its list minus its first pair index
     uint64_t own[CNW_W / 8];       // owner map, one byte per pair of the window
+    uint32_t q[CNW_Q];
     uint32_t fill, ovf;
 };
 static_assert(CNW_U == 8, "owner map: eight pairs (one u64 of bytes) per lane");
@@ -541,17 +546,46 @@ __global__ void __launch_bounds__(64 * CNW_WAVES, HGA_CNW_MINW) cn_wave(CnIn in,
                     cand[u] = CN_EMPTY;
                     if (j < T) cand[u] = in.kci[W.base[own8[j - w0]] + j];
                 }
+                // a candidate already at its home slot (most walks repeat a candidate) is one count add;
+                // the rest go through the wave's queue and are inserted with every lane busy (a lane's own
+                // probe loops would run with most lanes idle)
+                uint32_t miss = 0;
+                if (HGA_CN_HOME) {
+                    uint32_t hs[CNW_U];
+                    uint64_t hv[CNW_U];
 #pragma unroll
-                for (int u = 0; u < CNW_U; ++u)
-                    if (cand[u] != CN_EMPTY && cand[u] != p
-#ifdef HGA_CN_DIAG_HALF
-                        && cand[u] > p
-#endif
-#ifdef HGA_CN_DIAG_NOINS
-                        && cand[u] == 0xFFFFFFF0u
-#endif
-                    )
-                        (void)cn_insert64(W.tab, CNW_CAP - 1, cand[u], &W.fill, limit, &W.ovf);
+                    for (int u = 0; u < CNW_U; ++u) {
+                        hs[u] = cn_hash(cand[u]) & (CNW_CAP - 1);
+                        hv[u] = (cand[u] != CN_EMPTY && cand[u] != p) ? __atomic_load_n(&W.tab[hs[u]], __ATOMIC_RELAXED)
+                                                                       : CN_EMPTY64;
+                    }
+#pragma unroll
+                    for (int u = 0; u < CNW_U; ++u) {
+                        if (cand[u] == CN_EMPTY || cand[u] == p) continue;
+                        if ((uint32_t)hv[u] == cand[u]) atomicAdd((unsigned long long*)&W.tab[hs[u]], 1ull << 32);
+                        else miss |= 1u << u;
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < CNW_U; ++u)
+                        if (cand[u] != CN_EMPTY && cand[u] != p) miss |= 1u << u;
+                }
+                const uint32_t nm = (uint32_t)__popc(miss);
+                const uint32_t qinc = wave_scan_add_dpp(nm);
+                const uint32_t qtot = wave_lane(qinc, 63);
+                if (HGA_CN_HOME && qtot <= CNW_Q) {
+                    uint32_t pos = qinc - nm;
+#pragma unroll
+                    for (int u = 0; u < CNW_U; ++u)
+                        if ((miss >> u) & 1u) W.q[pos++] = cand[u];
+                    wave_lds_sync();
+                    for (uint32_t i = lane; i < qtot; i += 64)
+                        (void)cn_insert64(W.tab, CNW_CAP - 1, W.q[i], &W.fill, limit, &W.ovf);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < CNW_U; ++u)
+                        if ((miss >> u) & 1u) (void)cn_insert64(W.tab, CNW_CAP - 1, cand[u], &W.fill, limit, &W.ovf);
+                }
                 wave_lds_sync();
                 ok = __atomic_load_n(&W.ovf, __ATOMIC_RELAXED) == 0;
             }
