@@ -448,73 +448,6 @@ __global__ void __launch_bounds__(256) kc_transpose(const uint32_t* __restrict__
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) off[(uint64_t)nb * W] = 0;
 }
 
-// The same layout without the transposed copy and the generic scan (two kernels, wcnt read three
-// times from L2, off written once, coalesced): kc_col_tot sums every fine bucket's column of wcnt;
-// kc_col_scan gives each workgroup OB consecutive buckets — their output is one contiguous range
-// off[b0 * W, (b0 + OB) * W) — scans each column in 16 segments, stages the in-bucket offsets in LDS
-// and writes the range with the buckets' bases (the sum of the earlier buckets' totals) added.
-// Requires nb % OB == 0 and W <= OFF_WMAX (else the transpose + scan above).
-constexpr uint32_t OB = 16;
-constexpr uint32_t OFF_WMAX = 1024;
-__global__ void __launch_bounds__(256) kc_col_tot(const uint32_t* __restrict__ wcnt, uint32_t W, uint32_t nb,
-                                                  uint64_t* __restrict__ tot) {
-    __shared__ uint64_t part[256 / OB][OB];
-    const uint32_t bl = threadIdx.x % OB, sg = threadIdx.x / OB;
-    const uint32_t b = blockIdx.x * OB + bl;
-    uint64_t sum = 0;
-    for (uint32_t w = sg; w < W; w += 256 / OB) sum += wcnt[(uint64_t)w * nb + b];
-    part[sg][bl] = sum;
-    __syncthreads();
-    if (threadIdx.x < OB) {
-        uint64_t t = 0;
-#pragma unroll
-        for (uint32_t g = 0; g < 256 / OB; ++g) t += part[g][threadIdx.x];
-        tot[blockIdx.x * OB + threadIdx.x] = t;
-    }
-}
-__global__ void __launch_bounds__(256) kc_col_scan(const uint32_t* __restrict__ wcnt, uint32_t W, uint32_t nb,
-                                                   const uint64_t* __restrict__ tot, uint64_t* __restrict__ off) {
-    constexpr uint32_t NS = 256 / OB;   // column segments
-    __shared__ uint32_t st[OB * (OFF_WMAX + 1)];   // in-bucket exclusive offsets (a bucket holds < 2^32), rows padded
-    __shared__ uint32_t segs[NS][OB];
-    __shared__ uint64_t red[256 / 64];
-    __shared__ uint64_t bbase[OB + 1];
-    const uint32_t bl = threadIdx.x % OB, sg = threadIdx.x / OB;
-    const uint32_t b0 = blockIdx.x * OB, b = b0 + bl;
-    const uint32_t ch = (W + NS - 1) / NS, w0 = sg * ch, w1 = min(W, w0 + ch);
-    uint32_t ssum = 0;
-    for (uint32_t w = w0; w < w1; ++w) ssum += wcnt[(uint64_t)w * nb + b];
-    segs[sg][bl] = ssum;
-    // the sum of the totals of buckets [0, b0): a block reduction
-    uint64_t pre = 0;
-    for (uint32_t i = threadIdx.x; i < b0; i += 256) pre += tot[i];
-#pragma unroll
-    for (int o = 32; o; o >>= 1) pre += __shfl_xor(pre, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pre;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t base = red[0] + red[1] + red[2] + red[3];
-        for (uint32_t i = 0; i < OB; ++i) {
-            bbase[i] = base;
-            base += tot[b0 + i];
-        }
-        bbase[OB] = base;
-    }
-    uint32_t sbase = 0;
-    for (uint32_t g = 0; g < sg; ++g) sbase += segs[g][bl];
-    for (uint32_t w = w0; w < w1; ++w) {
-        st[bl * (W + 1) + w] = sbase;
-        sbase += wcnt[(uint64_t)w * nb + b];
-    }
-    __syncthreads();
-    uint64_t* __restrict__ o = off + (uint64_t)b0 * W;
-    for (uint32_t i = threadIdx.x; i < OB * W; i += 256) {
-        const uint32_t r = i / W;
-        o[i] = bbase[r] + st[i + r];
-    }
-    if (b0 + OB == nb && threadIdx.x == 0) off[(uint64_t)nb * W] = bbase[OB];
-}
-
 // fs[b*(F+1)+f] = start of file f's run in fine bucket b, fs[b*(F+1)+F] = bucket end.
 __global__ void kc_fs(const uint64_t* __restrict__ off, const BinFile* __restrict__ files, uint32_t W,
                       uint32_t nb, uint32_t F, uint64_t* __restrict__ fs) {
@@ -1778,9 +1711,6 @@ __global__ void kc_spec_publish(unsigned long long* __restrict__ ctrl, const uns
     if (run && t < 8) hrun[t] = run[t];
 }
 
-#ifndef HGA_COL_SCAN
-#define HGA_COL_SCAN 0   // 1: layout by kc_col_tot + kc_col_scan (0: kc_transpose + the generic scan)
-#endif
 #ifndef HGA_SEL_GRID
 #define HGA_SEL_GRID 1024u   // kc_select workgroups at most (each takes a contiguous range of chunks)
 #endif
@@ -2365,22 +2295,12 @@ void count_run(hga_ctx* c, uint32_t min_per_file) {
         c->check_launch("kc_bin1");
     }
     // L: (bucket, workgroup) output offsets and per-file bucket runs
-    if (HGA_COL_SCAN && W >= 1 && W <= OFF_WMAX && nb % OB == 0) {
-        uint64_t* tot = static_cast<uint64_t*>(s.scratch.ensure((size_t)nb * 8));
-        c->launch("kc_layout", [&] {
-            hipLaunchKernelGGL(kc_col_tot, dim3(nb / OB), dim3(256), 0, c->stream, wcnt, W, nb, tot);
-            hipLaunchKernelGGL(kc_col_scan, dim3(nb / OB), dim3(256), 0, c->stream, wcnt, W, nb, tot,
-                               reinterpret_cast<uint64_t*>(off));
-        });
-        c->check_launch("kc_col_scan");
-    } else {
-        c->launch("kc_layout", [&] {
-            hipLaunchKernelGGL(kc_transpose, dim3(blocks_for(nb, 64), blocks_for(std::max<uint32_t>(W, 1), 64)), dim3(256),
-                               0, c->stream, wcnt, W, nb, reinterpret_cast<uint64_t*>(off));
-        });
-        c->check_launch("kc_transpose");
-        exclusive_scan_u64(c, reinterpret_cast<uint64_t*>(off), (uint64_t)W * nb + 1, s.scratch);
-    }
+    c->launch("kc_layout", [&] {
+        hipLaunchKernelGGL(kc_transpose, dim3(blocks_for(nb, 64), blocks_for(std::max<uint32_t>(W, 1), 64)), dim3(256),
+                           0, c->stream, wcnt, W, nb, reinterpret_cast<uint64_t*>(off));
+    });
+    c->check_launch("kc_transpose");
+    exclusive_scan_u64(c, reinterpret_cast<uint64_t*>(off), (uint64_t)W * nb + 1, s.scratch);
     c->launch("kc_layout", [&] {
         hipLaunchKernelGGL(kc_fs, dim3(blocks_for((uint64_t)nb * (F + 1), 256)), dim3(256), 0, c->stream,
                            reinterpret_cast<const uint64_t*>(off), d_bf, W, nb, F, fs);
