@@ -424,7 +424,7 @@ constexpr int CNW_WAVES = HGA_CNW_WAVES;
 #define HGA_CN_HOME 1   // cn_wave: home-slot hits first, the rest through a per-wave queue (0: per-lane inserts)
 #endif
 #ifndef HGA_CNW_GRAB
-#define HGA_CNW_GRAB 2
+#define HGA_CNW_GRAB 4
 #endif
 #ifndef HGA_CNW_MINW
 #define HGA_CNW_MINW 4
