@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <vector>
 
@@ -237,26 +238,56 @@ struct DevEngine {
     void* send_buf(uint64_t bytes) { return c->count.xsend.ensure(bytes + 64); }
     void* recv_buf(uint64_t bytes) { return c->count.xrecv.ensure(bytes + 64); }
     int xb_pack(uint32_t P, uint64_t* per) { return count_xb_pack(c, P, per); }
-    // Fused head over an on-device communicator (the count kernels wrote the pieces): the per-owner
-    // totals, R, the extras and this rank's count error bits are all-gathered straight from device
-    // memory and the count's counters read back in the same host round trip (instead of one each for
-    // the settle, xb_pack and the all-gather).  Errors are decided on the gathered bits, so every rank
-    // raises the lowest failing rank's and none enters the piece all-to-all alone.
+    // Head of the packed exchange over an on-device communicator: the per-owner totals, R, the extras
+    // and this rank's count error bits are all-gathered from device memory as W + 1 words on EVERY
+    // rank, whatever its local state (a rank deciding alone between this gather and a
+    // W-word one would mismatch the collective).  A rank whose count kernels wrote the pieces (xb_on)
+    // enqueues its totals on the device and has its unsettled count's counters read back in the same
+    // host round trip; any other rank (a bucket left to the generic kernel, cached dump rows, a count
+    // already settled by a local query) settles first — without throwing: its error bits join the
+    // gather — and bins its rows (count_xb_pack).  Errors are decided on the gathered bits, so every
+    // rank raises the lowest failing rank's and none enters the piece all-to-all alone.
     bool xb_pack_gather(uint32_t P, std::vector<uint64_t>& per, std::vector<uint64_t>& all, int& R) {
         Comm& m = *c->comm;
         auto& s = c->count;
-        if (!m.on_device() || !(s.xb_on && s.xb_P == P)) return false;
+        if (!m.on_device()) return false;
         const size_t W = per.size(), Wg = W + 1;   // + the error word
         const uint64_t B = 8 * (uint64_t)Wg;
         char* ds = static_cast<char*>(m.stage.ensure(B * (P + 1) + 16));
         char* hs = static_cast<char*>(m.hstage.ensure(B * (P + 1) + 64 + 16));
         auto* hp = reinterpret_cast<unsigned long long*>(hs + B * (P + 1));   // the count's counters
-        const bool pend = s.pending;
-        if (!count_xb_pack_begin(c, P, reinterpret_cast<uint64_t*>(ds))) return false;
-        R = s.xb_R;
+        const bool emitted = s.xb_on && s.xb_P == P;
+        const bool pend = emitted && s.pending;
+        uint64_t ebits = 0;   // a non-emitting rank's settle bits
+        if (emitted) {
+            HGA_REQUIRE(count_xb_pack_begin(c, P, reinterpret_cast<uint64_t*>(ds)), HGA_ERR_STATE,
+                        "the count did not emit exchange pieces");
+            R = s.xb_R;
+        } else {
+            if (s.pending) {
+                HGA_HIP(hipMemcpyAsync(hp, s.cursor.p, 64, hipMemcpyDeviceToHost, c->stream));
+                c->sync();
+                ebits = hp[2] & 7ull;
+                if (ebits) {   // consumed as failed, as count_settle would (it would throw here)
+                    s.pending = false;
+                    s.last_err = ebits;
+                    s.ran = false;
+                } else {
+                    count_settle(c, hp);
+                }
+            }
+            if (ebits) {   // nothing to send: the gathered bits stop every rank before the all-to-all
+                R = proto::xb_base_bits(s.k);
+                std::fill(per.begin(), per.begin() + P, 0ull);
+            } else {
+                R = count_xb_pack(c, P, per.data());
+            }
+            if (extra0_instances && W > (size_t)P + 1) per[P + 1] = s.instances;
+        }
         per[P] = (uint64_t)R;
-        std::memcpy(hs + 8 * P, per.data() + P, 8 * (W - P));
-        HGA_HIP(hipMemcpyAsync(ds + 8 * P, hs + 8 * P, 8 * (W - P), hipMemcpyHostToDevice, c->stream));
+        const size_t h0 = emitted ? P : 0;   // an emitting rank's totals are on the device already
+        std::memcpy(hs + 8 * h0, per.data() + h0, 8 * (W - h0));
+        HGA_HIP(hipMemcpyAsync(ds + 8 * h0, hs + 8 * h0, 8 * (W - h0), hipMemcpyHostToDevice, c->stream));
         if (pend) {   // settle bits (gstat[2]) and, if asked, instances (gstat[4]) from the device
             HGA_HIP(hipMemcpyAsync(ds + 8 * W, static_cast<char*>(s.cursor.p) + 16, 8, hipMemcpyDeviceToDevice,
                                    c->stream));
@@ -265,7 +296,8 @@ struct DevEngine {
                                        hipMemcpyDeviceToDevice, c->stream));
             HGA_HIP(hipMemcpyAsync(hp, s.cursor.p, 64, hipMemcpyDeviceToHost, c->stream));
         } else {
-            HGA_HIP(hipMemsetAsync(ds + 8 * W, 0, 8, c->stream));
+            reinterpret_cast<uint64_t*>(hs)[W] = ebits;
+            HGA_HIP(hipMemcpyAsync(ds + 8 * W, hs + 8 * W, 8, hipMemcpyHostToDevice, c->stream));
         }
         std::vector<uint64_t> sz(P, B);
         std::vector<const void*> sp(P, ds);
@@ -290,8 +322,10 @@ struct DevEngine {
         all.assign((size_t)P * W, 0);
         for (uint32_t p = 0; p < P; ++p)
             for (size_t i = 0; i < W; ++i) all[(size_t)p * W + i] = g[(size_t)p * Wg + i];
-        for (uint32_t o = 0; o < P; ++o) per[o] = all[(size_t)m.rank * W + o];
-        count_xb_pack_finish(c, P, per.data());
+        if (emitted) {
+            for (uint32_t o = 0; o < P; ++o) per[o] = all[(size_t)m.rank * W + o];
+            count_xb_pack_finish(c, P, per.data());
+        }
         return true;
     }
     const void* xb_pieces() const { return c->count.xsend.p; }
@@ -314,10 +348,11 @@ struct DevEngine {
 void count_exchange(hga_ctx* c, uint32_t min_per_file) {
     auto& s = c->count;
     Comm& m = need_comm(c);
-    // an unsettled count whose kernels wrote the pieces is settled by the fused exchange head
-    // (DevEngine::xb_pack_gather), in the round trip of its all-gather
-    const bool fused = m.on_device() && s.pending && s.xb_on && s.xb_P == (uint32_t)m.nranks;
-    if (!fused) count_settle(c);
+    // over an on-device communicator the packed exchange's head (DevEngine::xb_pack_gather) settles an
+    // unsettled count itself, on every rank the same way, so that a failed count reaches the others
+    // through the gathered error words instead of leaving this rank alone
+    const bool dev_head = m.on_device() && count_pack_bits(c) > 0;
+    if (!dev_head) count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run(ctx, 1) first");
     HGA_REQUIRE(s.min_per_file == 1, HGA_ERR_STATE, "the local count must keep singletons: hga_count_run(ctx, 1)");
     HGA_REQUIRE(min_per_file >= 1, HGA_ERR_INVALID, "min_per_file must be >= 1");
@@ -326,7 +361,7 @@ void count_exchange(hga_ctx* c, uint32_t min_per_file) {
     std::vector<uint64_t> mine{s.instances, 0}, g;
     for (auto l : s.seq_len) mine[1] += l;
     DevEngine e{c};
-    e.extra0_instances = fused;
+    e.extra0_instances = dev_head;
     proto::count_exchange(e, x, min_per_file, mine, &g);
     s.g_instances = g[0];
     s.g_bytes = g[1];
@@ -405,7 +440,8 @@ __global__ void kx_hist_slot(const unsigned long long* __restrict__ ctrl, const 
                  {proto::QE_ROWCAP, HGA_ERR_OOM, "row capacity exceeded"},
                  {proto::QE_SPEC_THR, HGA_ERR_INVALID, "a row's specificity is above the last threshold"},
                  {proto::QE_OVER, HGA_ERR_OOM, "histogram overflow list full"},
-                 {proto::QE_COMPACT, HGA_ERR_OOM, "histogram compaction buffer full"}};
+                 {proto::QE_COMPACT, HGA_ERR_OOM, "histogram compaction buffer full"},
+                 {proto::QE_LOCAL, HGA_ERR_STATE, "count query failed before its gather"}};
     for (const auto& o : order)
         if (e.bits & o.bit) throw Error(o.code, "rank " + std::to_string(e.rank) + ": " + o.msg);
     throw Error(HGA_ERR_INVALID, "rank " + std::to_string(e.rank) + ": count query failed");
@@ -513,7 +549,13 @@ void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::
     CtxXport x(c);
     proto::QueryError qe;
     if (!m.on_device()) {
-        const uint64_t err = run_reporting(c, [&] { count_spec_hist(c, thr, n_thr, local); });
+        uint64_t err;
+        try {   // any local failure joins the gather as an error word (the others do not wait alone)
+            err = run_reporting(c, [&] { count_spec_hist(c, thr, n_thr, local); });
+        } catch (const Error&) {
+            err = c->count.last_err ? c->count.last_err : proto::QE_LOCAL;
+            local.clear();
+        }
         out = proto::spec_hist_global(x, local, err, &qe);
         if (qe.rank >= 0) throw_query_error(qe);
         return;
@@ -539,8 +581,29 @@ void count_spec_hist_global(hga_ctx* c, const double* thr, uint32_t n_thr, std::
         HGA_HIP(hipMemcpyAsync(hs, ds + sb, sb * P, hipMemcpyDeviceToHost, c->stream));
         gathered = true;
     };
-    const uint64_t err = run_reporting(c, [&] { count_spec_hist(c, thr, n_thr, local, &hook); });
-    if (!gathered) HGA_REQUIRE(false, HGA_ERR_STATE, "count_spec_hist failed before its gather");
+    // a local failure before the hook (no run, an allocation, a state check) still takes part in the
+    // slot gather, with its error word only, so the other ranks do not wait in it alone
+    uint64_t err = 0;
+    std::exception_ptr fail;
+    try {
+        err = run_reporting(c, [&] { count_spec_hist(c, thr, n_thr, local, &hook); });
+    } catch (...) {
+        fail = std::current_exception();
+    }
+    if (!gathered) {
+        unsigned long long hdr[HS_HDR] = {};
+        hdr[0] = c->count.last_err ? c->count.last_err : proto::QE_LOCAL;
+        HGA_HIP(hipMemcpyAsync(ds, hdr, sizeof(hdr), hipMemcpyHostToDevice, c->stream));
+        std::vector<uint64_t> sz(P, sb);
+        std::vector<const void*> sp(P, ds);
+        std::vector<void*> rp(P);
+        for (int p = 0; p < P; ++p) rp[p] = ds + sb * (p + 1);
+        m.alltoallv(c, sp.data(), sz.data(), rp.data(), sz.data());
+        HGA_HIP(hipMemcpyAsync(hs, ds + sb, sb * P, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+    } else if (fail) {
+        std::rethrow_exception(fail);   // after its gather: a device failure, this rank's own
+    }
     (void)err;   // this rank's bits are in its own slot
     const proto::SlotMerge r = proto::merge_hist_slots(reinterpret_cast<const uint64_t*>(hs), P, out, &qe);
     if (r == proto::SlotMerge::error) throw_query_error(qe);

@@ -1164,25 +1164,39 @@ constexpr uint32_t T_S = HGA_T_S;       // slots (32 KB keys + 32 KB counts)
 #ifndef HGA_GS_S
 #define HGA_GS_S 4
 #endif
-constexpr uint32_t GS_S = HGA_GS_S;     // keys per probe group (4: one ds_read_b128, 2: one ds_read_b64)
-constexpr uint32_t G_S = T_S / GS_S;
-static_assert(GS_S == 2 || GS_S == 4, "probe groups of 2 or 4 keys");
-using KGrp = std::conditional_t<GS_S == 4, uint4, uint2>;
+#ifndef HGA_GS_LAZY
+#define HGA_GS_LAZY 4
+#endif
+// keys per probe group, per kernel mode: 4 (one ds_read_b128) or 2 (one ds_read_b64).  A random
+// ds_read_b64 is serviced in 2 lane groups of 32 over 64 banks, a ds_read_b128 in 4 groups of 16
+// (MI355X_MICROARCH.md §LDS), but 2-key groups displace more keys from their home group (load ~0.48:
+// ~10 % vs ~3 %), and in the lazy kernel every instance of a displaced key goes through the miss
+// queue: measured at C2, lazy kc_count_s 0.381 ms with 4-key groups, 0.406 with 2 (round 6).
+template <int GS>
+using KGrpT = std::conditional_t<GS == 4, uint4, uint2>;
+static_assert(HGA_GS_S == 2 || HGA_GS_S == 4, "probe groups of 2 or 4 keys");
+static_assert(HGA_GS_LAZY == 2 || HGA_GS_LAZY == 4, "probe groups of 2 or 4 keys");
 
-__device__ __forceinline__ KGrp read_keys_s(const uint32_t* tkey, uint32_t g) {
-    return reinterpret_cast<const KGrp*>(tkey)[g];
-}
-__device__ __forceinline__ void match_s(const KGrp kg, uint32_t r, int& w, int& e0) {
-    uint32_t k[GS_S];
-    if constexpr (GS_S == 4) {
-        k[0] = kg.x; k[1] = kg.y; k[2] = reinterpret_cast<const uint4&>(kg).z; k[3] = reinterpret_cast<const uint4&>(kg).w;
+template <int GS>
+__device__ __forceinline__ void group_keys(const KGrpT<GS> kg, uint32_t (&k)[GS]) {
+    if constexpr (GS == 4) {
+        k[0] = kg.x; k[1] = kg.y; k[2] = kg.z; k[3] = kg.w;
     } else {
         k[0] = kg.x; k[1] = kg.y;
     }
+}
+template <int GS>
+__device__ __forceinline__ KGrpT<GS> read_keys_s(const uint32_t* tkey, uint32_t g) {
+    return reinterpret_cast<const KGrpT<GS>*>(tkey)[g];
+}
+template <int GS>
+__device__ __forceinline__ void match_s(const KGrpT<GS> kg, uint32_t r, int& w, int& e0) {
+    uint32_t k[GS];
+    group_keys<GS>(kg, k);
     w = -1;
     e0 = -1;
 #pragma unroll
-    for (int t = GS_S - 1; t >= 0; --t) {
+    for (int t = GS - 1; t >= 0; --t) {
         w = k[t] == r ? t : w;
         e0 = k[t] == 0xFFFFFFFFu ? t : e0;
     }
@@ -1190,31 +1204,30 @@ __device__ __forceinline__ void match_s(const KGrp kg, uint32_t r, int& w, int& 
 
 // The byte offset of r in a loaded group (4 x its slot), -1 if absent (keys are unique in the table:
 // at most one match).
-__device__ __forceinline__ int match_hit4_s(const KGrp kg, uint32_t r) {
-    uint32_t k[GS_S];
-    if constexpr (GS_S == 4) {
-        k[0] = kg.x; k[1] = kg.y; k[2] = reinterpret_cast<const uint4&>(kg).z; k[3] = reinterpret_cast<const uint4&>(kg).w;
-    } else {
-        k[0] = kg.x; k[1] = kg.y;
-    }
+template <int GS>
+__device__ __forceinline__ int match_hit4_s(const KGrpT<GS> kg, uint32_t r) {
+    uint32_t k[GS];
+    group_keys<GS>(kg, k);
     int w = k[0] == r ? 0 : -1;
 #pragma unroll
-    for (int t = 1; t < GS_S; ++t) w = k[t] == r ? 4 * t : w;
+    for (int t = 1; t < GS; ++t) w = k[t] == r ? 4 * t : w;
     return w;
 }
 
 // Settle key r (+inc) from its home group; false if MAXPROBE_P groups were full.
+template <int GS>
 __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t r, uint32_t inc) {
-    uint32_t g = r & (G_S - 1);
-    for (uint32_t steps = 0; steps < MAXPROBE_P;) {
+    constexpr uint32_t G = T_S / GS;
+    uint32_t g = r & (G - 1);
+    for (uint32_t steps = 0; steps < MAXPROBE_P * (4 / GS);) {
         int w, e0;
-        match_s(read_keys_s(tkey, g), r, w, e0);
+        match_s<GS>(read_keys_s<GS>(tkey, g), r, w, e0);
         if (w >= 0) {
-            atomicAdd(&tcnt[g * GS_S + w], inc);
+            atomicAdd(&tcnt[g * GS + w], inc);
             return true;
         }
         if (e0 >= 0) {
-            const uint32_t sl = g * GS_S + (uint32_t)e0;
+            const uint32_t sl = g * GS + (uint32_t)e0;
             const uint32_t old = atomicCAS(&tkey[sl], 0xFFFFFFFFu, r);
             if (old == 0xFFFFFFFFu || old == r) {
                 atomicAdd(&tcnt[sl], inc);
@@ -1222,7 +1235,7 @@ __device__ __forceinline__ bool probe_s(uint32_t* tkey, uint32_t* tcnt, uint32_t
             }
             continue;   // lost the slot to another key: re-read the same group
         }
-        g = (g + 1) & (G_S - 1);
+        g = (g + 1) & (G - 1);
         ++steps;
     }
     return false;
@@ -1248,6 +1261,9 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
     __shared__ uint32_t ws[NT_P / 64 + 1];
     __shared__ unsigned long long s_base;
     __shared__ uint32_t s_xw, s_xrows;   // exchange emission: pieces and rows so far
+    constexpr int GS = LAZY ? HGA_GS_LAZY : HGA_GS_S;
+    constexpr uint32_t G_S = T_S / GS;
+    using KGrp = KGrpT<GS>;
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     uint32_t* myq = qbuf[tid >> 6];
@@ -1314,7 +1330,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                     const uint32_t take = qn < 64 ? qn : 64;
                     const uint32_t q0 = qn - take;
                     bool ok = true;
-                    if (lane < take) ok = probe_s(tkey, tcnt, myq[q0 + lane], inc);
+                    if (lane < take) ok = probe_s<GS>(tkey, tcnt, myq[q0 + lane], inc);
                     if (!ok) s_ovf = 1u;
                     qn = q0;
                     wave_lds_sync();
@@ -1338,7 +1354,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                 uint32_t ga[PF_P];   // byte offset of each home group (keys; counts at the same offset)
 #pragma unroll
                 for (int q = 0; q < PF_P; ++q) {
-                    ga[q] = (rv[q] & (G_S - 1)) * (GS_S * 4u);
+                    ga[q] = (rv[q] & (G_S - 1)) * (GS * 4u);
                     kg[q] = *reinterpret_cast<const KGrp*>(reinterpret_cast<const char*>(tkey) + ga[q]);
                 }
                 uint32_t claim = 0, miss = 0, slot[PF_P];
@@ -1347,7 +1363,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                     // (tkey and tcnt share the layout); a lane without a hit adds to its dummy word
 #pragma unroll
                     for (int q = 0; q < PF_P; ++q) {
-                        const int w4 = match_hit4_s(kg[q], rv[q]);
+                        const int w4 = match_hit4_s<GS>(kg[q], rv[q]);
                         const bool live = rv[q] != 0xFFFFFFFFu;
                         const bool hit = live && w4 >= 0;
                         atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tcnt) +
@@ -1359,9 +1375,9 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
 #pragma unroll
                 for (int q = 0; q < PF_P && !LAZY; ++q) {
                     int w, e0;
-                    match_s(kg[q], rv[q], w, e0);
+                    match_s<GS>(kg[q], rv[q], w, e0);
                     const bool live = rv[q] != 0xFFFFFFFFu;
-                    slot[q] = (rv[q] & (G_S - 1)) * GS_S + (uint32_t)(w >= 0 ? w : e0);
+                    slot[q] = (rv[q] & (G_S - 1)) * GS + (uint32_t)(w >= 0 ? w : e0);
                     {   // every lane adds: a hit to its slot, anything else to its own dummy word
                         const bool hit = live && w >= 0;
                         atomicAdd(&tcnt[hit ? slot[q] : T_S + lane], inc);
@@ -1391,7 +1407,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                                 uint32_t pick = rv[0];
 #pragma unroll
                                 for (int t = 1; t < PF_P; ++t) pick = q == t ? rv[t] : pick;
-                                ok = probe_s(tkey, tcnt, pick, inc) && ok;
+                                ok = probe_s<GS>(tkey, tcnt, pick, inc) && ok;
                             }
                         }
                         if (!ok) s_ovf = 1u;
@@ -1405,7 +1421,7 @@ __global__ void __launch_bounds__(NT_P, HGA_CS_WAVES) kc_count_s(const uint32_t*
                         drain(64);
                     }
                 }
-                if ((i0 - a) % (4 * STEP) == 0 && __atomic_load_n(&s_ovf, __ATOMIC_RELAXED)) break;
+                if ((bi & 3u) == 0 && __atomic_load_n(&s_ovf, __ATOMIC_RELAXED)) break;
             }
             drain(1);
         }

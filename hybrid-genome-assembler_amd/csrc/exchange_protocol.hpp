@@ -187,7 +187,10 @@ uint64_t count_exchange(E& e, Xport& x, uint32_t min_per_file, const std::vector
 // gather) that a failed rank skips.  Bits: the settle bits of an unconsumed count run (1 a bucket
 // could not be split, 2 row capacity, 4 level-1 pool) and the histogram's own (8 a specificity above
 // the last threshold, 16 overflow list full, 32 compaction buffer full).
-enum : uint64_t { QE_UNSPLIT = 1, QE_ROWCAP = 2, QE_POOL = 4, QE_SPEC_THR = 8, QE_OVER = 16, QE_COMPACT = 32 };
+// 64: any other local failure before the rank's gather (state, allocation): it still takes part in the
+// gather with this bit set.
+enum : uint64_t { QE_UNSPLIT = 1, QE_ROWCAP = 2, QE_POOL = 4, QE_SPEC_THR = 8, QE_OVER = 16, QE_COMPACT = 32,
+                  QE_LOCAL = 64 };
 struct QueryError {
     int rank = -1;   // the lowest failing rank, -1: none
     uint64_t bits = 0;
