@@ -356,7 +356,11 @@ void write_kmer_dump(const std::string& path, int k, const uint64_t* keys, const
 
 void write_kmer_dump_rows(const std::string& path, int k, const uint64_t* keys, const uint32_t* counts, uint32_t F,
                           uint32_t file, uint64_t n) {
-    std::FILE* f = std::fopen(path.c_str(), "wb");
+    // written to `<path>.tmp` and renamed into place once complete: the cache's existence is all a
+    // later run checks (JellyfishOccurrenceReader.cpp:19-24), so an interrupted run (a Ctrl-C at the
+    // bounds prompt while the writer thread is busy) must not leave a truncated file under its name
+    const std::string tmp = path + ".tmp";
+    std::FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) throw std::runtime_error("cannot write " + path);
     // "KMER COUNT\n" lines formatted by host_threads() threads, chunk by chunk in row order, each
     // chunk's text written as soon as it and its predecessors are done
@@ -398,7 +402,14 @@ void write_kmer_dump_rows(const std::string& path, int k, const uint64_t* keys, 
         std::vector<char>().swap(text[c]);
     }
     for (auto& x : th) x.join();
-    if (std::fclose(f) != 0 || !ok) throw std::runtime_error("cannot write " + path);
+    if (std::fclose(f) != 0 || !ok) {
+        std::remove(tmp.c_str());
+        throw std::runtime_error("cannot write " + path);
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) {
+        std::remove(tmp.c_str());
+        throw std::runtime_error("cannot write " + path);
+    }
 }
 
 }  // namespace hgah

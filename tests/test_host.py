@@ -135,6 +135,8 @@ def test_dump_writer_matches_restatement(tmp_path, n, threads):
     got = p.read_text()
     lines = got.splitlines(keepends=True)
     assert len(lines) == n
+    # written to d.txt.tmp and renamed once complete (an interrupted run leaves no truncated cache)
+    assert sorted(x.name for x in tmp_path.iterdir()) == ["d.txt"]
 
     def kstr(c):
         return "".join("ACGT"[(int(c) >> (2 * (k - 1 - i))) & 3] for i in range(k))

@@ -49,11 +49,17 @@ def test_rccl_one_rank_count_exchange(monkeypatch, self_p2p, k, emit):
         ctx.comm_destroy()
 
 
-def test_rccl_fused_exchange_head_reports_count_errors(monkeypatch):
-    """A count that failed on the device (row capacity, HGA_ROW_CAP) and was never settled: the fused
+@pytest.mark.parametrize("generic", [False, True])
+def test_rccl_fused_exchange_head_reports_count_errors(monkeypatch, generic):
+    """A count that failed on the device (row capacity, HGA_ROW_CAP) and was never settled: the
     exchange head (comm.hip DevEngine::xb_pack_gather) decides on the gathered error bits and raises
-    the failing rank's error by name; the context stays usable for a new count."""
+    the failing rank's error by name; the context stays usable for a new count.  generic: the count
+    did not emit exchange pieces (HGA_XB_GENERIC, as a rank holding cached dump rows): that rank
+    settles inside the head without throwing and still gathers the same W + 1 words as an emitting
+    rank (the gather shape must not depend on a rank's local state)."""
     monkeypatch.setenv("HGA_FB_MIN", "10")
+    if generic:
+        monkeypatch.setenv("HGA_XB_GENERIC", "1")
     streams = make_streams()
     with hga.Ctx(0) as ctx:
         ctx.comm_init(hga.comm_unique_id(), 0, 1)
@@ -68,6 +74,7 @@ def test_rccl_fused_exchange_head_reports_count_errors(monkeypatch):
         ref = oracle.count_pipeline(streams, 13, 3, 40)
         ctx.count_run(1)
         ctx.count_exchange(2)
+        assert ctx.count_stats().instances == sum(oracle.count_instances(x, 13) for x in streams)
         keys, flags, nd = ctx.select(3, 40)
         assert np.array_equal(keys, ref["selected"]) and nd == ref["n_discr"]
         ctx.comm_destroy()
