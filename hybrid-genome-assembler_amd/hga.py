@@ -598,7 +598,7 @@ def cluster_config(sc_min=30, sc_max=-1, sc_fraction=0.15, sc_score=0, enrich=20
 CLUSTER_SYMBOLS = {
     "hgc_last_error": (C.c_char_p, []),
     "hgc_free": (None, [_vp]),
-    "hgc_cluster": (C.c_int, [C.c_char_p, _u64p, _i32p, C.c_uint64, C.c_uint64, C.c_uint32, _u64p, _u32p, _u64p,
+    "hgc_cluster": (C.c_int, [C.c_char_p, _u64p, _i32p, _u32p, _u32p, C.c_uint64, C.c_uint64, C.c_uint32, _u64p, _u32p, _u64p,
                               _u32p, _u32p, _u64p, _u32p, C.c_uint32, C.POINTER(ClusterConfig), C.c_int,
                               C.POINTER(_u32p), _u64p, C.POINTER(_u32p), C.POINTER(_vp)]),
     "hgc_union_find": (C.c_int, [_u32p, _u32p, _u64p, C.c_uint64, _u32p, C.c_uint64, C.c_int, C.c_int,
@@ -672,9 +672,11 @@ def sym_eigen(a):
     return val, vec
 
 
-def cluster_host(bases: bytes, offsets, category, idx, avg_read_length, cfg=None, debug=False, first_read_id=1):
+def cluster_host(bases: bytes, offsets, category, idx, avg_read_length, cfg=None, debug=False, first_read_id=1,
+                 start=None, end=None):
     """run_clustering after construct_indices on the host (no device state): (component ids,
-    per-read component id (0 = none), log text)."""
+    per-read component id (0 = none), log text).  start / end: the reads' simulator coordinates
+    (print_components' intervals under debug), None = 0."""
     L = cluster_lib()
     cfg = cfg or cluster_config()
     off = np.ascontiguousarray(offsets, np.uint64)
@@ -685,7 +687,11 @@ def cluster_host(bases: bytes, offsets, category, idx, avg_read_length, cfg=None
     ip, op = _u32p(), _u32p()
     lp = C.c_void_p()
     ni = C.c_uint64()
-    _cck(L.hgc_cluster(bases, _p(off, C.c_uint64), _p(cat, C.c_int32), n, avg_read_length, first_read_id,
+    st = None if start is None else np.ascontiguousarray(start, np.uint32)
+    en = None if end is None else np.ascontiguousarray(end, np.uint32)
+    _cck(L.hgc_cluster(bases, _p(off, C.c_uint64), _p(cat, C.c_int32),
+                       None if st is None else _p(st, C.c_uint32), None if en is None else _p(en, C.c_uint32),
+                       n, avg_read_length, first_read_id,
                        _p(a["hit_ptr"], C.c_uint64), _p(a["sorted_kid"], C.c_uint32), _p(a["first_ptr"], C.c_uint64),
                        _p(a["first_kid"], C.c_uint32), _p(a["first_pos"], C.c_uint32), _p(a["kci_ptr"], C.c_uint64),
                        _p(a["kci_read"], C.c_uint32), len(a["kci_ptr"]) - 1, C.byref(cfg), 1 if debug else 0,

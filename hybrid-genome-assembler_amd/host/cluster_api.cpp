@@ -67,9 +67,11 @@ void hgc_free(void* p) { std::free(p); }
 
 // run_clustering after construct_indices (host-only: no device state) on the lookup's CSR
 // outputs; reads in reader order with ReadID = first_read_id + i.  Outputs: the returned
-// component ids (ascending), per read the id of the returned component containing it (0 =
-// none), the timing/log text.
-int hgc_cluster(const char* bases, const uint64_t* offsets, const int32_t* category, uint64_t n_reads,
+// component ids (ascending; under debug in print_components' order), per read the id of the returned
+// component containing it (0 = none), the timing/log text (with print_components' blocks under debug).
+// start / end: the reads' simulator-header coordinates (GenomeReadData start / end), null = 0.
+int hgc_cluster(const char* bases, const uint64_t* offsets, const int32_t* category, const uint32_t* start,
+                const uint32_t* end, uint64_t n_reads,
                 uint64_t avg_read_length, uint32_t first_read_id, const uint64_t* hit_ptr, const uint32_t* sorted_kid,
                 const uint64_t* first_ptr, const uint32_t* first_kid, const uint32_t* first_pos, const uint64_t* kci_ptr,
                 const uint32_t* kci_read, uint32_t n_sdk, const hgc_config* cfg, int debug, uint32_t** ids_out,
@@ -79,6 +81,10 @@ int hgc_cluster(const char* bases, const uint64_t* offsets, const int32_t* categ
         rs.bases.append(bases, n_reads ? offsets[n_reads] : 0);
         rs.offsets.assign(offsets, offsets + n_reads + 1);
         rs.category.assign(category, category + n_reads);
+        if (start && end) {
+            rs.start.assign(start, start + n_reads);
+            rs.end.assign(end, end + n_reads);
+        }
         rs.meta.avg_read_length = avg_read_length;
         hgah::ClusteringConfig c;
         c.scaffold_component_min_size = cfg->sc_min_size;

@@ -393,6 +393,15 @@ std::vector<ComponentList> spectral_clustering(const std::vector<Connection>& co
     std::vector<double> m((size_t)n * n, 0.0);
     const Score max_score = *std::max_element(scores.begin(), scores.end());
     const Score min_score = *std::min_element(scores.begin(), scores.end());
+    // Every score equal (e.g. one strong connection): scale_strength is 0/0 = NaN for every edge there
+    // (:672-674) and the whole affinity matrix NaN; Eigen2's eigenvectors of it are unspecified (parity
+    // unpinned).  Here that case is explicit: no grouping, every component its own cluster (what the NaN
+    // matrix gave through this eigensolver and rotation), so merge_components changes nothing.
+    if (max_score == min_score) {
+        std::vector<ComponentList> alone;
+        for (ComponentID v : id_to) alone.push_back({v});
+        return alone;
+    }
     auto scale = [&](Score s) {
         return ((double)(max_exponent - 0.3) * (double)(s - min_score)) / (double)(max_score - min_score) + 0.3;
     };
@@ -791,6 +800,65 @@ std::vector<Connection> ClusteringEngine::core_component_connections(
     return filter_connections(edges, [](const Connection& c) { return c.score > 0; });
 }
 
+// ReadComponent::to_string (ReadClusteringEngine.h:98-112) with consistency (:52-64) and
+// category_intervals (:66-96): read counts per category, categories 0 and 1 always listed, joined by
+// "/"; per category present, the union of the reads' [start, end] simulator coordinates as
+// "(a,b)" joined by ";", categories joined by " / ".
+std::string ClusteringEngine::component_string(ComponentID id) const {
+    const Component& c = index_.at(id);
+    std::map<int32_t, int> counts{{0, 0}, {1, 0}};
+    std::map<int32_t, std::vector<std::pair<uint32_t, bool>>> endpoints;   // Endpoint = (position, is start)
+    for (uint32_t r : c.reads) {
+        const uint64_t i = r - first_id_;
+        const int32_t cat = reads_.category[i];
+        ++counts[cat];
+        auto& e = endpoints[cat];
+        e.emplace_back(reads_.start.empty() ? 0u : reads_.start[i], true);
+        e.emplace_back(reads_.end.empty() ? 0u : reads_.end[i], false);
+    }
+    std::string s = "#" + std::to_string(id) + " : ";
+    bool first = true;
+    for (auto& kv : counts) {
+        if (!first) s += "/";
+        s += std::to_string(kv.second);
+        first = false;
+    }
+    s += " [";
+    first = true;
+    for (auto& kv : endpoints) {
+        auto& e = kv.second;
+        std::sort(e.begin(), e.end());   // (position, false) before (position, true), as std::pair orders them
+        if (!first) s += " / ";
+        first = false;
+        uint32_t open_at = 0;   // (uninitialised there until the first opening endpoint)
+        int opened = 0;
+        bool any = false;
+        for (auto& ep : e) {
+            if (ep.second) {
+                if (++opened == 1) open_at = ep.first;
+            } else if (--opened == 0) {
+                if (any) s += ";";
+                s += "(" + std::to_string(open_at) + "," + std::to_string(ep.first) + ")";
+                any = true;
+            }
+        }
+    }
+    s += "]";
+    return s;
+}
+
+void ClusteringEngine::print_components(std::vector<ComponentID>& ids, std::ostream& out) const {
+    if (!debug_) return;
+    std::stable_sort(ids.begin(), ids.end(), [this](ComponentID x, ComponentID y) {
+        const size_t a = index_.at(x).reads.size(), b = index_.at(y).reads.size();
+        return a != b ? a > b : x < y;
+    });
+    out << "### Printing " << ids.size() << " components ###\n";
+    for (ComponentID id : ids) out << component_string(id) << "\n";
+    out << "### ###\n\n";
+    out.flush();
+}
+
 // run_clustering after construct_indices (:737-801).
 std::vector<ComponentID> ClusteringEngine::run(std::ostream& out) {
     if (cfg_.force_spectral) {   // :739-746
@@ -798,7 +866,9 @@ std::vector<ComponentID> ClusteringEngine::run(std::ostream& out) {
         auto spectral = timed(out, "Forced spectral clustering",
                               [&] { return spectral_clustering(conns, cfg_.spectral_dims); });
         merge_components(spectral);
-        return component_ids((uint64_t)(int64_t)cfg_.scaffold_component_min_size);
+        auto ids = component_ids((uint64_t)(int64_t)cfg_.scaffold_component_min_size);
+        print_components(ids, out);   // :745
+        return ids;
     }
     std::vector<Connection> scaffold_forming, conns;
     if (cfg_.scaffold_forming_score > 0) {   // :749-756
@@ -823,6 +893,7 @@ std::vector<ComponentID> ClusteringEngine::run(std::ostream& out) {
     });
     auto scaffold_ids = timed(out, "Merging of initial components",
                               [&] { return merge_components(extract_components(comps_and_trees)); });
+    print_components(scaffold_ids, out);   // :766
     if (scaffold_ids.size() > 2) {   // :768-777
         auto core = timed(out, "Calculation of tail connections", [&] { return core_component_connections(comps_and_trees); });
         auto strong = filter_connections(core, [](const Connection& c) { return c.score > 5; });
@@ -834,6 +905,7 @@ std::vector<ComponentID> ClusteringEngine::run(std::ostream& out) {
     }
     const uint64_t min_size = (uint64_t)(int64_t)cfg_.scaffold_component_min_size;   // int -> u64 as there
     auto core_ids = component_ids(min_size);
+    print_components(core_ids, out);   // :781 (sorts core_ids in place, as there)
     {   // :785-794
         conns = timed(out, "Calculation of enrichment connections",
                       [&] { return get_connections(core_ids, cfg_.enrichment_connections_min_score); });
@@ -843,6 +915,7 @@ std::vector<ComponentID> ClusteringEngine::run(std::ostream& out) {
         remove_merged_components();
         core_ids = component_ids(min_size);
     }
+    print_components(core_ids, out);   // :797
     return core_ids;
 }
 

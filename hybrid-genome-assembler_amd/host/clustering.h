@@ -88,6 +88,13 @@ class ClusteringEngine {
     // run_clustering after construct_indices (:737-801); the timing lines go to `out`.
     std::vector<ComponentID> run(std::ostream& out);
 
+    // print_components (:189-198) under debug: ids sorted in place by size, largest first (ties by
+    // ascending id; std::sort leaves them unspecified there), then one ReadComponent::to_string line
+    // each (ReadClusteringEngine.h:52-112): "#<id> : <per-category read counts a/b/..> [<per-category
+    // simulator-coordinate intervals>]".
+    void print_components(std::vector<ComponentID>& ids, std::ostream& out) const;
+    std::string component_string(ComponentID id) const;
+
     // export_components (:804-826).
     void export_components(const std::vector<ComponentID>& ids, const std::string& dir, std::ostream& out) const;
 

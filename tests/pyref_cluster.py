@@ -156,6 +156,8 @@ def spectral_clustering(conns, dims):   # :653-697
         scores.append(s)
     n = len(id_to)
     mx, mn = max(scores), min(scores)
+    if mx == mn:   # scale_strength 0/0 = NaN for every edge (:672-674): every component alone (host/clustering.cpp)
+        return [[v] for v in id_to]
     m = np.zeros((n, n))
     for x, y, s, *_ in conns:
         w = math.exp((20 - 0.3) * (s - mn) / (mx - mn) + 0.3)
@@ -173,8 +175,13 @@ def spectral_clustering(conns, dims):   # :653-697
 
 # ---------------------------------------------------------------- engine
 class Engine:
-    def __init__(self, idx, lengths, categories, avg_len, debug, cfg, first_id=1):
+    def __init__(self, idx, lengths, categories, avg_len, debug, cfg, first_id=1, start=None, end=None):
         self.cfg, self.debug, self.avg_len, self.first_id = cfg, debug, avg_len, first_id
+        n = len(lengths)
+        self.cat = {first_id + i: int(categories[i]) for i in range(n)}
+        self.start = {first_id + i: int(start[i]) if start is not None else 0 for i in range(n)}
+        self.end = {first_id + i: int(end[i]) if end is not None else 0 for i in range(n)}
+        self.printed = []   # print_components' lines under debug
         hp, sk = idx["hit_ptr"], idx["sorted_kid"]
         self.lengths = {first_id + i: int(l) for i, l in enumerate(lengths)}
         self.comps = {}
@@ -334,6 +341,37 @@ class Engine:
                     edges.append((a, b, s, self.good(a, b)))
         return [e for e in sort_conns(edges) if e[2] > 0]
 
+    def to_string(self, cid):   # ReadComponent::to_string, ReadClusteringEngine.h:52-112
+        reads = self.comps[cid]["reads"]
+        counts = {0: 0, 1: 0}
+        ends = {}
+        for r in reads:
+            c = self.cat[r]
+            counts[c] = counts.get(c, 0) + 1
+            ends.setdefault(c, []).extend([(self.start[r], True), (self.end[r], False)])
+        parts = []
+        for c in sorted(ends):
+            cur, opened, iv = 0, 0, []
+            for pos, is_start in sorted(ends[c]):   # (pos, False) before (pos, True)
+                if is_start:
+                    opened += 1
+                    if opened == 1:
+                        cur = pos
+                else:
+                    opened -= 1
+                    if opened == 0:
+                        iv.append(f"({cur},{pos})")
+            parts.append(";".join(iv))
+        return f"#{cid} : {'/'.join(str(counts[c]) for c in sorted(counts))} [{' / '.join(parts)}]"
+
+    def print_components(self, ids):   # :189-198, sorts ids in place (largest first; ties by id here)
+        if not self.debug:
+            return
+        ids.sort(key=lambda i: (-len(self.comps[i]["reads"]), i))
+        self.printed.append(f"### Printing {len(ids)} components ###")
+        self.printed += [self.to_string(i) for i in ids]
+        self.printed.append("### ###")
+
     def run(self):   # :737-801
         c = self.cfg
         all_ids = sorted(self.comps)
@@ -346,14 +384,18 @@ class Engine:
             scaffold = conns[:int(len(conns) * c["sc_fraction"])]
         cts = union_find(scaffold, set(), c["sc_min"], c["sc_max"])
         sids = self.merge([x[0] for x in cts])
+        self.print_components(sids)
         if len(sids) > 2:
             strong = [x for x in self.core_connections(cts) if x[2] > 5]
             if strong:
                 self.merge(spectral_clustering(strong, c["dims"]))
             self.remove_merged()
         core = self.ids(c["sc_min"])
+        self.print_components(core)
         conns = self.get_connections(core, c["enrich"])
         cts = union_find(conns, set(core), 2, -1)
         self.merge([x[0] for x in cts])
         self.remove_merged()
-        return self.ids(c["sc_min"])
+        core = self.ids(c["sc_min"])
+        self.print_components(core)
+        return core

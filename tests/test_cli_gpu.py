@@ -187,9 +187,13 @@ def test_categorization_clusters_and_export(tmp_path, hga_mod, args, cfg):
     rec = hga_mod.load_records(paths, True)
     idx = oracle.construct_indices(rec["bases"], rec["offsets"], k, sdk)
     lengths = np.diff(rec["offsets"])
-    eng = pc.Engine(idx, lengths, rec["category"], int(rec["meta"][-1][4]), True, cfg)
+    eng = pc.Engine(idx, lengths, rec["category"], int(rec["meta"][-1][4]), True, cfg, start=rec["start"],
+                    end=rec["end"])
     want = eng.run()
     assert f"Exported {len(want)} components\n" in out.stdout
+    # -d: print_components after each merge (ReadClusteringEngine.cpp:189-198 at :766, :781, :797)
+    assert [ln for ln in out.stdout.splitlines() if ln.startswith("#")] == eng.printed
+    assert out.stdout.count("### Printing") >= 2
     files = sorted(os.listdir(tmp_path / "clusters"))
     assert files == sorted(f"#{c}.fa" for c in want)
     headers = [l.split("\n")[0] for p in paths for l in open(p).read().split(">")[1:]]
