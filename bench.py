@@ -376,12 +376,32 @@ def write_kmer_text(path, codes, k):
     txt.tofile(path)
 
 
-def categorization_pipeline_leg(paths, sdk, threads, d):
-    """Verdict r04 item 7: the drop-in `categorization` CLI end to end on the C3 reads (Nanosim-like FASTA,
-    both haplotypes, -d) against the C2 [10,25] export as a k-mer text file: its own per-stage "took" lines
+def parse_print_blocks(stdout):
+    """print_components' blocks of a `categorization -d` run (ReadClusteringEngine.cpp:189-198):
+    per block [(component id, per-category read counts)]."""
+    blocks, cur = [], None
+    for ln in stdout.splitlines():
+        if ln.startswith("### Printing"):
+            cur = []
+        elif ln == "### ###":
+            blocks.append(cur)
+            cur = None
+        elif cur is not None and ln.startswith("#") and " : " in ln:
+            head = ln.split(" [", 1)[0]
+            cid, counts = head.split(" : ")
+            cur.append((int(cid[1:]), [int(v) for v in counts.split("/")]))
+    return blocks
+
+
+def categorization_pipeline_leg(paths, sdk, threads, d, label="C3"):
+    """Verdict r04 item 7: the drop-in `categorization` CLI end to end on long reads (Nanosim-like FASTA,
+    both haplotypes, -d) against a [10,25] export as a k-mer text file: its own per-stage "took" lines
     (src/common/Utils.h:17-35 timeMeasure: index construction and the first connection pass on the GPU,
-    union-find, merging, tails, spectral clustering, enrichment on the host), next to the reference's
-    published ENP75 run on an i5-8250U (writing/Evaluation.txt:75-82) as context only."""
+    union-find, merging, tails, spectral clustering, enrichment on the host), its HGA_TIMING=1 phases
+    (host work around the stages), and print_components' blocks under -d (ReadClusteringEngine.cpp:
+    189-198): scaffold components, final components with their per-haplotype read counts and the purity
+    (reads of each final component's majority haplotype / reads in final components) — next to the
+    reference's published ENP75 run on an i5-8250U (writing/Evaluation.txt:75-82) as context only."""
     import re
     import subprocess
     cli = os.path.join(ROOT, "hybrid-genome-assembler_amd", "bin", "categorization")
@@ -391,17 +411,30 @@ def categorization_pipeline_leg(paths, sdk, threads, d):
     write_kmer_text(kpath, sdk, K)
     t0 = time.perf_counter()
     r = subprocess.run([cli, *paths, "-k", kpath, "-d", "-o", os.path.join(d, "clusters"), "-t", str(threads)],
-                       capture_output=True, text=True, cwd=d, timeout=900)
+                       capture_output=True, text=True, cwd=d, timeout=900, env=dict(os.environ, HGA_TIMING="1"))
     wall = time.perf_counter() - t0
     stages = {}
     for line in r.stdout.splitlines():
         m = re.match(r"(.+) took (\d+)ms$", line.strip())
         if m:
             stages[m.group(1)] = stages.get(m.group(1), 0) + int(m.group(2))
+    phases = {}
+    for line in r.stderr.splitlines():   # "hga-timing <phase> <ms>" (HGA_TIMING=1)
+        f = line.split()
+        if len(f) == 3 and f[0] == "hga-timing":
+            phases[f[1]] = float(f[2])
     exported = re.search(r"Exported (\d+) components", r.stdout)
-    return {"argv": f"categorization mg1655_nanosim.fasta uti89_nanosim.fasta -k {os.path.basename(kpath)} -d -t {threads}",
-            "rc": r.returncode, "wall_s": round(wall, 3), "stages_ms": stages,
+    blocks = parse_print_blocks(r.stdout)
+    final = blocks[-1] if blocks else []
+    tot = sum(sum(c) for _, c in final)
+    return {"argv": f"categorization {' '.join(os.path.basename(p) for p in paths)} -k {os.path.basename(kpath)} "
+                    f"-d -t {threads}",
+            "workload": label, "rc": r.returncode, "wall_s": round(wall, 3), "stages_ms": stages,
+            "phases_ms": phases,
             "components": int(exported.group(1)) if exported else None,
+            "scaffold_components": len(blocks[0]) if blocks else None,
+            "final_components_reads_per_haplotype": [[cid, c] for cid, c in final],
+            "purity": round(sum(max(c) for _, c in final) / tot, 4) if tot else None,
             "stderr_tail": r.stderr[-300:] if r.returncode else None,
             "published_reference_ENP75_ms": {"Index construction": 49225, "All connections": 4353,
                                              "Merging into scaffold c.": 8751, "Tail connections": 7281,
@@ -409,6 +442,52 @@ def categorization_pipeline_leg(paths, sdk, threads, d):
                                              "Enrichment connections": 116, "Merging into core c.": 2634,
                                              "note": "writing/Evaluation.txt:75-82, Intel Core i5-8250U, the "
                                                      "reference's real ENP75 reads: context, not the same input"}}
+
+
+def mosaic_haplotype(ga, seed, gap=40_000, period=600_000):
+    """Haplotype B for the tails workload: the C2 derivation of A (d = DIV substitutions, no inserted
+    blocks, so coordinates align) made identical to A over `gap`-base stretches every `period` bases.
+    Those stretches hold no SDK, so each haplotype's long-read chain breaks into pieces and the union-find
+    yields more than two scaffold components — the case where run_clustering computes tail connections,
+    spectral clustering and the scaffold-component merge (ReadClusteringEngine.cpp:768-777), which the
+    plain C3 pair (one unbroken chain per haplotype) never reaches."""
+    gb = bytearray(hga.gen_haplotype(ga, DIV, 0, seed))
+    for s0 in range(period // 2, len(ga), period):
+        gb[s0:s0 + gap] = ga[s0:s0 + gap]
+    return bytes(gb)
+
+
+def tails_pipeline_leg(ga, dev, threads):
+    """the categorization CLI on a C3-sized workload that reaches the tails and spectral
+    stages (mosaic_haplotype): its SDKs counted on the GPU from ART-like 30x short reads of the pair and
+    exported at [10, 25] as jf_occurrences does, long reads Nanosim-like at 75x (C3's generators)."""
+    import shutil
+    import tempfile
+    gbm = mosaic_haplotype(ga, 77)
+    ra = hga.gen_art(ga, COVERAGE * LA // READ_LEN, READ_LEN, 5000)
+    rb = hga.gen_art(gbm, COVERAGE * len(gbm) // READ_LEN, READ_LEN, 5001)
+    with hga.Ctx(dev) as c:
+        c.count_begin(K, 2)
+        c.count_add(0, ra.seq)
+        c.count_add(1, rb.seq)
+        c.count_run(2)
+        sdk, _, _ = c.select(LOWER, UPPER)
+    del ra, rb
+    d = tempfile.mkdtemp(prefix="hga_tails_")
+    try:
+        n = round(LA / 7777 * 75)
+        paths = [os.path.join(d, "hapA_nanosim.fasta"), os.path.join(d, "hapB_mosaic_nanosim.fasta")]
+        hga.write_nanosim_fasta(ga, "A", n, 5002, paths[0])
+        hga.write_nanosim_fasta(gbm, "B", n, 5003, paths[1])
+        out = categorization_pipeline_leg(paths, sdk, threads, d,
+                                          label="C3-sized tails workload: haplotype B = A with d=0.021 except 40 kb "
+                                                "identical stretches every 600 kb; SDKs: GPU count of ART-like 30x "
+                                                "short reads, [10,25]; long reads Nanosim-like 75x")
+        if out is not None:
+            out["sdk"] = int(len(sdk))
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def lookup_parse_leg(ga, gb, n_reads, lookup_s, bases, offsets, threads, sdk=None):
@@ -568,24 +647,33 @@ def scale_leg(D, reps=2):
         ms = D.max((time.perf_counter() - t0) / reps * 1e3)
         st = c4.count_stats()   # global after the exchange
         export = None
-        if ex4:   # the full export of the last step in code order on every rank (re-partition + gather)
+        if ex4:   # the full export of the last step in code order, to one writer (rank 0)
+            import resource
+            c4.comm_set_root(0)   # hga_comm_set_root: one copy crosses the ranks, not N
             D.barrier()
+            rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
             t1 = time.perf_counter()
             keys, flags = ex4.select(LOWER, UPPER)
             D.barrier()
             exp_ms = D.max((time.perf_counter() - t1) * 1e3)
+            rss1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
             k64 = keys.astype(np.uint64)
+            off_root = D.max(float(len(keys)) if D.rank != 0 else 0.0)
             # size-independent invariants of the exchanged C4 result (its rows are not checked against
             # the oracle at this size: parity unpinned here, the C2 shards carry the N > 1 parity check)
             inv = {"export_ascending": bool(len(k64) < 2 or bool(np.all(k64[1:] > k64[:-1]))),
                    "export_count_matches_select": int(len(keys)) == int(n_sel),
                    "discriminative_matches_flags": int(flags.sum()) == int(n_disc),
-                   "global_instances_equal_sum_of_ranks": int(st.instances) == int(D.sum(float(c4_local_inst)))}
-            export = {"ms": round(exp_ms, 2), "keys": int(len(keys)),
-                      "note": "hga_count_select + hga_count_fetch_selected after the exchange: the owners' sorted "
-                              "selections re-partitioned by code range (one all-to-all), every rank's range "
-                              "gathered to every rank in rank order",
+                   "global_instances_equal_sum_of_ranks": int(st.instances) == int(D.sum(float(c4_local_inst))),
+                   "other_ranks_receive_nothing": off_root == 0.0}
+            export = {"ms": round(exp_ms, 2), "keys": int(len(keys)), "bytes_on_root": int(len(keys)) * 9,
+                      "max_keys_on_other_ranks": int(off_root),
+                      "max_rss_growth_mb": round(D.max((rss1 - rss0) / 1024.0), 1),
+                      "note": "hga_comm_set_root(0) + hga_count_select_ex after the exchange: the owners' sorted "
+                              "selections re-partitioned by code range (one all-to-all), the ranges gathered to "
+                              "rank 0 only, in rank order (one writer, JellyfishOccurrenceReader.cpp:110-135)",
                       "invariants": inv, "parity": "unpinned at C4 size (invariants only)"}
+            c4.comm_set_root(-1)
         return {"workload": f"C4 (configs[3]): {D.world} of the 8 rank shards of ART-like 30x reads of a 2 x 500 Mbp "
                             "diploid (d=0.005), k=19, 2 files per shard; step = count_run + "
                             + ("hga_count_exchange (owner all-to-all) + " if ex4 else "")
@@ -733,15 +821,19 @@ def main():
                               "achieved": round(pipe_gbs, 1), "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)},
         "kernels_ms_per_step": {k: round(v["ms_per_step"], 4) for k, v in kernels.items()},
     }
-    if ex:   # the full export of the last timed step in code order on every rank
+    if ex:   # the full export of the last timed step in code order, to one writer
+        ctx.comm_set_root(0)
         D.barrier()
         t1 = time.perf_counter()
         ek, ef = ex.select(LOWER, UPPER)
         D.barrier()
+        off_root = D.max(float(len(ek)) if D.rank != 0 else 0.0)
         result["export"] = {"ms": round(D.max((time.perf_counter() - t1) * 1e3), 3), "keys": int(len(ek)),
-                            "discriminative": int(ef.sum()),
-                            "note": "select + fetch after the exchange: owners' sorted selections re-partitioned by "
-                                    "code range (one all-to-all of the export), ranges gathered in rank order"}
+                            "discriminative": int(ef.sum()), "max_keys_on_other_ranks": int(off_root),
+                            "note": "hga_comm_set_root(0) + select + fetch after the exchange: owners' sorted "
+                                    "selections re-partitioned by code range (one all-to-all of the export), "
+                                    "ranges gathered to rank 0 in rank order"}
+        ctx.comm_set_root(-1)
         del ek, ef
     if ex and not args.no_check:   # the state of the last timed step: the exchanged global count
         result["parity"] = dist_parity(ctx, D, min(16 * D.world, os.cpu_count() or 16))
@@ -804,6 +896,8 @@ def main():
             if wp.get("pipeline") is not None:
                 result["categorize"]["pipeline"] = wp.pop("pipeline")
             result["categorize"]["with_parsing"] = wp
+        if D.world == 1 and not args.no_ingest:
+            result["categorize"]["pipeline_tails"] = tails_pipeline_leg(ga, dev, args.cpu_threads)
         result["categorize"]["connections"] = connections_leg(ctx2, D, reps, args)
         result["categorize"]["hll_auto_k"] = hll_leg(ctx2, D, len(bases), bases, offsets, args)
         ctx2.close()

@@ -181,8 +181,9 @@ hga_status hga_count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t**
             std::vector<uint8_t> f;
             hga::count_fetch_selected_global(c, k, f);
             *keys = host_dup(k.data(), k.size());
-            *n = m;
-            *n_discriminative = d;
+            const bool leaf = hga::comm_is_gather_leaf(c);   // (hga_comm_set_root: an empty list here)
+            *n = leaf ? 0 : m;
+            *n_discriminative = leaf ? 0 : d;
             return;
         }
         hga::count_select(c, lower, upper, &m, &d);
@@ -207,8 +208,9 @@ hga_status hga_count_select_ex(hga_ctx* c, int64_t lower, int64_t upper, uint64_
             hga::count_fetch_selected_global(c, k, f);
             *keys = host_dup(k.data(), k.size());
             *disc = host_dup(f.data(), f.size());
-            *n = m;
-            *n_discriminative = d;
+            const bool leaf = hga::comm_is_gather_leaf(c);   // (hga_comm_set_root: an empty list here)
+            *n = leaf ? 0 : m;
+            *n_discriminative = leaf ? 0 : d;
             return;
         }
         hga::count_select(c, lower, upper, &m, &d);
@@ -394,6 +396,10 @@ hga_status hga_comm_info(hga_ctx* c, int* rank, int* nranks) {
         *rank = c->comm ? c->comm->rank : 0;
         *nranks = c->comm ? c->comm->nranks : 1;
     });
+}
+
+hga_status hga_comm_set_root(hga_ctx* c, int root) {
+    HGA_CTX_GUARD(c, { hga::comm_set_root(c, root); });
 }
 
 hga_status hga_comm_destroy(hga_ctx* c) {

@@ -154,6 +154,53 @@ std::vector<std::vector<char>> comm_allgatherv(hga_ctx* c, const void* mine, uin
     return out;
 }
 
+// Variable-size gather of host bytes to `root`, in rank order (empty on the other ranks): the sizes
+// all-gathered (8 B each), then one all-to-all in which every rank sends only to the root.
+std::vector<std::vector<char>> comm_gatherv_root(hga_ctx* c, const void* mine, uint64_t bytes, int root) {
+    Comm& m = need_comm(c);
+    const int P = m.nranks, me = m.rank;
+    HGA_REQUIRE(root >= 0 && root < P, HGA_ERR_INVALID, "gather root out of range");
+    std::vector<uint64_t> sz(P);
+    comm_allgather(c, &bytes, 8, sz.data());
+    std::vector<std::vector<char>> out(P);
+    std::vector<uint64_t> sb(P, 0), rb(P, 0);
+    sb[root] = bytes;
+    if (me == root)
+        for (int p = 0; p < P; ++p) rb[p] = sz[p];
+    std::vector<const void*> sp(P);
+    std::vector<void*> rp(P);
+    if (!m.on_device()) {
+        for (int p = 0; p < P; ++p) {
+            if (me == root) out[p].resize(sz[p]);
+            sp[p] = mine;
+            rp[p] = me == root ? out[p].data() : nullptr;
+        }
+        m.alltoallv(c, sp.data(), sb.data(), rp.data(), rb.data());
+        return out;
+    }
+    uint64_t tot = 0;
+    for (int p = 0; p < P; ++p) tot += rb[p];
+    char* ds = static_cast<char*>(m.stage.ensure(bytes + tot + 16));
+    if (bytes) HGA_HIP(hipMemcpyAsync(ds, mine, bytes, hipMemcpyHostToDevice, c->stream));
+    uint64_t o = bytes;
+    for (int p = 0; p < P; ++p) {
+        sp[p] = ds;
+        rp[p] = ds + o;
+        o += rb[p];
+    }
+    m.alltoallv(c, sp.data(), sb.data(), rp.data(), rb.data());
+    if (me == root) {
+        o = bytes;
+        for (int p = 0; p < P; ++p) {
+            out[p].resize(sz[p]);
+            if (sz[p]) HGA_HIP(hipMemcpyAsync(out[p].data(), ds + o, sz[p], hipMemcpyDeviceToHost, c->stream));
+            o += sz[p];
+        }
+    }
+    c->sync();
+    return out;
+}
+
 // All-to-all-v of DEVICE buffers whose per-peer slices are contiguous in rank order; keep_self
 // false: the rank's own slice is not moved (rb[rank] must be 0).
 void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb_in, void* recv, const uint64_t* rb,
@@ -220,6 +267,9 @@ struct CtxXport : proto::Xport {
     }
     void alltoallv_eng(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb, bool keep_self) override {
         comm_alltoallv_dev(c, send, sb, recv, rb, keep_self);
+    }
+    std::vector<std::vector<char>> gatherv_root(const void* mine, uint64_t bytes, int root) override {
+        return comm_gatherv_root(c, mine, bytes, root);
     }
 };
 
@@ -677,10 +727,12 @@ uint64_t count_export_repartition(hga_ctx* c) {
     return s.sel_rep_n;
 }
 
-// The whole export on every rank (after count_select): the ranks' code ranges concatenated in rank
-// order — ascending, no merge.
+// The whole export (after count_select): the ranks' code ranges concatenated in rank order —
+// ascending, no merge — on every rank, or on the gather root only (hga_comm_set_root: one writer,
+// JellyfishOccurrenceReader.cpp:110-135; the other ranks get an empty list).
 void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::vector<uint8_t>& flags) {
     auto& s = c->count;
+    const int root = need_comm(c).root;
     const uint64_t n = count_export_repartition(c);
     const bool flag_bit = s.k <= 31;
     std::vector<uint64_t> k(n);
@@ -699,14 +751,16 @@ void count_fetch_selected_global(hga_ctx* c, std::vector<uint64_t>& keys, std::v
         }
     }
     CtxXport x(c);
-    keys = proto::concat(x, k);
-    flags = proto::concat(x, f);
+    keys = proto::concat_root(x, k, root);
+    flags = proto::concat_root(x, f, root);
 }
 
 // The global rows (file < 0) or one file's dump rows: the owners' sorted rows re-partitioned by code
-// range on the device (one all-to-all of the rows), each rank's range fetched, concatenated.
+// range on the device (one all-to-all of the rows), each rank's range fetched, concatenated on every
+// rank or on the gather root only (hga_comm_set_root).
 void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::vector<uint32_t>& counts) {
     auto& s = c->count;
+    const int root = need_comm(c).root;
     count_settle(c);
     HGA_REQUIRE(s.ran, HGA_ERR_STATE, "hga_count_run not called");
     count_dense(c);
@@ -736,8 +790,18 @@ void count_rows_global(hga_ctx* c, int file, std::vector<uint64_t>& keys, std::v
                 mv.push_back(v[i * F + (uint32_t)file]);
             }
     }
-    keys = proto::concat(x, mk);
-    counts = proto::concat(x, mv);
+    keys = proto::concat_root(x, mk, root);
+    counts = proto::concat_root(x, mv, root);
+}
+
+void comm_set_root(hga_ctx* c, int root) {
+    Comm& m = need_comm(c);
+    HGA_REQUIRE(root >= -1 && root < m.nranks, HGA_ERR_INVALID, "root must be -1 or a rank");
+    m.root = root;
+}
+
+bool comm_is_gather_leaf(hga_ctx* c) {   // a rank that gets no copy of the gathered lists
+    return c->comm && c->comm->root >= 0 && c->comm->root != c->comm->rank;
 }
 
 // ---- sharded categorization ------------------------------------------------------------------

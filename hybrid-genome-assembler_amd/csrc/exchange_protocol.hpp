@@ -41,6 +41,9 @@ struct Xport {
     virtual std::vector<std::vector<char>> allgatherv(const void* mine, uint64_t bytes) = 0;
     virtual void alltoallv_eng(const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes,
                                bool keep_self = true) = 0;
+    // Every rank's bytes, in rank order, on `root` only (the other ranks get an empty list): one copy of
+    // a gathered result crosses the ranks instead of P (the export to one writer).
+    virtual std::vector<std::vector<char>> gatherv_root(const void* mine, uint64_t bytes, int root) = 0;
 };
 
 // Owner ranges over canonical codes in [0, 4^k): canonical = min(fwd, rc) of uniform codes has mass
@@ -264,6 +267,19 @@ inline std::vector<uint64_t> sum_u64(Xport& x, const std::vector<uint64_t>& mine
 template <class T>
 std::vector<T> concat(Xport& x, const std::vector<T>& mine) {
     const auto parts = x.allgatherv(mine.data(), mine.size() * sizeof(T));
+    std::vector<T> out;
+    for (const auto& pt : parts) {
+        const T* v = reinterpret_cast<const T*>(pt.data());
+        out.insert(out.end(), v, v + pt.size() / sizeof(T));
+    }
+    return out;
+}
+
+// concat on `root` only (root >= 0; the other ranks get an empty vector), or on every rank (root < 0).
+template <class T>
+std::vector<T> concat_root(Xport& x, const std::vector<T>& mine, int root) {
+    if (root < 0) return concat(x, mine);
+    const auto parts = x.gatherv_root(mine.data(), mine.size() * sizeof(T), root);
     std::vector<T> out;
     for (const auto& pt : parts) {
         const T* v = reinterpret_cast<const T*>(pt.data());

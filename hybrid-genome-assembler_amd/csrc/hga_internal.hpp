@@ -211,6 +211,7 @@ struct ConnState {
 // Multi-GPU transport of one rank (comm.hip): RCCL over xGMI, or a caller's host-staged hook.
 struct Comm {
     int rank = 0, nranks = 1;
+    int root = -1;   // hga_comm_set_root: gathered lists on this rank only (-1: every rank)
     DevBuf stage;   // device staging of host-memory collectives over RCCL (grow-only: no hipMalloc per call)
     PinnedBuf hstage;   // their host side
     virtual ~Comm() = default;
@@ -309,6 +310,9 @@ void comm_init_rccl(hga_ctx* c, const void* id, int rank, int nranks);
 void comm_init_host(hga_ctx* c, int rank, int nranks, const hga_transport* t);
 void comm_allgather(hga_ctx* c, const void* mine, uint64_t bytes, void* all);
 std::vector<std::vector<char>> comm_allgatherv(hga_ctx* c, const void* mine, uint64_t bytes);
+std::vector<std::vector<char>> comm_gatherv_root(hga_ctx* c, const void* mine, uint64_t bytes, int root);
+void comm_set_root(hga_ctx* c, int root);
+bool comm_is_gather_leaf(hga_ctx* c);
 void comm_alltoallv_dev(hga_ctx* c, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb,
                         bool keep_self = true);
 std::vector<uint64_t> owner_splitters(int k, int P);

@@ -101,6 +101,7 @@ HGA_SYMBOLS = {
     "hga_comm_init_host": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(Transport)]),
     "hga_comm_info": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hga_comm_destroy": (C.c_int, [_vp]),
+    "hga_comm_set_root": (C.c_int, [_vp, C.c_int]),
     "hga_count_exchange": (C.c_int, [_vp, C.c_uint32]),
     "hga_lookup_gather": (C.c_int, [_vp]),
     "hga_connections_gather": (C.c_int, [_vp, _u64p]),
@@ -250,6 +251,11 @@ class Ctx:
     def comm_init_host(self, rank: int, nranks: int, transport: "Transport"):
         self._transport = transport
         _ck(lib().hga_comm_init_host(self._h, rank, nranks, C.byref(transport)))
+
+    def comm_set_root(self, root: int):
+        """Gathered lists (select / select_ex / rows / dump after an exchange) on rank `root` only; the
+        other ranks get empty ones (-1: every rank)."""
+        _ck(lib().hga_comm_set_root(self._h, root))
 
     def comm_info(self):
         r, n = C.c_int(), C.c_int()

@@ -26,15 +26,18 @@
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
 #include "args.h"
 #include "clustering.h"
 #include "hga.h"
+#include "phase_timer.h"
 #include "ranks.h"
 #include "seqio.h"
 
@@ -101,17 +104,36 @@ int main(int argc, char* argv[]) {
     }
     if (read_paths.empty()) throw std::invalid_argument("You need to specify paths to read files");
     if (kmer_path.empty()) throw std::invalid_argument("You need to specify path to kmers");
+    hgah::PhaseTimer tm;
+    const char* dev_env = std::getenv("HGA_DEVICE");
+    // device set-up (HIP init, contexts) on a thread while the k-mer file and the reads are read
+    std::unique_ptr<hgah::Ranks> ranks_p;
+    std::exception_ptr init_err;
+    std::thread init_th([&] {
+        try {
+            ranks_p = std::make_unique<hgah::Ranks>(gpus, dev_env ? std::atoi(dev_env) : 0);
+        } catch (...) {
+            init_err = std::current_exception();
+        }
+    });
+    struct InitJoin {   // joined on every way out (an input error must not leave the thread running)
+        std::thread& t;
+        ~InitJoin() { if (t.joinable()) t.join(); }
+    } init_join{init_th};
     auto kk = load_text_file_kmers(kmer_path);
     const int k = kk.second;
     if (k < 1 || k > 32) throw std::invalid_argument("Kmer size must be in [1, 32]");
+    tm.mark("sdk_load");
 
     hgah::RecordSet rs = hgah::load_records(read_paths, debug, true);   // headers/qualities for the export
     for (auto& m : rs.file_meta) std::cout << m.repr();
     if (output_folder_path.empty()) output_folder_path = "./" + rs.meta.filename + "_clusters/";
     const bool engine_debug = rs.file_meta.size() == rs.categories;   // ReadClusteringEngine.cpp:229
-
-    const char* dev_env = std::getenv("HGA_DEVICE");
-    hgah::Ranks ranks(gpus, dev_env ? std::atoi(dev_env) : 0);
+    tm.mark("read_files");
+    init_th.join();
+    if (init_err) std::rethrow_exception(init_err);
+    tm.mark("device_init_wait");
+    hgah::Ranks& ranks = *ranks_p;
     hga_ctx* ctx = ranks.ctx[0];
     const int P = ranks.size();
     const uint64_t n_reads = rs.size();
@@ -143,6 +165,7 @@ int main(int argc, char* argv[]) {
     const auto t1 = std::chrono::steady_clock::now();
     std::cout << "Index construction took "
               << std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count() << "ms\n";
+    tm.mark("index_construction");
 
     if (engine_debug) {   // ReadClusteringEngine.cpp:285-297
         uint32_t discriminative = 0, total = 0;
@@ -153,6 +176,7 @@ int main(int argc, char* argv[]) {
             if (!cats.empty()) ++total;
         }
         std::cout << discriminative << " out of " << total << " kmers are discriminative \n";
+        tm.mark("discriminative_check");
     }
     if (!index_out.empty()) {
         std::FILE* f = std::fopen(index_out.c_str(), "wb");
@@ -212,7 +236,11 @@ int main(int argc, char* argv[]) {
             return out;
         });
     }
+    tm.mark("engine_setup");
     const std::vector<hgah::ComponentID> cluster_ids = engine.run(std::cout);   // run_clustering (:699-802)
+    tm.mark("run_clustering");
     engine.export_components(cluster_ids, output_folder_path, std::cout);       // read_clustering.cpp:82
+    tm.mark("export_components");
+    tm.total();
     return 0;
 }

@@ -48,6 +48,7 @@
 #include "args.h"
 #include "hga.h"
 #include "kmer_analysis.h"
+#include "phase_timer.h"
 #include "ranks.h"
 #include "seqio.h"
 
@@ -73,23 +74,7 @@ int run_command_with_input(const std::string& cmd, const std::string& in) {
     return EXIT_SUCCESS;
 }
 
-// Phase timer for HGA_TIMING=1.
-struct PhaseTimer {
-    bool on = false;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
-    void mark(const char* phase) {
-        if (!on) return;
-        const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "hga-timing %s %.2f\n", phase,
-                     std::chrono::duration<double, std::milli>(now - last).count());
-        last = now;
-    }
-    void total() {
-        if (on)
-            std::fprintf(stderr, "hga-timing total %.2f\n",
-                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-    }
-};
+using hgah::PhaseTimer;
 
 using KmerSpecificity = std::map<double, std::map<int, int>>;
 
@@ -143,7 +128,6 @@ int main(int argc, char* argv[]) {
     if (read_paths.empty()) throw std::invalid_argument("You need to specify paths to read files");
 
     PhaseTimer tm;
-    if (const char* te = std::getenv("HGA_TIMING")) tm.on = std::string(te) == "1";
     const char* dev_env = std::getenv("HGA_DEVICE");
     // device set-up (HIP init, contexts) on a thread while the files are read, when k is given
     std::unique_ptr<hgah::Ranks> ranks_p;
@@ -188,7 +172,12 @@ int main(int argc, char* argv[]) {
     hgah::Ranks& ranks = *ranks_p;
     hga_ctx* ctx = ranks.ctx[0];
     const int P = ranks.size();
-    for (auto* c : ranks.ctx) check(hga_count_begin(c, k, (uint32_t)read_paths.size()), "hga_count_begin");
+    for (auto* c : ranks.ctx) {
+        check(hga_count_begin(c, k, (uint32_t)read_paths.size()), "hga_count_begin");
+        // --gpus N: the dumps and the export reach rank 0 only (one writer, one copy in this process,
+        // as the reference's single export pass writes them, JellyfishOccurrenceReader.cpp:110-135)
+        if (P > 1) check(hga_comm_set_root(c, 0), "hga_comm_set_root");
+    }
     for (uint32_t f = 0; f < read_paths.size(); ++f) {
         if (cached[f]) {
             check(hga_count_add_rows(ctx, f, cache_k[f].data(), cache_c[f].data(), cache_k[f].size()),

@@ -197,6 +197,12 @@ typedef struct hga_transport {
 hga_status hga_comm_init_host(hga_ctx* ctx, int rank, int nranks, const hga_transport* transport);
 /* This ctx's rank and rank count (0 and 1 without a communicator). */
 hga_status hga_comm_info(hga_ctx* ctx, int* rank, int* nranks);
+/* Gathered lists on one rank only (the export and the dumps to one writer, as the
+ * reference's single export_kmers pass writes them, JellyfishOccurrenceReader.cpp:110-135): after it,
+ * hga_count_select / _select_ex / _rows / _dump still run on every rank (collectives), but only rank
+ * `root` receives the list; the other ranks get an empty one (*n, *n_discriminative, *rows = 0).  One
+ * copy crosses the ranks instead of P.  root = -1 (the default): every rank gets the whole list. */
+hga_status hga_comm_set_root(hga_ctx* ctx, int root);
 hga_status hga_comm_destroy(hga_ctx* ctx);
 
 /* Owner exchange after hga_count_run(ctx, 1) on every rank: owners hold ranges of a hash of the

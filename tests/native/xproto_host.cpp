@@ -60,6 +60,23 @@ struct HostXport : Xport {
         if (!keep_self) ss[rank] = rr[rank] = 0;
         a2a(s.data(), ss.data(), r.data(), rr.data());
     }
+    std::vector<std::vector<char>> gatherv_root(const void* mine, uint64_t bytes, int root) override {
+        std::vector<uint64_t> sz(nranks);
+        allgather(&bytes, 8, sz.data());
+        std::vector<std::vector<char>> out(nranks);
+        std::vector<const void*> s(nranks, mine);
+        std::vector<void*> r(nranks, nullptr);
+        std::vector<uint64_t> sb(nranks, 0), rb(nranks, 0);
+        sb[root] = bytes;
+        if (rank == root)
+            for (int p = 0; p < nranks; ++p) {
+                out[p].resize(sz[p]);
+                r[p] = out[p].data();
+                rb[p] = sz[p];
+            }
+        a2a(s.data(), sb.data(), r.data(), rb.data());
+        return out;
+    }
 };
 
 int jf_code(unsigned char c) {
@@ -276,6 +293,7 @@ struct Rank {
     HostEngine e;
     HostXport x;
     std::vector<std::string> shard;
+    int root = -1;   // hga_comm_set_root: gathered lists on this rank only
 };
 
 template <class T>
@@ -364,6 +382,9 @@ int64_t xt_hist_merge(void* h, const int64_t* local, int64_t n_triples, int64_t*
     return (int64_t)g.size() / 3;
 }
 
+// the product's hga_comm_set_root
+void xt_set_root(void* h, int root) { static_cast<Rank*>(h)->root = root; }
+
 // global export: keys ascending (the owners' slices merged), flags; *n_discr over all owners
 int64_t xt_select(void* h, int64_t lower, int64_t upper, uint64_t** keys, uint8_t** flags, uint64_t* n_discr) {
     auto* r = static_cast<Rank*>(h);
@@ -390,8 +411,8 @@ int64_t xt_select(void* h, int64_t lower, int64_t upper, uint64_t** keys, uint8_
     l.v.assign(f.begin(), f.end());
     hga::proto::repartition(l, r->x, r->e.k_);
     std::vector<uint8_t> lf(l.v.begin(), l.v.end());
-    const std::vector<uint64_t> gk = hga::proto::concat(r->x, l.k);
-    const std::vector<uint8_t> gf = hga::proto::concat(r->x, lf);
+    const std::vector<uint64_t> gk = hga::proto::concat_root(r->x, l.k, r->root);
+    const std::vector<uint8_t> gf = hga::proto::concat_root(r->x, lf, r->root);
     *n_discr = hga::proto::sum_u64(r->x, {d})[0];
     *keys = dup(gk);
     *flags = dup(gf);
@@ -410,8 +431,8 @@ int64_t xt_rows(void* h, uint64_t** keys, uint32_t** counts) {
     l.k = r->e.keys;
     l.v = c;
     hga::proto::repartition(l, r->x, r->e.k_);
-    const std::vector<uint64_t> gk = hga::proto::concat(r->x, l.k);
-    const std::vector<uint32_t> gc = hga::proto::concat(r->x, l.v);
+    const std::vector<uint64_t> gk = hga::proto::concat_root(r->x, l.k, r->root);
+    const std::vector<uint32_t> gc = hga::proto::concat_root(r->x, l.v, r->root);
     *keys = dup(gk);
     *counts = dup(gc);
     return (int64_t)gk.size();

@@ -42,6 +42,7 @@ def xlib():
     L.xt_rows.restype = C.c_int64
     L.xt_rows.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
     L.xt_splitters.argtypes = [C.c_int, C.c_int, C.c_void_p]
+    L.xt_set_root.argtypes = [C.c_void_p, C.c_int]
     L.xt_free.argtypes = [C.c_void_p]
     L.xt_destroy.argtypes = [C.c_void_p]
     return L
@@ -84,13 +85,14 @@ def make_streams(seed=7, n_reads=600, L=3000, heavy=False):
     return out
 
 
-def _worker(rank, world, port, lower, upper, out_path, packed, k, heavy):
+def _worker(rank, world, port, lower, upper, out_path, packed, k, heavy, root=-1):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         L = xlib()
         streams = make_streams(heavy=heavy)
         t = hga_dist.gloo_transport()
         h = L.xt_create(k, len(streams), rank, world, C.addressof(t), 1 if packed else 0)
+        L.xt_set_root(h, root)
         for f, s in enumerate(streams):
             sh = hga_dist.shard_reads(s, rank, world)
             L.xt_add(h, f, sh, len(sh))
@@ -124,6 +126,25 @@ def test_exchange_protocol_matches_single_process(world, packed, k, heavy, tmp_p
         assert np.array_equal(r["hist"], ref["hist"])
         assert np.array_equal(r["keys"], ref["selected"])
         assert int(r["d"]) == ref["n_discr"] and int(r["flags"].sum()) == ref["n_discr"]
+
+
+@pytest.mark.parametrize("world,root", [(2, 0), (3, 2)])
+def test_gathered_lists_to_one_root(world, root, tmp_path):
+    """hga_comm_set_root (one writer as JellyfishOccurrenceReader.cpp:110-135): the
+    export and the rows reach the root rank only, equal to the single-process oracle; every other rank
+    takes part in the collectives and receives nothing (one copy crosses the ranks, not P)."""
+    out = str(tmp_path / "dist")
+    mp.start_processes(_worker, args=(world, _free_port(), 3, 40, out, True, 11, False, root), nprocs=world,
+                       start_method="spawn")
+    ref = oracle.count_pipeline(make_streams(), 11, 3, 40)
+    for rank in range(world):
+        r = np.load(out + f".{rank}.npz")
+        assert np.array_equal(r["hist"], ref["hist"])   # (the histogram stays on every rank)
+        if rank == root:
+            assert np.array_equal(r["rkeys"], ref["keys"]) and np.array_equal(r["rcnts"], ref["counts"])
+            assert np.array_equal(r["keys"], ref["selected"]) and int(r["flags"].sum()) == ref["n_discr"]
+        else:
+            assert len(r["keys"]) == 0 and len(r["rkeys"]) == 0 and len(r["flags"]) == 0
 
 
 def _hist_worker(rank, world, port, sizes, out_path):

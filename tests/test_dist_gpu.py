@@ -93,7 +93,7 @@ def test_partition_merge_min_counts_and_empty_owner():
     assert np.array_equal(keys, rk) and np.array_equal(counts, rc)
 
 
-def _worker(rank, world, port, out_path, k, envs=None, big=False):
+def _worker(rank, world, port, out_path, k, envs=None, big=False, root=-1):
     import os
     import torch.distributed as dist
     if envs:   # this rank's exchange test hooks (count.hip / exchange.hip)
@@ -107,6 +107,8 @@ def _worker(rank, world, port, out_path, k, envs=None, big=False):
             ctx.count_add(f, hga_dist.shard_reads(s, rank, world))
         ex = hga_dist.OwnerExchange(ctx)
         assert ctx.comm_info() == (rank, world)
+        if root >= 0:
+            ctx.comm_set_root(root)
         ex.count(2)
         hist = ex.spec_hist(THR)
         keys, flags = ex.select(3, 40)
@@ -325,3 +327,29 @@ def test_sharded_lookup_gather_and_connections(tmp_path, world):
             assert np.array_equal(r[name], ref[name]), name
         assert np.array_equal(r["x"], rx) and np.array_equal(r["y"], ry)
         assert np.array_equal(r["s"], rs) and np.array_equal(r["g"], rg)
+
+
+@pytest.mark.parametrize("world,root,envs", [(2, 1, None), (3, 0, (EMIT, _gen(10), EMIT))])
+def test_gathered_lists_to_one_root(tmp_path, world, root, envs):
+    """hga_comm_set_root (the export and the dumps to one writer, as the reference's
+    single export pass, JellyfishOccurrenceReader.cpp:110-135): after the exchange, select / rows / dump
+    deliver the whole list on the root only — equal to the oracle there — and empty lists elsewhere; the
+    histogram and the global counts stay on every rank."""
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "d")
+    mp.start_processes(_worker, args=(world, port, out, 13, envs, False, root), nprocs=world, start_method="spawn")
+    ref = oracle.count_pipeline(make_streams(), 13, 3, 40)
+    for rank in range(world):
+        r = np.load(out + f".{rank}.npz")
+        assert np.array_equal(r["hist"], ref["hist"])
+        assert int(r["rows"]) == len(ref["keys"])
+        if rank == root:
+            assert np.array_equal(r["keys"], ref["selected"]) and int(r["flags"].sum()) == ref["n_discr"]
+            assert np.array_equal(r["rk"], ref["keys"]) and np.array_equal(r["rc"], ref["counts"])
+            assert np.array_equal(r["d0k"], ref["dumps"][0][0]) and np.array_equal(r["d0c"], ref["dumps"][0][1])
+        else:
+            assert len(r["keys"]) == 0 and len(r["rk"]) == 0 and len(r["d0k"]) == 0
