@@ -128,6 +128,8 @@ HOST_SYMBOLS = {
     "hgh_fmt_double": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
     "hgh_hll_estimate": (C.c_double, [_u8p, C.c_int]),
     "hgh_set_threads": (None, [C.c_int]),
+    "hgh_load_kmer_text": (C.c_int, [C.c_char_p, C.POINTER(_u64p), _u64p, C.POINTER(C.c_int)]),
+    "hgh_unordered_set_order": (C.c_int, [_u64p, C.c_uint64, C.POINTER(_u64p), _u64p]),
     "hgh_write_kmer_dump": (C.c_int, [C.c_char_p, C.c_int, _u64p, _u32p, C.c_uint64]),
 }
 
@@ -534,6 +536,22 @@ def write_kmer_dump(path: str, k: int, keys, counts):
     keys = np.ascontiguousarray(keys, dtype=np.uint64)
     counts = np.ascontiguousarray(counts, dtype=np.uint32)
     _hck(host().hgh_write_kmer_dump(path.encode(), k, keys.ctypes.data_as(_u64p), counts.ctypes.data_as(_u32p), len(keys)))
+
+
+def load_kmer_text(path: str):
+    """categorization's SDK loader (load_text_file_kmers, read_clustering.cpp:18-33): (codes in KmerID
+    order, k)."""
+    p, n, k = _u64p(), C.c_uint64(), C.c_int()
+    _hck(host().hgh_load_kmer_text(path.encode(), C.byref(p), C.byref(n), C.byref(k)))
+    return _take(p, n.value, np.uint64, host().hgh_free), k.value
+
+
+def unordered_set_order(keys):
+    """The iteration order of a std::unordered_set<uint64_t> filled with `keys` in order."""
+    keys = np.ascontiguousarray(keys, np.uint64)
+    p, m = _u64p(), C.c_uint64()
+    _hck(host().hgh_unordered_set_order(keys.ctypes.data_as(_u64p), len(keys), C.byref(p), C.byref(m)))
+    return _take(p, m.value, np.uint64, host().hgh_free)
 
 
 def set_host_threads(n: int):

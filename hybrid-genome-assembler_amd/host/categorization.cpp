@@ -46,17 +46,14 @@ void check(hga_status s, const char* what) {
     if (s != HGA_OK) throw std::runtime_error(std::string(what) + ": " + hga_last_error());
 }
 
-// load_text_file_kmers (src/read_clustering.cpp:18-33)
+// load_text_file_kmers (src/read_clustering.cpp:18-33): KmerID = the iteration order of the
+// std::unordered_set the reference fills line by line (hgah::load_kmer_text reproduces it without the
+// per-key node allocations: 0.78 s -> see DESIGN.md §7 for the C2 export's 1.82 M lines).
 std::pair<std::vector<uint64_t>, int> load_text_file_kmers(const std::string& path) {
-    std::ifstream in(path);
-    std::string line;
+    if (!std::ifstream(path)) return {{}, 0};   // (an unreadable file reads as empty there)
     int k = 0;
-    std::unordered_set<uint64_t> s;
-    while (std::getline(in, line)) {
-        k = (int)line.length();
-        s.insert(hgah::line_canonical(line.data(), line.size()));
-    }
-    return {std::vector<uint64_t>(s.begin(), s.end()), k};   // KmerID = iteration order
+    std::vector<uint64_t> keys = hgah::load_kmer_text(path, &k);
+    return {std::move(keys), k};
 }
 }  // namespace
 

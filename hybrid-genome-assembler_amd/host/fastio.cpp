@@ -27,6 +27,8 @@
 #include <stdexcept>
 #include <memory>
 #include <thread>
+#include <unordered_set>
+#include <vector>
 
 #include "seqio.h"
 #include "seqio_internal.h"
@@ -400,6 +402,119 @@ RecordSet load_records(const std::vector<std::string>& paths, bool annotate, boo
     for (size_t i = 0; i < names.size(); ++i) rs.meta.filename += (i ? "__" : "") + names[i];
     rs.categories = annotate ? (uint32_t)F : 1u;
     return rs;
+}
+
+}  // namespace hgah
+
+namespace hgah {
+
+// The iteration order of a std::unordered_set<uint64_t> (libstdc++) after inserting `keys` in order,
+// without building it: the same rehash policy object (std::__detail::_Prime_rehash_policy, whose
+// _M_need_rehash / _M_next_bkt are the library's own), std::hash<uint64_t> = identity and bucket =
+// key % bucket_count, the same node-list moves as _Hashtable::_M_insert_bucket_begin and
+// _M_rehash_aux(unique), on index arrays instead of heap nodes (no allocation per key, one int32 link
+// per key); a present key is found as _M_find_before_node finds it (its bucket's run) and not inserted.  tests/test_host.py
+// checks it against a real std::unordered_set (the oracle's or_load_sdk_text) on random key sets.
+std::vector<uint64_t> unordered_set_order(const uint64_t* keys, size_t n) {
+    constexpr int32_t NIL = -1, BB = -2;   // BB: _M_before_begin
+    std::vector<uint64_t> val;             // node i's key (nodes in insertion order)
+    val.reserve(n);
+    std::vector<int32_t> nxt;
+    nxt.reserve(n);
+    int32_t bb_next = NIL;
+    std::__detail::_Prime_rehash_policy pol;
+    size_t nb = 1;                          // _M_single_bucket
+    std::vector<int32_t> bkt(1, NIL);       // NIL: empty; BB or a node: the node before the bucket's first
+    auto next_of = [&](int32_t p) { return p == BB ? bb_next : nxt[(size_t)p]; };
+    auto set_next = [&](int32_t p, int32_t v) {
+        if (p == BB) bb_next = v;
+        else nxt[(size_t)p] = v;
+    };
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t key = keys[i];
+        size_t b = (size_t)(key % nb);
+        if (bkt[b] != NIL) {   // _M_find_before_node: the bucket's run, until the bucket changes
+            bool dup = false;
+            for (int32_t p = next_of(bkt[b]); p != NIL; p = nxt[(size_t)p]) {
+                const uint64_t v = val[(size_t)p];
+                if (v == key) { dup = true; break; }
+                if ((size_t)(v % nb) != b) break;
+            }
+            if (dup) continue;   // insert() of a present key: no change
+        }
+        const size_t m = val.size();
+        const auto r = pol._M_need_rehash(nb, m, 1);
+        if (r.first) {   // _M_rehash_aux(n, true_type)
+            const size_t nn = r.second;
+            std::vector<int32_t> nbk(nn, NIL);
+            int32_t p = bb_next;
+            bb_next = NIL;
+            size_t bbegin = 0;
+            while (p != NIL) {
+                const int32_t next = nxt[(size_t)p];
+                const size_t pb = (size_t)(val[(size_t)p] % nn);
+                if (nbk[pb] == NIL) {
+                    nxt[(size_t)p] = bb_next;
+                    bb_next = p;
+                    nbk[pb] = BB;
+                    if (nxt[(size_t)p] != NIL) nbk[bbegin] = p;
+                    bbegin = pb;
+                } else {
+                    nxt[(size_t)p] = next_of(nbk[pb]);
+                    set_next(nbk[pb], p);
+                }
+                p = next;
+            }
+            bkt.swap(nbk);
+            nb = nn;
+            b = (size_t)(key % nb);
+        }
+        const int32_t node = (int32_t)m;   // _M_insert_bucket_begin
+        val.push_back(key);
+        if (bkt[b] != NIL) {
+            nxt.push_back(next_of(bkt[b]));
+            set_next(bkt[b], node);
+        } else {
+            nxt.push_back(bb_next);
+            bb_next = node;
+            if (nxt[m] != NIL) bkt[(size_t)(val[(size_t)nxt[m]] % nb)] = node;
+            bkt[b] = BB;
+        }
+    }
+    std::vector<uint64_t> out;
+    out.reserve(val.size());
+    for (int32_t p = bb_next; p != NIL; p = nxt[(size_t)p]) out.push_back(val[(size_t)p]);
+    return out;
+}
+
+// load_text_file_kmers (src/read_clustering.cpp:18-33) without its per-line cost: the file mapped, its
+// lines ('\n'-split as std::getline, a CR kept in the line, no line after a final '\n') encoded on
+// host_threads() threads (line_canonical = KmerIterator(line, len).next_kmer()), then the KmerID order
+// of inserting them into a std::unordered_set in file order (unordered_set_order).  k = the last line's
+// length; a line longer than 32 throws, the first such line in file order deciding, as the reference's.
+std::vector<uint64_t> load_kmer_text(const std::string& path, int* k_out) {
+    MappedFile f(path);
+    std::vector<size_t> ends;   // line i = [ends[i-1] + 1, ends[i])
+    each_newline(f.p, 0, f.n, [&](size_t pos) { ends.push_back(pos); });
+    if (f.n && (ends.empty() || ends.back() != f.n - 1)) ends.push_back(f.n);   // last line without '\n'
+    const size_t L = ends.size();
+    std::vector<uint64_t> codes(L);
+    std::atomic<size_t> bad{SIZE_MAX};
+    const size_t CH = 1 << 16;
+    par_for((L + CH - 1) / CH, host_threads(), [&](size_t c) {
+        for (size_t i = c * CH; i < std::min(L, (c + 1) * CH); ++i) {
+            const size_t b = i ? ends[i - 1] + 1 : 0, e = ends[i];
+            if (e - b > 32) {
+                size_t cur = bad.load();
+                while (i < cur && !bad.compare_exchange_weak(cur, i)) {}
+                continue;
+            }
+            codes[i] = line_canonical(f.p + b, e - b);
+        }
+    });
+    if (bad.load() != SIZE_MAX) throw std::invalid_argument("Kmer size is too big");
+    *k_out = L ? (int)(ends[L - 1] - (L > 1 ? ends[L - 2] + 1 : 0)) : 0;
+    return unordered_set_order(codes.data(), codes.size());
 }
 
 }  // namespace hgah

@@ -161,6 +161,24 @@ int hgh_fmt_double(double v, char* buf, int cap) {
 // Reader threads of load_records / jf_stream (1 = the sequential readers).
 void hgh_set_threads(int n) { hgah::set_host_threads(n); }
 
+// load_text_file_kmers (read_clustering.cpp:18-33): canonical codes in KmerID order, k.
+int hgh_load_kmer_text(const char* path, uint64_t** keys, uint64_t* n, int* k) {
+    return guard([&] {
+        const std::vector<uint64_t> v = hgah::load_kmer_text(path, k);
+        *keys = dup(v.data(), v.size());
+        *n = v.size();
+    });
+}
+
+// The iteration order of a std::unordered_set<uint64_t> filled with keys[0..n) in order.
+int hgh_unordered_set_order(const uint64_t* keys, uint64_t n, uint64_t** out, uint64_t* m) {
+    return guard([&] {
+        const std::vector<uint64_t> v = hgah::unordered_set_order(keys, n);
+        *out = dup(v.data(), v.size());
+        *m = v.size();
+    });
+}
+
 // hll::HyperLogLog::estimate of 2^b registers (kmer_analysis.h).
 double hgh_hll_estimate(const uint8_t* regs, int b) { return hgah::hll_estimate(regs, b); }
 

@@ -99,6 +99,14 @@ void kmer_to_chars(uint64_t code, int k, char* out);
 // KmerIterator canonical code of a whole line (load_text_file_kmers, read_clustering.cpp:18-33).
 uint64_t line_canonical(const char* s, size_t len);
 
+// load_text_file_kmers (read_clustering.cpp:18-33): the SDK file's canonical codes in KmerID order (the
+// iteration order of the std::unordered_set the reference fills line by line,
+// ReadClusteringEngine.cpp:237-241); *k = the last line's length.  Lines encoded in parallel; the set's
+// order reproduced without building it (unordered_set_order).
+std::vector<uint64_t> load_kmer_text(const std::string& path, int* k);
+// The iteration order of a libstdc++ std::unordered_set<uint64_t> after inserting keys[0..n) in order.
+std::vector<uint64_t> unordered_set_order(const uint64_t* keys, size_t n);
+
 // "<reads>_<k>-mers_sorted" dump cache (JellyfishOccurrenceReader.cpp:19-24; written by
 // run_jellyfish.sh:5-6 as `jellyfish dump -c` + LC_ALL=C sort): one "KMER COUNT" line per
 // k-mer.  read_kmer_dump parses it like parse_line (JellyfishOccurrenceReader.cpp:9-14); the

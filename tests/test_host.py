@@ -5,6 +5,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import oracle
 import pyref_reader
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -146,3 +147,53 @@ def test_dump_writer_matches_restatement(tmp_path, n, threads):
     for i in idx:
         kstr = "".join("ACGT"[(int(keys[i]) >> (2 * (k - 1 - j))) & 3] for j in range(k))
         assert lines[i] == f"{kstr} {int(counts[i])}\n"
+
+
+@pytest.mark.parametrize("n,dup_frac,eol", [(0, 0.0, "\n"), (1, 0.0, "\n"), (12, 0.3, "\n"), (13, 0.0, ""),
+                                            (1000, 0.2, "\n"), (29_000, 0.1, "\r\n"), (300_000, 0.05, "\n")])
+def test_kmer_text_loader_matches_unordered_set(tmp_path, n, dup_frac, eol):
+    """categorization's SDK loader (host/fastio.cpp load_kmer_text: lines encoded in parallel, the KmerID
+    order computed by unordered_set_order instead of filling a std::unordered_set) against the oracle's
+    load_text_file_kmers (read_clustering.cpp:18-33 with a real std::unordered_set<uint64_t>): same codes
+    in the same iteration order (KmerIDs, ReadClusteringEngine.cpp:237-241), same k; sizes cross the
+    set's rehash points, lines repeat (also as reverse complements: the same canonical code), CRLF lines
+    (the CR is part of the line there), a last line without a newline."""
+    import hga as hga_mod
+    rng = np.random.default_rng(n)
+    k = 19 if eol != "\r\n" else 18   # (with the CR a line is k + 1 long)
+    comp = {"A": "T", "C": "G", "G": "C", "T": "A"}
+    lines = ["".join(rng.choice(list("ACGT"), k)) for _ in range(n)]
+    for i in range(n):
+        if i and rng.random() < dup_frac:
+            src = lines[int(rng.integers(0, i))]
+            lines[i] = src if rng.random() < 0.5 else "".join(comp[c] for c in reversed(src))
+    text = "".join(ln + (eol if eol else "\n") for ln in lines)
+    if not eol and text:
+        text = text[:-1]
+    p = tmp_path / "sdk.txt"
+    p.write_bytes(text.encode())
+    got, gk = hga_mod.load_kmer_text(str(p))
+    want, wk = oracle.load_sdk_text(text.encode())
+    assert np.array_equal(got, want) and gk == wk
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 11, 12, 13, 24, 100, 5000, 200_000])
+def test_unordered_set_order_matches_libstdcxx(n):
+    """unordered_set_order (an array simulation of libstdc++'s node list and rehashes) against a real
+    std::unordered_set<uint64_t>: the oracle's load_text_file_kmers fills one from lines written so that
+    each line's canonical code is the key itself (31-mers, the smaller strand), duplicates included."""
+    import hga as hga_mod
+    rng = np.random.default_rng(1000 + n)
+    k = 31
+    keys = rng.integers(0, 4 ** k, n, dtype=np.uint64)
+    # make every key its own canonical form (the smaller of it and its reverse complement)
+    lines, canon = [], []
+    for v in keys.tolist():
+        s = "".join("ACGT"[(v >> (2 * (k - 1 - j))) & 3] for j in range(k))
+        rc = "".join({"A": "T", "C": "G", "G": "C", "T": "A"}[c] for c in reversed(s))
+        lines.append(min(s, rc))
+    text = ("\n".join(lines) + "\n").encode() if lines else b""
+    want, _ = oracle.load_sdk_text(text)
+    codes = [int("".join(str("ACGT".index(c)) for c in ln), 4) for ln in lines]
+    got = hga_mod.unordered_set_order(np.array(codes, np.uint64))
+    assert np.array_equal(got, want)

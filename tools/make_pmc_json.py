@@ -25,15 +25,21 @@ def main(src, out_dir):
         # MI355X_MICROARCH.md establishes the x2 FETCH_SIZE correction for wide coalesced streaming
         # reads only; random gathers (table probes, index walks) are reported raw
         gather = base in GATHER
-        rd = row["read_bytes_corr"] / 2 if gather else row["read_bytes_corr"]
-        wr = row["write_bytes"]
+        main = "main_read_bytes_corr" in row
+        rcorr = row["main_read_bytes_corr"] if main else row["read_bytes_corr"]
+        rd = rcorr / 2 if gather else rcorr
+        wr = row["main_write_bytes"] if main else row["write_bytes"]
         rec = {"kernel": k, "hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
-               "fetch_size_raw_bytes": int(row["read_bytes_corr"] / 2), "read_access": "gather" if gather else "stream",
+               "fetch_size_raw_bytes": int(rcorr / 2), "read_access": "gather" if gather else "stream",
                "ms_median": row["ms_median"], "dispatches": row["dispatches"],
+               "main_dispatches": row.get("main_dispatches", row["dispatches"]),
+               "mean_bytes_all_dispatches": int((row["read_bytes_corr"] / 2 if gather else row["read_bytes_corr"]) +
+                                                row["write_bytes"]),
                "note": ("FETCH_SIZE raw (random gathers: the x2 correction is not established for them)" if gather else
                         "FETCH_SIZE x2 (gfx950 wide streaming-read correction)") +
-                       " + WRITE_SIZE, KB->B, mean over dispatches; separate --pmc passes over tools/kprof.py "
-                       "(MI355X_MICROARCH.md HBM section)"}
+                       " + WRITE_SIZE, KB->B, mean over the main launches (those moving >= half the bytes of the "
+                       "heaviest; a label's small spill launches are in mean_bytes_all_dispatches); separate --pmc "
+                       "passes over tools/kprof.py (MI355X_MICROARCH.md HBM section)"}
         name = f"pmc_{base}.json"
         p = os.path.join(out_dir, name)
         # keep the heaviest instantiation when a template kernel has several

@@ -31,7 +31,8 @@ def main(dirs, out=None):
     dur = collections.defaultdict(list)
     for d in dirs:
         for f in glob.glob(f"{d}/*counter_collection.csv"):
-            for r in csv.DictReader(open(f)):
+            rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Dispatch_Id"]))
+            for r in rows:   # values in dispatch order: the n-th dispatch of a kernel is the same launch in every pass
                 k = kname(r["Kernel_Name"])
                 agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for f in glob.glob(f"{d}/*kernel_trace.csv"):
@@ -54,6 +55,16 @@ def main(dirs, out=None):
         row["dispatches"] = len(ds)
         row["read_bytes_corr"] = 2 * row["FETCH_SIZE"] * 1024
         row["write_bytes"] = row["WRITE_SIZE"] * 1024
+        # the main launches: a kernel label can cover unlike launches (kc_rebin's main launch and its small
+        # spill-block launch); the mean above mixes them, so the launches moving at least half the bytes
+        # of the heaviest one are also averaged on their own (pmc_<kernel>.json reports those)
+        fs, ws = agg[k].get("FETCH_SIZE", []), agg[k].get("WRITE_SIZE", [])
+        if fs and len(fs) == len(ws):
+            tot = [a + b for a, b in zip(fs, ws)]
+            main_i = [i for i, t in enumerate(tot) if t >= 0.5 * max(tot)]
+            row["main_dispatches"] = len(main_i)
+            row["main_read_bytes_corr"] = 2 * 1024 * sum(fs[i] for i in main_i) / len(main_i)
+            row["main_write_bytes"] = 1024 * sum(ws[i] for i in main_i) / len(main_i)
         res[k] = row
         print(k[:26].ljust(26), f"{med:8.3f}", *[f"{row[c]:11.3g}" for c in cols])
     if out:
