@@ -2109,7 +2109,7 @@ __global__ void __launch_bounds__(256) kc_bx_wsort(uint64_t* __restrict__ keys, 
                                                    const uint32_t* __restrict__ dbase, int bits) {
     const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t len = hist[d], st = dbase[d];
-    if (len <= 1) return;
+    if (len <= 1 || len > BX_MAX) return;   // (larger segments: kc_bx_lsort)
     if (bits - 12 + 1 <= 32) {
         if (len <= 64) bx_sort_seg32<1>(keys, st, len, lane, bits, d);
         else if (len <= 256) bx_sort_seg32<4>(keys, st, len, lane, bits, d);
@@ -2121,6 +2121,50 @@ __global__ void __launch_bounds__(256) kc_bx_wsort(uint64_t* __restrict__ keys, 
     else if (len <= 256) bx_sort_seg<4>(keys, st, len, lane, bits);
     else if (len <= 512) bx_sort_seg<8>(keys, st, len, lane, bits);
     else bx_sort_seg<16>(keys, st, len, lane, bits);   // len <= BX_MAX (checked by the host)
+}
+
+// Large exports (a C4 rank shard's ~50 M keys: ~12 K a digit, ~25 K in the lowest digits, canonical
+// codes being twice as dense there): every digit segment of BX_MAX < len <= cap keys sorted by one
+// 1024-thread workgroup in LDS (stable LSD passes, kmer_dev.hpp lds_lsd_sort_t).  With the code bits
+// below the digit and the flag in 32 bits (k <= 21) the keys are sorted as u32 (low code bits << 1 |
+// flag, by bits 1.., the digit restored on the way out): 32 K keys fit the LDS; else as u64 by the low
+// code bits (the flag in bit 63 lies above them; codes are unique), 16 K keys.  With kc_bx_scatter this
+// replaces the global LSD radix sort of the low bits + the MSD pass (5-6 global passes over the export)
+// by one scatter and one LDS pass.
+constexpr uint32_t BX_CAP32 = SS_T * 2 * SS_I;
+template <bool U32>
+__global__ void __launch_bounds__(SS_T) kc_bx_lsort(uint64_t* __restrict__ keys, const uint32_t* __restrict__ hist,
+                                                    const uint32_t* __restrict__ dbase, int bits) {
+    using T = std::conditional_t<U32, uint32_t, uint64_t>;
+    constexpr int I = U32 ? 2 * SS_I : SS_I;
+    __shared__ T sk[SS_T * I];
+    __shared__ uint32_t wcnt[SS_T / 64][256];
+    __shared__ uint32_t ws[SS_T / 64 + 1];
+    const uint32_t d = blockIdx.x;
+    const uint32_t cnt = hist[d], start = dbase[d];
+    if (cnt <= BX_MAX || cnt > (uint32_t)(SS_T * I)) return;   // (the host checked the cap for every digit)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lb = bits - 12;   // code bits below the digit
+    const uint64_t lm = (1ull << lb) - 1;
+    T key[I];
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+        const uint32_t i = (uint32_t)wave * (I * 64) + (uint32_t)j * 64 + lane;
+        const uint64_t k = i < cnt ? keys[(uint64_t)start + i] : 0ull;
+        if constexpr (U32) key[j] = (uint32_t)(((k & lm) << 1) | (k >> 63));
+        else key[j] = k;
+    }
+    if constexpr (U32) lds_lsd_sort_t<uint32_t, I>(key, cnt, 1, lb, sk, wcnt, ws);
+    else lds_lsd_sort_t<uint64_t, I>(key, cnt, 0, lb, sk, wcnt, ws);
+    const uint64_t hi = (uint64_t)d << lb;
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+        const uint32_t i = (uint32_t)wave * (I * 64) + (uint32_t)j * 64 + lane;
+        if (i < cnt) {
+            if constexpr (U32) keys[(uint64_t)start + i] = hi | (uint64_t)(key[j] >> 1) | ((uint64_t)(key[j] & 1u) << 63);
+            else keys[(uint64_t)start + i] = key[j];
+        }
+    }
 }
 
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
@@ -2750,8 +2794,11 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
     if (before_sync) (*before_sync)(stat);
     c->sync();
     const uint64_t n = hs[0];
-    const bool bx = msd && n > 1 && hs[2] <= BX_MAX && !std::getenv("HGA_BX_OFF");
-    if (bx) {   // bucketed export sort: digit segments straight from the workgroup regions, one wave each
+    // bucketed export sort while every 12-bit digit segment fits one workgroup's LDS sort (C2: all of them
+    // fit one wave's registers; a C4 rank shard's ~12 K-key segments take kc_bx_lsort)
+    const bool u32seg = bits - 12 + 1 <= 32;
+    const bool bx = msd && n > 1 && hs[2] <= (u32seg ? (uint64_t)BX_CAP32 : (uint64_t)SS_CAP) && !std::getenv("HGA_BX_OFF");
+    if (bx) {   // bucketed export sort: digit segments straight from the workgroup regions
         c->launch("bx_colscan", [&] {
             hipLaunchKernelGGL(kc_bx_colscan, dim3(SEL_HB / 16), dim3(256), 0, c->stream, (const uint32_t*)dhist_rows,
                                grid, (const uint32_t*)bx_dbase, bx_off);
@@ -2765,6 +2812,17 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
                                (const uint32_t*)bx_dbase, bits);
         });
         c->check_launch("kc_bx_wsort");
+        if (hs[2] > BX_MAX) {
+            c->launch("radix_segsort", [&] {
+                if (u32seg)
+                    hipLaunchKernelGGL(kc_bx_lsort<true>, dim3(SEL_HB), dim3(SS_T), 0, c->stream, out,
+                                       (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits);
+                else
+                    hipLaunchKernelGGL(kc_bx_lsort<false>, dim3(SEL_HB), dim3(SS_T), 0, c->stream, out,
+                                       (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits);
+            });
+            c->check_launch("kc_bx_lsort");
+        }
     } else if (msd && n > 1) {
         // compaction, then the MSD pass: digit = (code >> shift) - dbase over the occupied 12-bit bins
         // [lo, hi], <= 256 digits (kc_sel_span: span into stat + 4, the 256 digit counts into dig256)

@@ -510,4 +510,78 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* ws, ui
     return r;
 }
 
+// ---- LDS segment sort (the export sort: sort.hip ss_segsort, count.hip kc_bx_lsort) ----
+constexpr int SS_T = 1024, SS_I = 16, SS_CAP = SS_T * SS_I;
+
+// One segment of cnt <= SS_T * I keys (loaded by the caller into key[], items in (wave, j, lane) order)
+// sorted in LDS by bits [lo, lo + nbits) of the key: stable LSD passes over 8-bit digits, ballot-matched
+// ranks inside each wave, waves in order.  T = uint64_t (I = SS_I) or uint32_t (I = 2 SS_I: the same LDS
+// holds twice the keys).
+template <class T, int I>
+__device__ __forceinline__ void lds_lsd_sort_t(T (&key)[I], uint32_t cnt, int lo, int nbits, T* sk,
+                                               uint32_t (*wcnt)[256], uint32_t* ws) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int sh = lo; sh < lo + nbits; sh += 8) {
+        const uint32_t dm = lo + nbits - sh >= 8 ? 255u : ((1u << (lo + nbits - sh)) - 1u);
+        for (int i = tid; i < (SS_T / 64) * 256; i += SS_T) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t dr[I];   // rank << 9 | digit (256: no item) — one register per item
+#pragma unroll
+        for (int j = 0; j < I; ++j) {   // stable rank inside the wave, items in (j, lane) order
+            const uint32_t i0 = (uint32_t)wave * (I * 64) + (uint32_t)j * 64;   // wave-uniform
+            const uint32_t i = i0 + lane;
+            const bool ok = i < cnt;
+            const uint32_t d = ok ? ((uint32_t)(key[j] >> sh) & dm) : 256u;
+            dr[j] = d;
+            if (i0 >= cnt) continue;   // no item of this row: skip its ballots
+            uint64_t m = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            uint32_t before = 0;
+            if (ok) before = wcnt[wave][d];
+            dr[j] = d | (before + (uint32_t)__popcll(m & lt)) << 9;
+            if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
+            wave_lds_sync();
+        }
+        __syncthreads();
+        {   // digit starts, then each wave's start inside its digit (waves in order: stable)
+            const uint32_t d = (uint32_t)tid & 255u;
+            uint32_t tot_d = 0;
+            if (tid < 256)
+                for (int w = 0; w < SS_T / 64; ++w) tot_d += wcnt[w][d];
+            uint32_t tt;
+            const uint32_t exd = block_excl_scan<SS_T>(tid < 256 ? tot_d : 0u, ws, &tt);
+            if (tid < 256) {
+                uint32_t o = exd;
+                for (int w = 0; w < SS_T / 64; ++w) {
+                    const uint32_t c = wcnt[w][d];
+                    wcnt[w][d] = o;
+                    o += c;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < I; ++j)
+            if ((dr[j] & 511u) < 256u) sk[wcnt[wave][dr[j] & 511u] + (dr[j] >> 9)] = key[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < I; ++j) {
+            const uint32_t i = (uint32_t)wave * (I * 64) + (uint32_t)j * 64 + lane;
+            if (i < cnt) key[j] = sk[i];
+        }
+        __syncthreads();
+    }
+}
+// The u64 form over the low bits_low bits (sort.hip ss_segsort).
+__device__ __forceinline__ void lds_lsd_sort(uint64_t (&key)[SS_I], uint32_t cnt, int bits_low, uint64_t* sk,
+                                             uint32_t (*wcnt)[256], uint32_t* ws) {
+    lds_lsd_sort_t<uint64_t, SS_I>(key, cnt, 0, bits_low, sk, wcnt, ws);
+}
+
 }  // namespace hga

@@ -303,72 +303,7 @@ __global__ void __launch_bounds__(RS_T) rs_onesweep(const K* __restrict__ kin, c
 // sorts in LDS by the remaining bits (stable LSD passes over 8-bit digits: ballot-matched ranks
 // inside each wave, waves in order), instead of ceil(2k/8) global passes.  Segments larger than
 // the LDS (rare: a prefix holding > 16384 keys) are sorted by the global radix sort.
-constexpr int SS_T = 1024, SS_I = 16, SS_CAP = SS_T * SS_I;
-
-// One segment of cnt <= SS_CAP keys (loaded by the caller into key[], items in (wave, j, lane)
-// order) sorted in LDS by the low bits_low bits: stable LSD passes over 8-bit digits, ballot-matched
-// ranks inside each wave, waves in order.
-__device__ __forceinline__ void lds_lsd_sort(uint64_t (&key)[SS_I], uint32_t cnt, int bits_low, uint64_t* sk,
-                                             uint32_t (*wcnt)[256], uint32_t* ws) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    for (int sh = 0; sh < bits_low; sh += 8) {
-        const uint32_t dm = bits_low - sh >= 8 ? 255u : ((1u << (bits_low - sh)) - 1u);
-        for (int i = tid; i < (SS_T / 64) * 256; i += SS_T) (&wcnt[0][0])[i] = 0;
-        __syncthreads();
-        uint32_t dig[SS_I], rank[SS_I];
-#pragma unroll
-        for (int j = 0; j < SS_I; ++j) {   // stable rank inside the wave, items in (j, lane) order
-            const uint32_t i0 = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64;   // wave-uniform
-            const uint32_t i = i0 + lane;
-            const bool ok = i < cnt;
-            const uint32_t d = ok ? ((uint32_t)(key[j] >> sh) & dm) : 256u;
-            dig[j] = d;
-            rank[j] = 0;
-            if (i0 >= cnt) continue;   // no item of this row: skip its ballots
-            uint64_t m = __ballot(ok);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const bool bit = (d >> b) & 1u;
-                const uint64_t bb = __ballot(bit);
-                m &= bit ? bb : ~bb;
-            }
-            uint32_t before = 0;
-            if (ok) before = wcnt[wave][d];
-            rank[j] = before + (uint32_t)__popcll(m & lt);
-            if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
-            wave_lds_sync();
-        }
-        __syncthreads();
-        {   // digit starts, then each wave's start inside its digit (waves in order: stable)
-            const uint32_t d = (uint32_t)tid & 255u;
-            uint32_t tot_d = 0;
-            if (tid < 256)
-                for (int w = 0; w < SS_T / 64; ++w) tot_d += wcnt[w][d];
-            uint32_t tt;
-            const uint32_t exd = block_excl_scan<SS_T>(tid < 256 ? tot_d : 0u, ws, &tt);
-            if (tid < 256) {
-                uint32_t o = exd;
-                for (int w = 0; w < SS_T / 64; ++w) {
-                    const uint32_t c = wcnt[w][d];
-                    wcnt[w][d] = o;
-                    o += c;
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < SS_I; ++j)
-            if (dig[j] < 256u) sk[wcnt[wave][dig[j]] + rank[j]] = key[j];
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < SS_I; ++j) {
-            const uint32_t i = (uint32_t)wave * (SS_I * 64) + (uint32_t)j * 64 + lane;
-            if (i < cnt) key[j] = sk[i];
-        }
-        __syncthreads();
-    }
-}
+// (SS_T / SS_I / SS_CAP and lds_lsd_sort live in kmer_dev.hpp: count.hip sorts export segments with them too)
 
 __global__ void __launch_bounds__(SS_T) ss_segsort(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
                                                    const uint32_t* __restrict__ ghist, int bits_low) {

@@ -166,11 +166,14 @@ int main(int argc, char* argv[]) {
 
     if (engine_debug) {   // ReadClusteringEngine.cpp:285-297
         uint32_t discriminative = 0, total = 0;
-        for (uint64_t id = 0; id < sz.n_sdk; ++id) {
-            std::set<int32_t> cats;
-            for (uint64_t j = kci_ptr[id]; j < kci_ptr[id + 1]; ++j) cats.insert(rs.category[kci_read[j] - 1]);
-            if (cats.size() == 1) ++discriminative;
-            if (!cats.empty()) ++total;
+        for (uint64_t id = 0; id < sz.n_sdk; ++id) {   // (the set of categories has one element iff all agree)
+            const uint64_t a = kci_ptr[id], b = kci_ptr[id + 1];
+            if (a == b) continue;
+            const int32_t c0 = rs.category[kci_read[a] - 1];
+            bool one = true;
+            for (uint64_t j = a + 1; j < b && one; ++j) one = rs.category[kci_read[j] - 1] == c0;
+            discriminative += one ? 1u : 0u;
+            ++total;
         }
         std::cout << discriminative << " out of " << total << " kmers are discriminative \n";
         tm.mark("discriminative_check");

@@ -102,3 +102,28 @@ def test_export_sort_few_big_segments(gpu_ctx):
     want = keys[(counts >= 10) & (counts <= 25)]
     assert np.array_equal(sel, want)
     assert nd == len(want) and np.all(flags == 1)
+
+
+@pytest.mark.parametrize("k,hot", [(19, 0), (19, 30_000), (19, 40_000), (27, 0), (27, 15_000), (27, 20_000)])
+def test_export_sort_workgroup_segments(gpu_ctx, k, hot):
+    """~4.5 M exported keys spread over the code space (~1.1 K per 12-bit digit, many past one wave's
+    BX_MAX = 1024): the bucketed export sort with workgroup LDS sorts of the larger digit segments
+    (count.hip kc_bx_lsort, the C4-shard-sized path: u32 keys up to 32768 a segment at k <= 21, u64 up to
+    16384 above); `hot` keys packed into one digit — within the cap, or past it (the MSD + global-radix
+    path)."""
+    rng = np.random.default_rng(hot + 3 + k)
+    lb = 2 * k - 12
+    keys = rng.integers(0, 1 << (2 * k), 6_000_000, dtype=np.uint64)
+    if hot:
+        keys = np.concatenate([keys, rng.integers(901 << lb, (901 << lb) + (1 << lb), hot, dtype=np.uint64)])
+    keys = np.unique(keys)
+    counts = rng.integers(10, 30, len(keys), dtype=np.uint32)
+    if hot:   # the hot digit's keys all selected
+        counts[(keys >> np.uint64(lb)) == 901] = 15
+    gpu_ctx.count_begin(k, 1)
+    gpu_ctx.count_add_rows(0, keys, counts)
+    gpu_ctx.count_run(2)
+    sel, flags, nd = gpu_ctx.select(10, 25)
+    want = keys[(counts >= 10) & (counts <= 25)]
+    assert np.array_equal(sel, want)
+    assert nd == len(want) and np.all(flags == 1)
