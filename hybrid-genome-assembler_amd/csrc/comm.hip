@@ -859,6 +859,7 @@ void lookup_gather(hga_ctx* c) {
     h2d(L.first_pos, g.first_pos.data(), Ug * 4);
     h2d(L.kci_ptr, g.kci_ptr.data(), (K + 1) * 8);
     h2d(L.kci_val, g.kci_read.data(), Hg * 4);
+    ++L.kci_epoch;
     c->sync();
     L.loc_n_reads = L.n_reads;
     L.loc_first_read_id = L.first_read_id;

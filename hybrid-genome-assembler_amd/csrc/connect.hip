@@ -73,7 +73,38 @@ struct CnIn {
     const uint64_t* kci_ptr;   // per KmerID, into kci
     const uint32_t* kci;       // read indices per KmerID, sorted, with duplicates
     uint32_t min_kmers, min_score;
+    const uint32_t* slots;     // cn_wave: per KmerID one 128-B slot (cn_slots), or null
 };
+
+// kmer_component_index as one 128-B slot (one L2 line) per KmerID for cn_wave: word 0 = the list's
+// length when it fits (<= SLOT_W - 1 read indices, in words 1..), else SLOT_LONG with the length in
+// word 1 and the list's kci offset in words 2-3.  A hit's list then costs one aligned line fetch with
+// no kci_ptr read before it (the pointer read and the list's line straddles made cn_wave fetch ~2x
+// its model bytes), and the slot header arrives with the entries.
+constexpr uint32_t SLOT_W = 32, SLOT_LONG = 0xFFFFFFFFu;
+__global__ void __launch_bounds__(256) cn_slots(const uint64_t* __restrict__ kci_ptr, const uint32_t* __restrict__ kci,
+                                                uint64_t K, uint32_t* __restrict__ slots) {
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= K) return;
+    const uint64_t l0 = kci_ptr[k], len = kci_ptr[k + 1] - l0;
+    uint32_t w[SLOT_W];
+#pragma unroll
+    for (uint32_t i = 0; i < SLOT_W; ++i) w[i] = 0;
+    if (len < SLOT_W) {
+        w[0] = (uint32_t)len;
+#pragma unroll
+        for (uint32_t i = 1; i < SLOT_W; ++i)
+            if (i <= len) w[i] = kci[l0 + i - 1];
+    } else {
+        w[0] = SLOT_LONG;
+        w[1] = (uint32_t)len;
+        w[2] = (uint32_t)l0;
+        w[3] = (uint32_t)(l0 >> 32);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(slots + k * SLOT_W);
+#pragma unroll
+    for (uint32_t i = 0; i < SLOT_W / 4; ++i) dst[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
 
 // Output: CN_R regions of rcap entries, each with its own cursor in its own 128-B line, so the
 // per-pivot reservations spread over CN_R addresses instead of serialising on one.  Pivot p
@@ -437,7 +468,7 @@ constexpr uint32_t CNW_GRAB = HGA_CNW_GRAB;   // pivots per work-counter atomic
 constexpr uint32_t CNW_Q = 128;   // per-wave queue of a window's candidates not found at their home slot
 struct CnWaveLds {
     uint64_t tab[CNW_CAP];
-    uint64_t base[64];             // per hit of the chunk: kci offset of its list minus its first pair index
+    uint64_t base[64];             // per hit of the chunk: byte address of its list minus 4 x its first pair index
     uint64_t own[CNW_W / 8];       // owner map, one byte per pair of the window
     uint32_t q[CNW_Q];
     uint32_t fill, ovf;
@@ -504,17 +535,31 @@ __global__ void __launch_bounds__(64 * CNW_WAVES, HGA_CNW_MINW) cn_wave(CnIn in,
         for (uint64_t cb = b; cb < e && ok; cb += 64) {
             const uint64_t i = cb + lane;
             uint32_t len = 0;
-            uint64_t l0 = 0;
+            uint64_t first = 0;   // byte address of the hit's first read index
             if (i < e) {
                 const uint32_t kid = in.skid[i];
-                l0 = in.kci_ptr[kid];
-                len = (uint32_t)(in.kci_ptr[kid + 1] - l0);
+                if (in.slots) {   // one 128-B slot: header and (short) list in the same line
+                    const uint32_t* sl = in.slots + (uint64_t)kid * SLOT_W;
+                    const uint4 h = *reinterpret_cast<const uint4*>(sl);
+                    if (h.x != SLOT_LONG) {
+                        len = h.x;
+                        first = reinterpret_cast<uint64_t>(sl + 1);
+                    } else {
+                        len = h.y;
+                        first = reinterpret_cast<uint64_t>(in.kci + ((uint64_t)h.z | ((uint64_t)h.w << 32)));
+                    }
+                } else {
+                    const uint64_t l0 = in.kci_ptr[kid];
+                    len = (uint32_t)(in.kci_ptr[kid + 1] - l0);
+                    first = reinterpret_cast<uint64_t>(in.kci + l0);
+                }
             }
-            // pairs of the chunk numbered 0..T: hit h owns [o, o + len); pair j of h reads kci[l0 + j - o]
+            // pairs of the chunk numbered 0..T: hit h owns [o, o + len); pair j of h reads the word at
+            // first + 4 (j - o)
             const uint32_t inc = wave_scan_add_dpp(len);
             const uint32_t o = inc - len;
             const uint32_t T = wave_lane(inc, 63);
-            W.base[lane] = l0 - o;
+            W.base[lane] = first - 4ull * o;
             for (uint32_t w0 = 0; w0 < T && ok; w0 += CNW_W) {
                 // owner map of pairs [w0, w0 + CNW_W): segment starts, then a max-scan (bytes within a
                 // lane's u64, then across lanes)
@@ -544,7 +589,7 @@ __global__ void __launch_bounds__(64 * CNW_WAVES, HGA_CNW_MINW) cn_wave(CnIn in,
                 for (int u = 0; u < CNW_U; ++u) {
                     const uint32_t j = w0 + lane + 64 * u;
                     cand[u] = CN_EMPTY;
-                    if (j < T) cand[u] = in.kci[W.base[own8[j - w0]] + j];
+                    if (j < T) cand[u] = *reinterpret_cast<const uint32_t*>(W.base[own8[j - w0]] + 4ull * j);
                 }
                 // a candidate already at its home slot (most walks repeat a candidate) is one count add;
                 // the rest go through the wave's queue and are inserted with every lane busy (a lane's own
@@ -966,8 +1011,21 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
         HGA_HIP(hipMemcpyAsync(S.cat.ensure(nr * 4), categories, nr * 4, hipMemcpyHostToDevice, c->stream));
         d_cat = S.cat.as<int32_t>();
     }
+    const uint32_t* slots = nullptr;
+    if (!std::getenv("HGA_CN_NO_SLOTS") && L.n_sdk) {   // cn_wave's list slots, once per index
+        if (S.slots_epoch != L.kci_epoch) {
+            uint32_t* sl = static_cast<uint32_t*>(S.slots.ensure((uint64_t)L.n_sdk * SLOT_W * 4));
+            c->launch("cn_slots", [&] {
+                hipLaunchKernelGGL(cn_slots, dim3(cn_blocks(L.n_sdk, 256)), dim3(256), 0, c->stream,
+                                   L.kci_ptr.as<uint64_t>(), L.kci_val.as<uint32_t>(), (uint64_t)L.n_sdk, sl);
+            });
+            c->check_launch("cn_slots");
+            S.slots_epoch = L.kci_epoch;
+        }
+        slots = S.slots.as<uint32_t>();
+    }
     CnIn in{L.hit_ptr.as<uint64_t>(), L.s_val2.as<uint32_t>(), L.kci_ptr.as<uint64_t>(), L.kci_val.as<uint32_t>(),
-            min_kmers, ms};
+            min_kmers, ms, slots};
     const size_t ctr_bytes = 64 + (size_t)CN_R * CN_RSTRIDE * 8;
     auto* ctr = static_cast<unsigned long long*>(S.ctr.ensure(ctr_bytes));
     unsigned long long* rcur = ctr + 8;

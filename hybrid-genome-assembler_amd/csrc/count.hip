@@ -2124,25 +2124,25 @@ __global__ void __launch_bounds__(256) kc_bx_wsort(uint64_t* __restrict__ keys, 
 }
 
 // Large exports (a C4 rank shard's ~50 M keys: ~12 K a digit, ~25 K in the lowest digits, canonical
-// codes being twice as dense there): every digit segment of BX_MAX < len <= cap keys sorted by one
-// 1024-thread workgroup in LDS (stable LSD passes, kmer_dev.hpp lds_lsd_sort_t).  With the code bits
-// below the digit and the flag in 32 bits (k <= 21) the keys are sorted as u32 (low code bits << 1 |
-// flag, by bits 1.., the digit restored on the way out): 32 K keys fit the LDS; else as u64 by the low
-// code bits (the flag in bit 63 lies above them; codes are unique), 16 K keys.  With kc_bx_scatter this
-// replaces the global LSD radix sort of the low bits + the MSD pass (5-6 global passes over the export)
-// by one scatter and one LDS pass.
-constexpr uint32_t BX_CAP32 = SS_T * 2 * SS_I;
-template <bool U32>
-__global__ void __launch_bounds__(SS_T) kc_bx_lsort(uint64_t* __restrict__ keys, const uint32_t* __restrict__ hist,
-                                                    const uint32_t* __restrict__ dbase, int bits) {
+// codes being twice as dense there): every digit segment of more than BX_MAX keys is sorted by one
+// workgroup in LDS (stable LSD passes, kmer_dev.hpp lds_lsd_sort_t).  With the code bits below the digit
+// and the flag in 32 bits (k <= 21) the keys are sorted as u32 (low code bits << 1 | flag, by bits 1..,
+// the digit restored on the way out): segments up to 16 K keys by 512 threads over 9-bit digits (80 KB
+// of LDS: two workgroups a CU; 3 passes for k = 19), up to 32 K by 1024 threads over 8-bit digits;
+// else as u64 by the low code bits (the flag in bit 63 lies above them; codes are unique), 16 K.  With
+// kc_bx_scatter this replaces the global LSD radix sort of the low bits + the MSD pass (5-6 global
+// passes over the export) by one scatter and one LDS pass.
+constexpr uint32_t BX_CAP32 = SS_T * 2 * SS_I;   // 32 K u32 keys
+template <bool U32, int NT, int I, int DB>
+__global__ void __launch_bounds__(NT) kc_bx_lsort(uint64_t* __restrict__ keys, const uint32_t* __restrict__ hist,
+                                                  const uint32_t* __restrict__ dbase, int bits, uint32_t min_len) {
     using T = std::conditional_t<U32, uint32_t, uint64_t>;
-    constexpr int I = U32 ? 2 * SS_I : SS_I;
-    __shared__ T sk[SS_T * I];
-    __shared__ uint32_t wcnt[SS_T / 64][256];
-    __shared__ uint32_t ws[SS_T / 64 + 1];
+    __shared__ T sk[NT * I];
+    __shared__ uint32_t wcnt[NT / 64][1 << DB];
+    __shared__ uint32_t ws[NT / 64 + 1];
     const uint32_t d = blockIdx.x;
     const uint32_t cnt = hist[d], start = dbase[d];
-    if (cnt <= BX_MAX || cnt > (uint32_t)(SS_T * I)) return;   // (the host checked the cap for every digit)
+    if (cnt <= min_len || cnt > (uint32_t)(NT * I)) return;   // (another launch has it)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lb = bits - 12;   // code bits below the digit
     const uint64_t lm = (1ull << lb) - 1;
@@ -2154,8 +2154,8 @@ __global__ void __launch_bounds__(SS_T) kc_bx_lsort(uint64_t* __restrict__ keys,
         if constexpr (U32) key[j] = (uint32_t)(((k & lm) << 1) | (k >> 63));
         else key[j] = k;
     }
-    if constexpr (U32) lds_lsd_sort_t<uint32_t, I>(key, cnt, 1, lb, sk, wcnt, ws);
-    else lds_lsd_sort_t<uint64_t, I>(key, cnt, 0, lb, sk, wcnt, ws);
+    if constexpr (U32) lds_lsd_sort_t<uint32_t, I, NT, DB>(key, cnt, 1, lb, sk, wcnt, ws);
+    else lds_lsd_sort_t<uint64_t, I, NT, DB>(key, cnt, 0, lb, sk, wcnt, ws);
     const uint64_t hi = (uint64_t)d << lb;
 #pragma unroll
     for (int j = 0; j < I; ++j) {
@@ -2814,12 +2814,16 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
         c->check_launch("kc_bx_wsort");
         if (hs[2] > BX_MAX) {
             c->launch("radix_segsort", [&] {
-                if (u32seg)
-                    hipLaunchKernelGGL(kc_bx_lsort<true>, dim3(SEL_HB), dim3(SS_T), 0, c->stream, out,
-                                       (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits);
-                else
-                    hipLaunchKernelGGL(kc_bx_lsort<false>, dim3(SEL_HB), dim3(SS_T), 0, c->stream, out,
-                                       (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits);
+                if (u32seg) {
+                    hipLaunchKernelGGL((kc_bx_lsort<true, 512, 32, 9>), dim3(SEL_HB), dim3(512), 0, c->stream, out,
+                                       (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits, BX_MAX);
+                    if (hs[2] > 16384u)
+                        hipLaunchKernelGGL((kc_bx_lsort<true, 1024, 32, 8>), dim3(SEL_HB), dim3(1024), 0, c->stream,
+                                           out, (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits, 16384u);
+                } else {
+                    hipLaunchKernelGGL((kc_bx_lsort<false, SS_T, SS_I, 8>), dim3(SEL_HB), dim3(SS_T), 0, c->stream,
+                                       out, (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits, BX_MAX);
+                }
             });
             c->check_launch("kc_bx_lsort");
         }

@@ -180,6 +180,7 @@ struct CountState {
 
 struct LookupState {
     bool loaded = false, have_reads = false, ran = false;
+    uint64_t kci_epoch = 0;   // bumped whenever kci_ptr / kci_val change (connect.hip's list slots follow it)
     bool packed_ok = false;   // packed / valid / starts / word_read hold the current reads (lookup_pack)
     int k = 0, km = 0;
     uint32_t n_sdk = 0;
@@ -204,6 +205,9 @@ struct LookupState {
 struct ConnState {
     bool ready = false;
     uint64_t n = 0, cap_hint = 0;
+    // cn_wave's per-KmerID list slots (connect.hip cn_slots), built for the index of kci_epoch
+    DevBuf slots;
+    uint64_t slots_epoch = ~0ull;
     DevBuf piv, cat, ctr, rpre, ovf, ovf2, big, x, y, s, gk, gv, key, idx, skey, pos, ox, oy, os, og, pst, pcnt, sk2, sv2,
         lst;
 };

@@ -513,52 +513,54 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* ws, ui
 // ---- LDS segment sort (the export sort: sort.hip ss_segsort, count.hip kc_bx_lsort) ----
 constexpr int SS_T = 1024, SS_I = 16, SS_CAP = SS_T * SS_I;
 
-// One segment of cnt <= SS_T * I keys (loaded by the caller into key[], items in (wave, j, lane) order)
-// sorted in LDS by bits [lo, lo + nbits) of the key: stable LSD passes over 8-bit digits, ballot-matched
-// ranks inside each wave, waves in order.  T = uint64_t (I = SS_I) or uint32_t (I = 2 SS_I: the same LDS
-// holds twice the keys).
-template <class T, int I>
+// One segment of cnt <= NT * I keys (loaded by the caller into key[], items in (wave, j, lane) order)
+// sorted in LDS by bits [lo, lo + nbits) of the key by NT threads: stable LSD passes over DB-bit digits
+// (DB <= 9, 2^DB <= NT), ballot-matched ranks inside each wave, waves in order.  T = uint64_t or
+// uint32_t (u32 keys: the same LDS holds twice as many); wcnt holds [NT / 64][2^DB] counters.
+template <class T, int I, int NT = SS_T, int DB = 8>
 __device__ __forceinline__ void lds_lsd_sort_t(T (&key)[I], uint32_t cnt, int lo, int nbits, T* sk,
-                                               uint32_t (*wcnt)[256], uint32_t* ws) {
+                                               uint32_t (*wcnt)[1 << DB], uint32_t* ws) {
+    static_assert(DB <= 9 && (1 << DB) <= NT, "digit counters: one per thread in the scan");
+    constexpr uint32_t ND = 1u << DB, NONE = ND;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
-    for (int sh = lo; sh < lo + nbits; sh += 8) {
-        const uint32_t dm = lo + nbits - sh >= 8 ? 255u : ((1u << (lo + nbits - sh)) - 1u);
-        for (int i = tid; i < (SS_T / 64) * 256; i += SS_T) (&wcnt[0][0])[i] = 0;
+    for (int sh = lo; sh < lo + nbits; sh += DB) {
+        const uint32_t dm = lo + nbits - sh >= DB ? ND - 1 : ((1u << (lo + nbits - sh)) - 1u);
+        for (int i = tid; i < (NT / 64) * (int)ND; i += NT) (&wcnt[0][0])[i] = 0;
         __syncthreads();
-        uint32_t dr[I];   // rank << 9 | digit (256: no item) — one register per item
+        uint32_t dr[I];   // rank << 10 | digit (ND: no item) — one register per item
 #pragma unroll
         for (int j = 0; j < I; ++j) {   // stable rank inside the wave, items in (j, lane) order
             const uint32_t i0 = (uint32_t)wave * (I * 64) + (uint32_t)j * 64;   // wave-uniform
             const uint32_t i = i0 + lane;
             const bool ok = i < cnt;
-            const uint32_t d = ok ? ((uint32_t)(key[j] >> sh) & dm) : 256u;
+            const uint32_t d = ok ? ((uint32_t)(key[j] >> sh) & dm) : NONE;
             dr[j] = d;
             if (i0 >= cnt) continue;   // no item of this row: skip its ballots
             uint64_t m = __ballot(ok);
 #pragma unroll
-            for (int b = 0; b < 8; ++b) {
+            for (int b = 0; b < DB; ++b) {
                 const bool bit = (d >> b) & 1u;
                 const uint64_t bb = __ballot(bit);
                 m &= bit ? bb : ~bb;
             }
             uint32_t before = 0;
             if (ok) before = wcnt[wave][d];
-            dr[j] = d | (before + (uint32_t)__popcll(m & lt)) << 9;
+            dr[j] = d | (before + (uint32_t)__popcll(m & lt)) << 10;
             if (ok && (m & lt) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
             wave_lds_sync();
         }
         __syncthreads();
         {   // digit starts, then each wave's start inside its digit (waves in order: stable)
-            const uint32_t d = (uint32_t)tid & 255u;
+            const uint32_t d = (uint32_t)tid & (ND - 1);
             uint32_t tot_d = 0;
-            if (tid < 256)
-                for (int w = 0; w < SS_T / 64; ++w) tot_d += wcnt[w][d];
+            if (tid < (int)ND)
+                for (int w = 0; w < NT / 64; ++w) tot_d += wcnt[w][d];
             uint32_t tt;
-            const uint32_t exd = block_excl_scan<SS_T>(tid < 256 ? tot_d : 0u, ws, &tt);
-            if (tid < 256) {
+            const uint32_t exd = block_excl_scan<NT>(tid < (int)ND ? tot_d : 0u, ws, &tt);
+            if (tid < (int)ND) {
                 uint32_t o = exd;
-                for (int w = 0; w < SS_T / 64; ++w) {
+                for (int w = 0; w < NT / 64; ++w) {
                     const uint32_t c = wcnt[w][d];
                     wcnt[w][d] = o;
                     o += c;
@@ -568,7 +570,7 @@ __device__ __forceinline__ void lds_lsd_sort_t(T (&key)[I], uint32_t cnt, int lo
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < I; ++j)
-            if ((dr[j] & 511u) < 256u) sk[wcnt[wave][dr[j] & 511u] + (dr[j] >> 9)] = key[j];
+            if ((dr[j] & 1023u) < ND) sk[wcnt[wave][dr[j] & 1023u] + (dr[j] >> 10)] = key[j];
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < I; ++j) {

@@ -1147,6 +1147,7 @@ void lookup_run(hga_ctx* c) {
     }
     uint64_t* fptr = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
     uint64_t* kptr = static_cast<uint64_t*>(L.kci_ptr.ensure(((uint64_t)L.n_sdk + 1) * 8));
+    ++L.kci_epoch;
     c->launch("lk_post", [&] {
         if (!H)   // with hits the first-occurrence scan above already left the CSR pointers in fptr
             hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(U + 1, 256)), dim3(256), 0, c->stream,
