@@ -6,8 +6,8 @@
 //   lk_starts     read-start bitmap (1 bit per base): a window is in one read iff no read
 //                 starts inside (start, end].
 //   lk_build      read-only table {canonical code -> KmerID}, 5 keys + 5 ids per 64-B bucket,
-//                 and a minimizer-blocked Bloom filter (16-B block per minimizer, 3 bits per
-//                 key in one word; a power of two of >= 11 bits per key: 4 MiB at C3, mostly L2/MALL-resident).
+//                 and a minimizer-blocked Bloom filter (16-B block per minimizer, one bit per
+//                 key in each of its 4 words; a power of two of >= 11 bits per key: 4 MiB at C3, mostly L2/MALL-resident).
 //                 KmerIDs come from the host (std::unordered_set order,
 //                 ReadClusteringEngine.cpp:237-241).
 //   lk_scan<0>    32 window ends per thread from packed frames: closed-form canonical codes,
@@ -120,18 +120,16 @@ __device__ __forceinline__ uint32_t key_minimizer(uint64_t x, int k, int km, uin
 __device__ __forceinline__ uint32_t end_mix(uint32_t e) {
     return (e ^ (e >> 16)) * 0x9E3779B1u;
 }
-#ifndef HGA_LK_FBITS
-#define HGA_LK_FBITS 3
-#endif
-static_assert(HGA_LK_FBITS >= 1 && HGA_LK_FBITS <= 6, "bit fields of the filter hash below its 2 word-select bits");
-__device__ __forceinline__ uint32_t end_bits(uint32_t x) {   // HGA_LK_FBITS bits of the word (5-bit fields from bit 25 down)
-    uint32_t m = 0;
-#pragma unroll
-    for (int i = 0; i < HGA_LK_FBITS; ++i) m |= 1u << ((x >> (25 - 5 * i)) & 31);
-    return m;
-}
-__device__ __forceinline__ uint64_t end_word(uint32_t minh, uint32_t x, uint64_t fmask) {
-    return ((((uint64_t)minh) << 2) | (x >> 30)) & fmask;
+// Partitioned block (km > 0): a key sets ONE bit in EACH of its block's four 32-bit words (5-bit
+// fields of x from bit 27 down), a window passes when all four are set.  The lane loads the whole
+// 16-B block per minimizer run anyway, so the four words cost nothing extra; against the former three
+// bits of one word picked by two hash bits, the same 16-B request and ~12 VALU a window, filter false
+// positives fall by ~40 % (tools/lk_filter_sim: 0.54 -> 0.32 per hit on a 1/8-scale C2/C3; each is a
+// table-line probe in lk_scan).
+__device__ __forceinline__ uint32_t part_bit(uint32_t x, int w) { return (x >> (27 - 5 * w)) & 31u; }
+__device__ __forceinline__ uint64_t block_of(uint32_t minh, uint64_t fmask) { return (((uint64_t)minh) << 2) & fmask; }
+__device__ __forceinline__ bool part_pass(const uint4& b, uint32_t x) {
+    return ((b.x >> part_bit(x, 0)) & (b.y >> part_bit(x, 1)) & (b.z >> part_bit(x, 2)) & (b.w >> part_bit(x, 3)) & 1u) != 0;
 }
 
 // Packed layout (2k bits of key + the KmerID bits fit 64: the SDK sets of C3-C5): 32-B buckets of
@@ -162,7 +160,9 @@ __global__ void lk_build(const uint64_t* __restrict__ keys, uint32_t n, Bucket* 
         uint32_t e;
         const uint32_t mz = key_minimizer(key, k, km, &e);
         const uint32_t x = end_mix(e);
-        atomicOr(&filt[end_word(mz, x, fmask)], end_bits(x));
+        const uint64_t w0 = block_of(mz, fmask);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) atomicOr(&filt[w0 + (uint64_t)w], 1u << part_bit(x, w));
     } else {
         atomicOr(&filt[filter_word(key_minimizer(key, k, km), h, fmask)], bloom_bits(h));
     }
@@ -405,18 +405,16 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
                     blk = filt4[bi];
                     cur = bi;
                 }
-                uint32_t sel, bb;
+                bool fp;   // the filter lets the window through
                 if constexpr (KM > 0) {
-                    const uint32_t x = end_mix(mh[j] ^ mh[j + KM]);
-                    sel = x >> 30;
-                    bb = end_bits(x);
+                    fp = part_pass(blk, end_mix(mh[j] ^ mh[j + KM]));
                 } else {
                     const uint64_t h = tab_hash(lk_canon(f, j, mask));
-                    sel = (uint32_t)(h >> 56) & 3u;
-                    bb = bloom_bits(h);
+                    const uint32_t sel = (uint32_t)(h >> 56) & 3u, bb = bloom_bits(h);
+                    const uint32_t wv = sel == 0 ? blk.x : sel == 1 ? blk.y : sel == 2 ? blk.z : blk.w;
+                    fp = (wv & bb) == bb;
                 }
-                const uint32_t wv = sel == 0 ? blk.x : sel == 1 ? blk.y : sel == 2 ? blk.z : blk.w;
-                const bool pass = (((wv & bb) == bb) || ((force >> j) & 1u)) && ((wm >> j) & 1u);
+                const bool pass = (fp || ((force >> j) & 1u)) && ((wm >> j) & 1u);
                 if (pass) {
                     const uint64_t key = lk_canon(f, j, mask);
                     const uint32_t pos = atomicAdd(&qcnt[wave], 1u);
