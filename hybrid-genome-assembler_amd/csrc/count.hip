@@ -2167,6 +2167,80 @@ __global__ void __launch_bounds__(NT) kc_bx_lsort(uint64_t* __restrict__ keys, c
     }
 }
 
+// The u32 case (k <= 21) of the large-segment sort without LSD passes: the segment's keys (unique
+// codes, spread evenly below their digit) are counted into 4096 sub-buckets by the next 12 code bits (LDS
+// atomics), the counts scanned, the keys scattered into LDS by sub-bucket (an L2-hot second read of the
+// segment), and each thread then sorts its sub-buckets (~3 keys each at a C4 shard's 12 K-key segments,
+// ~6 at its 25 K ones: insertion sort; a crowded one by Shell sort) in LDS and writes them out in order —
+// about one LDS atomic, write and read per key instead of three stable 9-bit passes with ten ballots a key.
+constexpr int CS_T = 1024, CS_B = 12;
+__global__ void __launch_bounds__(CS_T) kc_bx_csort(uint64_t* __restrict__ keys, const uint32_t* __restrict__ hist,
+                                                    const uint32_t* __restrict__ dbase, int bits, uint32_t min_len) {
+    __shared__ uint32_t sk[BX_CAP32];
+    __shared__ uint32_t cnt[1 << CS_B];
+    __shared__ uint32_t ws[CS_T / 64 + 1];
+    const uint32_t d = blockIdx.x;
+    const uint32_t n = hist[d], st = dbase[d];
+    if (n <= min_len || n > BX_CAP32) return;   // (the host checked the cap for every digit)
+    const uint32_t tid = threadIdx.x;
+    const int lb = bits - 12;                    // code bits below the digit (<= 30: u32 keys)
+    const int sb = lb < CS_B ? lb : CS_B;        // sub-bucket bits
+    const int sh = lb - sb;
+    const uint64_t lm = (1ull << lb) - 1;
+    const uint32_t nsb = 1u << sb;
+    for (uint32_t i = tid; i < nsb; i += CS_T) cnt[i] = 0;
+    __syncthreads();
+    const uint64_t* __restrict__ src = keys + st;
+    for (uint32_t i = tid; i < n; i += CS_T) atomicAdd(&cnt[(uint32_t)((src[i] & lm) >> sh)], 1u);
+    __syncthreads();
+    {   // exclusive scan of the sub-bucket counts, four per thread
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = 4 * tid + (uint32_t)q;
+            v[q] = i < nsb ? cnt[i] : 0u;
+            sum += v[q];
+        }
+        uint32_t tot;
+        uint32_t o = block_excl_scan<CS_T>(sum, ws, &tot);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = 4 * tid + (uint32_t)q;
+            if (i < nsb) cnt[i] = o;
+            o += v[q];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += CS_T) {
+        const uint64_t k = src[i];
+        const uint32_t pos = atomicAdd(&cnt[(uint32_t)((k & lm) >> sh)], 1u);   // cnt[c] ends at c's end
+        sk[pos] = (uint32_t)(((k & lm) << 1) | (k >> 63));
+    }
+    __syncthreads();
+    const uint64_t hi = (uint64_t)d << lb;
+    for (uint32_t c = tid; c < nsb; c += CS_T) {
+        const uint32_t b = c ? cnt[c - 1] : 0u, e = cnt[c];
+        // Shell sort (Ciura's gaps; gap 1 = insertion sort, all a sub-bucket of a few keys needs): a
+        // skewed segment — keys crowded into a few sub-buckets, e.g. a narrow code range — stays
+        // O(n^1.3) per thread instead of insertion sort's O(n^2)
+        constexpr uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+        for (int gi = 0; gi < 8; ++gi) {
+            const uint32_t g = gaps[gi];
+            if (g >= e - b) continue;
+            for (uint32_t i = b + g; i < e; ++i) {
+                const uint32_t v = sk[i];
+                uint32_t j = i;
+                for (; j >= b + g && sk[j - g] > v; j -= g) sk[j] = sk[j - g];
+                sk[j] = v;
+            }
+        }
+        for (uint32_t i = b; i < e; ++i) {
+            const uint32_t v = sk[i];
+            keys[(uint64_t)st + i] = hi | (uint64_t)(v >> 1) | ((uint64_t)(v & 1u) << 63);
+        }
+    }
+}
+
 __global__ void kc_iota(uint32_t* v, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
@@ -2814,7 +2888,10 @@ void count_select(hga_ctx* c, int64_t lower, int64_t upper, uint64_t* n_out, uin
         c->check_launch("kc_bx_wsort");
         if (hs[2] > BX_MAX) {
             c->launch("radix_segsort", [&] {
-                if (u32seg) {
+                if (u32seg && !std::getenv("HGA_BX_LSD")) {   // (HGA_BX_LSD: the LSD-pass kernels, tests)
+                    hipLaunchKernelGGL(kc_bx_csort, dim3(SEL_HB), dim3(CS_T), 0, c->stream, out, (const uint32_t*)dhist,
+                                       (const uint32_t*)bx_dbase, bits, BX_MAX);
+                } else if (u32seg) {
                     hipLaunchKernelGGL((kc_bx_lsort<true, 512, 32, 9>), dim3(SEL_HB), dim3(512), 0, c->stream, out,
                                        (const uint32_t*)dhist, (const uint32_t*)bx_dbase, bits, BX_MAX);
                     if (hs[2] > 16384u)

@@ -104,13 +104,18 @@ def test_export_sort_few_big_segments(gpu_ctx):
     assert nd == len(want) and np.all(flags == 1)
 
 
-@pytest.mark.parametrize("k,hot", [(19, 0), (19, 30_000), (19, 40_000), (27, 0), (27, 15_000), (27, 20_000)])
-def test_export_sort_workgroup_segments(gpu_ctx, k, hot):
+@pytest.mark.parametrize("k,hot,lsd", [(19, 0, False), (19, 30_000, False), (19, 40_000, False), (19, 0, True),
+                                       (19, 30_000, True), (21, 25_000, False), (27, 0, False), (27, 15_000, False),
+                                       (27, 20_000, False)])
+def test_export_sort_workgroup_segments(gpu_ctx, monkeypatch, k, hot, lsd):
     """~4.5 M exported keys spread over the code space (~1.1 K per 12-bit digit, many past one wave's
     BX_MAX = 1024): the bucketed export sort with workgroup LDS sorts of the larger digit segments
     (count.hip kc_bx_lsort, the C4-shard-sized path: u32 keys up to 32768 a segment at k <= 21, u64 up to
     16384 above); `hot` keys packed into one digit — within the cap, or past it (the MSD + global-radix
-    path)."""
+    path).  At k <= 21 the segments go through the sub-bucket counting sort (kc_bx_csort) unless `lsd`
+    (HGA_BX_LSD: the LSD-pass kernels)."""
+    if lsd:
+        monkeypatch.setenv("HGA_BX_LSD", "1")
     rng = np.random.default_rng(hot + 3 + k)
     lb = 2 * k - 12
     keys = rng.integers(0, 1 << (2 * k), 6_000_000, dtype=np.uint64)
@@ -127,3 +132,19 @@ def test_export_sort_workgroup_segments(gpu_ctx, k, hot):
     want = keys[(counts >= 10) & (counts <= 25)]
     assert np.array_equal(sel, want)
     assert nd == len(want) and np.all(flags == 1)
+
+
+def test_export_sort_crowded_sub_buckets(gpu_ctx):
+    """A digit segment whose keys crowd into one sub-bucket of kc_bx_csort (20 K keys inside a 2^14-code
+    range, i.e. one of its 4096 sub-buckets at k = 19): sorted by the Shell sort path, ascending."""
+    rng = np.random.default_rng(11)
+    spread = rng.integers(0, 1 << 38, 2_000_000, dtype=np.uint64)
+    crowd = rng.integers(333 << 26, (333 << 26) + (1 << 14), 20_000, dtype=np.uint64)
+    keys = np.unique(np.concatenate([spread, crowd]))
+    counts = np.full(len(keys), 12, np.uint32)
+    gpu_ctx.count_begin(19, 1)
+    gpu_ctx.count_add_rows(0, keys, counts)
+    gpu_ctx.count_run(2)
+    sel, flags, nd = gpu_ctx.select(10, 25)
+    assert np.array_equal(sel, keys)
+    assert nd == len(keys) and np.all(flags == 1)
