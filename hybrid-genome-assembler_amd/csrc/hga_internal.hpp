@@ -192,7 +192,7 @@ struct LookupState {
     DevBuf bases, offsets;
     // results
     DevBuf tile_cnt, hit_read, hit_kid, hit_pos, hit_ptr, s_key, s_val, s_key2, s_val2,
-        first_flag, first_kid, first_pos, first_read, first_ptr, kci_key, kci_val, kci_ptr, scratch,
+        first_flag, first_kid, first_pos, first_read, first_ptr, kci_key, kci_val, kci_ptr, kci_tmp, scratch,
         scratch2, scratch3, big_list, hll_part;
     std::vector<uint64_t> h_offsets;
     uint64_t windows = 0, hits = 0, firsts = 0, reads_hit = 0;

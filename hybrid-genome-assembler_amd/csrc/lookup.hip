@@ -565,6 +565,170 @@ __global__ void lk_ptr(const uint32_t* __restrict__ idx, uint64_t H, uint64_t ns
     for (uint64_t s = lo; s <= hi; ++s) ptr[s] = i;
 }
 
+// ---- kmer_component_index without LSD radix passes (ReadClusteringEngine.cpp:262-267, 282-284) ----
+// The hits arrive in read order; kmer_component_index is, per KmerID, its reads ascending (with
+// duplicates).  One MSD pass on the top D KmerID bits (per-tile LDS histograms, a column scan of them:
+// deterministic offsets, no global atomics) scatters (low KmerID bits, read) pairs into <= 4096 buckets;
+// one workgroup per bucket then counts its pairs into 2^S sub-buckets = single KmerIDs (S = kbits - D <=
+// 12), which gives kci_ptr directly, places the reads by sub-bucket in LDS and each thread sorts its
+// KmerIDs' reads (insertion sort of ~11 at C3; Shell sort for a crowded one) — the order a stable sort
+// by KmerID leaves them in.  Replaces three 8-bit LSD passes (upsweep + downsweep each) and lk_ptr.
+constexpr int KC_T = 256, KC_I = 32;
+constexpr uint32_t KC_TILE = KC_T * KC_I;   // hits per histogram / scatter tile
+constexpr int KC_DMAX = 12, KC_SMAX = 12;
+constexpr uint32_t KC_CAP = 32768;          // pairs per bucket held in LDS (u32 reads)
+constexpr int KC_CT = 1024;                 // bucket-sort workgroup
+__global__ void __launch_bounds__(KC_T) lk_kci_hist(const uint32_t* __restrict__ hk, uint64_t H, int sh, uint32_t nb,
+                                                    uint32_t* __restrict__ rows) {
+    __shared__ uint32_t h[1 << KC_DMAX];
+    for (uint32_t i = threadIdx.x; i < nb; i += KC_T) h[i] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * KC_TILE;
+#pragma unroll 8
+    for (int j = 0; j < KC_I; ++j) {
+        const uint64_t i = base + (uint64_t)j * KC_T + threadIdx.x;
+        if (i < H) atomicAdd(&h[hk[i] >> sh], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += KC_T) rows[(uint64_t)blockIdx.x * nb + i] = h[i];
+}
+// tot[b] = column sums of rows[tiles][nb] (one thread per bucket, rows strided)
+__global__ void lk_kci_colsum(const uint32_t* __restrict__ rows, uint32_t tiles, uint32_t nb, uint32_t* __restrict__ tot) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint32_t s = 0;
+    for (uint32_t t = 0; t < tiles; ++t) s += rows[(uint64_t)t * nb + b];
+    tot[b] = s;
+}
+// bbase[b] = exclusive scan of tot (nb <= 4096: one 1024-thread workgroup, four a thread); stat[0] = the
+// largest bucket
+__global__ void __launch_bounds__(1024) lk_kci_scan(const uint32_t* __restrict__ tot, uint32_t nb,
+                                                    uint32_t* __restrict__ bbase, unsigned long long* __restrict__ stat) {
+    __shared__ uint32_t ws[1024 / 64 + 1];
+    __shared__ uint32_t mx;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) mx = 0;
+    uint32_t v[4], sum = 0, m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + (uint32_t)q;
+        v[q] = i < nb ? tot[i] : 0u;
+        sum += v[q];
+        m = max(m, v[q]);
+    }
+    uint32_t total;
+    uint32_t o = block_excl_scan<1024>(sum, ws, &total);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + (uint32_t)q;
+        if (i < nb) bbase[i] = o;
+        o += v[q];
+    }
+    atomicMax(&mx, m);
+    __syncthreads();
+    if (t == 0) stat[0] = mx;
+}
+// rows[t][b] := bbase[b] + the counts of bucket b in tiles before t (in place; one thread a bucket
+// walks its column, consecutive threads on consecutive buckets: coalesced rows)
+__global__ void lk_kci_colscan(uint32_t* __restrict__ rows, uint32_t tiles, uint32_t nb, const uint32_t* __restrict__ bbase) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint32_t o = bbase[b];
+    for (uint32_t t = 0; t < tiles; ++t) {
+        const uint32_t c = rows[(uint64_t)t * nb + b];
+        rows[(uint64_t)t * nb + b] = o;
+        o += c;
+    }
+}
+// Per tile: its pairs to their buckets from the offsets lk_kci_colscan left in rows[tile], ranks inside the
+// tile by LDS atomics (the order inside a bucket is re-sorted by lk_kci_bsort)
+__global__ void __launch_bounds__(KC_T) lk_kci_scatter(const uint32_t* __restrict__ hk, const uint32_t* __restrict__ hr,
+                                                       uint64_t H, int sh, uint32_t nb, const uint32_t* __restrict__ off,
+                                                       uint64_t* __restrict__ pairs) {
+    __shared__ uint32_t cur[1 << KC_DMAX];
+    const uint32_t t = blockIdx.x;
+    for (uint32_t b = threadIdx.x; b < nb; b += KC_T) cur[b] = off[(uint64_t)t * nb + b];
+    __syncthreads();
+    const uint64_t base = (uint64_t)t * KC_TILE;
+    const uint32_t smask = (1u << sh) - 1u;
+#pragma unroll 8
+    for (int j = 0; j < KC_I; ++j) {
+        const uint64_t i = base + (uint64_t)j * KC_T + threadIdx.x;
+        if (i < H) {
+            const uint32_t k = hk[i];
+            const uint32_t pos = atomicAdd(&cur[k >> sh], 1u);
+            pairs[pos] = ((uint64_t)(k & smask) << 32) | hr[i];
+        }
+    }
+}
+// One workgroup per bucket: sub-bucket counts -> kci_ptr of its KmerIDs, reads placed by KmerID in LDS,
+// each KmerID's reads sorted ascending, written to kci_val.  A bucket past KC_CAP sets *flag (the host
+// redoes the index by the radix path).
+__global__ void __launch_bounds__(KC_CT) lk_kci_bsort(const uint64_t* __restrict__ pairs, const uint32_t* __restrict__ tot,
+                                                      const uint32_t* __restrict__ bbase, int S, uint64_t n_sdk,
+                                                      uint64_t H, uint64_t* __restrict__ kptr, uint32_t* __restrict__ kv,
+                                                      unsigned long long* __restrict__ flag) {
+    __shared__ uint32_t sk[KC_CAP];
+    __shared__ uint32_t cnt[1 << KC_SMAX];
+    __shared__ uint32_t ws[KC_CT / 64 + 1];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t n = tot[b], st = bbase[b];
+    const uint32_t ns = 1u << S;
+    if (b == 0 && tid == 0) kptr[n_sdk] = H;
+    if (n > KC_CAP) {
+        if (tid == 0) atomicOr(flag, 1ull);
+        return;
+    }
+    for (uint32_t i = tid; i < ns; i += KC_CT) cnt[i] = 0;
+    __syncthreads();
+    const uint64_t* __restrict__ src = pairs + st;
+    for (uint32_t i = tid; i < n; i += KC_CT) atomicAdd(&cnt[(uint32_t)(src[i] >> 32)], 1u);
+    __syncthreads();
+    {   // exclusive scan of the sub-bucket counts (<= 4096: four a thread); kci_ptr of the bucket's KmerIDs
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = 4 * tid + (uint32_t)q;
+            v[q] = i < ns ? cnt[i] : 0u;
+            sum += v[q];
+        }
+        uint32_t total;
+        uint32_t o = block_excl_scan<KC_CT>(sum, ws, &total);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = 4 * tid + (uint32_t)q;
+            if (i < ns) {
+                cnt[i] = o;
+                const uint64_t kid = ((uint64_t)b << S) | i;
+                if (kid < n_sdk) kptr[kid] = (uint64_t)st + o;
+            }
+            o += v[q];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += KC_CT) {
+        const uint64_t pr = src[i];
+        sk[atomicAdd(&cnt[(uint32_t)(pr >> 32)], 1u)] = (uint32_t)pr;   // cnt[s] ends at s's end
+    }
+    __syncthreads();
+    constexpr uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+    for (uint32_t s2 = tid; s2 < ns; s2 += KC_CT) {
+        const uint32_t lo = s2 ? cnt[s2 - 1] : 0u, hi = cnt[s2];
+        for (int gi = 0; gi < 8; ++gi) {   // Shell sort (gap 1 = insertion sort of a KmerID's ~11 reads)
+            const uint32_t g = gaps[gi];
+            if (g >= hi - lo) continue;
+            for (uint32_t i = lo + g; i < hi; ++i) {
+                const uint32_t v = sk[i];
+                uint32_t j = i;
+                for (; j >= lo + g && sk[j - g] > v; j -= g) sk[j] = sk[j - g];
+                sk[j] = v;
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += KC_CT) kv[(uint64_t)st + i] = sk[i];
+}
+
 // Number of non-empty CSR segments, the largest one, and the segments with more than 512 / 2048 entries
 // listed for the per-segment sort tiers (order irrelevant; one list atomic per workgroup): out[0] non-empty
 // segments, out[1] largest, out[2] / out[3]
@@ -1138,26 +1302,69 @@ void lookup_run(hga_ctx* c) {
                                fptr0, kmask, fk, fp, fr);
         });
         c->check_launch("lk_first_write");
-        // kmer_component_index: stable sort of the read-ordered hits by KmerID
-        uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
-        uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(H * 4));
-        radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
     }
     uint64_t* fptr = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
     uint64_t* kptr = static_cast<uint64_t*>(L.kci_ptr.ensure(((uint64_t)L.n_sdk + 1) * 8));
+    uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(std::max<uint64_t>(H, 1) * 4));
     ++L.kci_epoch;
+    // kmer_component_index: the bucketed sort (lk_kci_*) when every bucket fits a workgroup's LDS, else
+    // (or with HGA_KCI_RADIX) a stable radix sort of the read-ordered hits by KmerID + lk_ptr
+    const int kD = kbits > KC_SMAX ? kbits - KC_SMAX : 0, kS = kbits - kD;
+    const bool bucketed = H && kD <= KC_DMAX && !std::getenv("HGA_KCI_RADIX");
+    auto radix_kci = [&] {
+        uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
+        radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
+        c->launch("lk_post", [&] {
+            hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(H + 1, 256)), dim3(256), 0, c->stream, (const uint32_t*)kk, H,
+                               (uint64_t)L.n_sdk, kptr);
+        });
+        c->check_launch("lk_ptr");
+    };
+    unsigned long long* kflag = nullptr;
+    if (bucketed) {
+        const uint32_t nbk = 1u << kD, tiles = (uint32_t)((H + KC_TILE - 1) / KC_TILE);
+        const size_t rows_b = (size_t)tiles * nbk * 4;
+        char* kt = static_cast<char*>(L.kci_tmp.ensure(64 + rows_b + 2 * (size_t)nbk * 4 + H * 8 + 256));
+        kflag = reinterpret_cast<unsigned long long*>(kt);
+        uint32_t* rows = reinterpret_cast<uint32_t*>(kt + 64);
+        uint32_t* tot = reinterpret_cast<uint32_t*>(kt + 64 + rows_b);
+        uint32_t* bbase = tot + nbk;
+        uint64_t* pairs = reinterpret_cast<uint64_t*>(kt + ((64 + rows_b + 2 * (size_t)nbk * 4 + 255) & ~(size_t)255));
+        HGA_HIP(hipMemsetAsync(kflag, 0, 64, c->stream));
+        c->launch("lk_kci", [&] {
+            hipLaunchKernelGGL(lk_kci_hist, dim3(tiles), dim3(KC_T), 0, c->stream, hk, H, kS, nbk, rows);
+            hipLaunchKernelGGL(lk_kci_colsum, dim3(blocks_for(nbk, 256)), dim3(256), 0, c->stream, (const uint32_t*)rows,
+                               tiles, nbk, tot);
+            hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)tot, nbk, bbase, kflag + 1);
+            hipLaunchKernelGGL(lk_kci_colscan, dim3(blocks_for(nbk, 256)), dim3(256), 0, c->stream, rows, tiles, nbk,
+                               (const uint32_t*)bbase);
+            hipLaunchKernelGGL(lk_kci_scatter, dim3(tiles), dim3(KC_T), 0, c->stream, hk, hr, H, kS, nbk,
+                               (const uint32_t*)rows, pairs);
+            hipLaunchKernelGGL(lk_kci_bsort, dim3(nbk), dim3(KC_CT), 0, c->stream, (const uint64_t*)pairs,
+                               (const uint32_t*)tot, (const uint32_t*)bbase, kS, (uint64_t)L.n_sdk, H, kptr, kv, kflag);
+        });
+        c->check_launch("lk_kci");
+    } else if (H) {
+        radix_kci();
+    }
     c->launch("lk_post", [&] {
         if (!H)   // with hits the first-occurrence scan above already left the CSR pointers in fptr
             hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(U + 1, 256)), dim3(256), 0, c->stream,
                                (const uint32_t*)nullptr, U, n, fptr);
-        hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(H + 1, 256)), dim3(256), 0, c->stream,
-                           H ? L.kci_key.as<uint32_t>() : (const uint32_t*)nullptr, H, (uint64_t)L.n_sdk, kptr);
+        if (!H)
+            hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(H + 1, 256)), dim3(256), 0, c->stream, (const uint32_t*)nullptr,
+                               H, (uint64_t)L.n_sdk, kptr);
     });
     c->check_launch("lk_ptr");
-    unsigned long long hc[4];
+    unsigned long long hc[4], kf = 0;
     HGA_HIP(hipMemcpyAsync(hc, ctr, 32, hipMemcpyDeviceToHost, c->stream));
     if (H) HGA_HIP(hipMemcpyAsync(&U, fptr + n, 8, hipMemcpyDeviceToHost, c->stream));
+    if (kflag) HGA_HIP(hipMemcpyAsync(&kf, kflag, 8, hipMemcpyDeviceToHost, c->stream));
     c->sync();
+    if (kf) {   // a bucket past the LDS: the radix path (reads hk / hr, still intact)
+        radix_kci();
+        c->sync();
+    }
     L.firsts = U;
     L.reads_hit = hc[0];
     L.ran = true;
