@@ -858,8 +858,8 @@ def main():
         for _ in range(reps):
             ctx2.lookup_run()
         lk = {}
-        for name in ("lk_pack", "lk_count", "lk_emit", "lk_post", "lk_sort", "radix_upsweep", "radix_downsweep",
-                     "scan"):
+        for name in ("lk_pack", "lk_count", "lk_emit", "lk_post", "lk_sort", "lk_kci", "radix_upsweep",
+                     "radix_downsweep", "scan"):
             ms, n = ctx2.profile_get(name)
             if n:
                 lk[name] = round(ms / reps, 4)
