@@ -573,13 +573,14 @@ __global__ void lk_ptr(const uint32_t* __restrict__ idx, uint64_t H, uint64_t ns
 // 12), which gives kci_ptr directly, places the reads by sub-bucket in LDS and each thread sorts its
 // KmerIDs' reads (insertion sort of ~11 at C3; Shell sort for a crowded one) — the order a stable sort
 // by KmerID leaves them in.  Replaces three 8-bit LSD passes (upsweep + downsweep each) and lk_ptr.
-constexpr int KC_T = 256, KC_I = 32;
-constexpr uint32_t KC_TILE = KC_T * KC_I;   // hits per histogram / scatter tile
+constexpr int KC_T = 512, KC_I = 64;
+constexpr uint32_t KC_TILE = KC_T * KC_I;   // hits per histogram / scatter tile (32 K: ~625 tiles at C3)
 constexpr int KC_DMAX = 12, KC_SMAX = 12;
-constexpr uint32_t KC_CAP = 32768;          // pairs per bucket held in LDS (u32 reads)
-constexpr int KC_CT = 1024;                 // bucket-sort workgroup
+constexpr int KC_CT = 1024, KC_PT = 15;     // bucket-sort workgroup, pairs a thread holds in registers
+constexpr uint32_t KC_CAP = KC_CT * KC_PT;  // pairs per bucket (60 KB of u32 reads + 16 KB of counters in LDS: two workgroups a CU)
+// per tile: counts of the top D KmerID bits, stored bucket-major (rows[b][tile]) for lk_kci_bscan
 __global__ void __launch_bounds__(KC_T) lk_kci_hist(const uint32_t* __restrict__ hk, uint64_t H, int sh, uint32_t nb,
-                                                    uint32_t* __restrict__ rows) {
+                                                    uint32_t tiles, uint32_t* __restrict__ rows) {
     __shared__ uint32_t h[1 << KC_DMAX];
     for (uint32_t i = threadIdx.x; i < nb; i += KC_T) h[i] = 0;
     __syncthreads();
@@ -590,15 +591,24 @@ __global__ void __launch_bounds__(KC_T) lk_kci_hist(const uint32_t* __restrict__
         if (i < H) atomicAdd(&h[hk[i] >> sh], 1u);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nb; i += KC_T) rows[(uint64_t)blockIdx.x * nb + i] = h[i];
+    for (uint32_t i = threadIdx.x; i < nb; i += KC_T) rows[(uint64_t)i * tiles + blockIdx.x] = h[i];
 }
-// tot[b] = column sums of rows[tiles][nb] (one thread per bucket, rows strided)
-__global__ void lk_kci_colsum(const uint32_t* __restrict__ rows, uint32_t tiles, uint32_t nb, uint32_t* __restrict__ tot) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per bucket: its tiles' counts -> exclusive offsets inside the bucket (in place, coalesced over
+// the bucket's row), tot[b] = the bucket's size
+__global__ void __launch_bounds__(256) lk_kci_bscan(uint32_t* __restrict__ rows, uint32_t tiles, uint32_t nb,
+                                                    uint32_t* __restrict__ tot) {
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (b >= nb) return;
-    uint32_t s = 0;
-    for (uint32_t t = 0; t < tiles; ++t) s += rows[(uint64_t)t * nb + b];
-    tot[b] = s;
+    uint32_t* __restrict__ r = rows + (uint64_t)b * tiles;
+    uint32_t run = 0;
+    for (uint32_t t0 = 0; t0 < tiles; t0 += 64) {
+        const uint32_t t = t0 + lane;
+        const uint32_t c = t < tiles ? r[t] : 0u;
+        const uint32_t inc = wave_incl_scan(c, (int)lane);
+        if (t < tiles) r[t] = run + inc - c;
+        run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) tot[b] = run;
 }
 // bbase[b] = exclusive scan of tot (nb <= 4096: one 1024-thread workgroup, four a thread); stat[0] = the
 // largest bucket
@@ -628,26 +638,15 @@ __global__ void __launch_bounds__(1024) lk_kci_scan(const uint32_t* __restrict__
     __syncthreads();
     if (t == 0) stat[0] = mx;
 }
-// rows[t][b] := bbase[b] + the counts of bucket b in tiles before t (in place; one thread a bucket
-// walks its column, consecutive threads on consecutive buckets: coalesced rows)
-__global__ void lk_kci_colscan(uint32_t* __restrict__ rows, uint32_t tiles, uint32_t nb, const uint32_t* __restrict__ bbase) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    uint32_t o = bbase[b];
-    for (uint32_t t = 0; t < tiles; ++t) {
-        const uint32_t c = rows[(uint64_t)t * nb + b];
-        rows[(uint64_t)t * nb + b] = o;
-        o += c;
-    }
-}
-// Per tile: its pairs to their buckets from the offsets lk_kci_colscan left in rows[tile], ranks inside the
-// tile by LDS atomics (the order inside a bucket is re-sorted by lk_kci_bsort)
+// Per tile: its pairs to their buckets at bbase[b] + the tile's offset inside b (lk_kci_bscan), ranks
+// inside the tile by LDS atomics (the order inside a bucket is re-sorted by lk_kci_bsort)
 __global__ void __launch_bounds__(KC_T) lk_kci_scatter(const uint32_t* __restrict__ hk, const uint32_t* __restrict__ hr,
-                                                       uint64_t H, int sh, uint32_t nb, const uint32_t* __restrict__ off,
+                                                       uint64_t H, int sh, uint32_t nb, uint32_t tiles,
+                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ bbase,
                                                        uint64_t* __restrict__ pairs) {
     __shared__ uint32_t cur[1 << KC_DMAX];
     const uint32_t t = blockIdx.x;
-    for (uint32_t b = threadIdx.x; b < nb; b += KC_T) cur[b] = off[(uint64_t)t * nb + b];
+    for (uint32_t b = threadIdx.x; b < nb; b += KC_T) cur[b] = bbase[b] + off[(uint64_t)b * tiles + t];
     __syncthreads();
     const uint64_t base = (uint64_t)t * KC_TILE;
     const uint32_t smask = (1u << sh) - 1u;
@@ -664,7 +663,7 @@ __global__ void __launch_bounds__(KC_T) lk_kci_scatter(const uint32_t* __restric
 // One workgroup per bucket: sub-bucket counts -> kci_ptr of its KmerIDs, reads placed by KmerID in LDS,
 // each KmerID's reads sorted ascending, written to kci_val.  A bucket past KC_CAP sets *flag (the host
 // redoes the index by the radix path).
-__global__ void __launch_bounds__(KC_CT) lk_kci_bsort(const uint64_t* __restrict__ pairs, const uint32_t* __restrict__ tot,
+__global__ void __launch_bounds__(KC_CT, 8) lk_kci_bsort(const uint64_t* __restrict__ pairs, const uint32_t* __restrict__ tot,
                                                       const uint32_t* __restrict__ bbase, int S, uint64_t n_sdk,
                                                       uint64_t H, uint64_t* __restrict__ kptr, uint32_t* __restrict__ kv,
                                                       unsigned long long* __restrict__ flag) {
@@ -682,7 +681,18 @@ __global__ void __launch_bounds__(KC_CT) lk_kci_bsort(const uint64_t* __restrict
     for (uint32_t i = tid; i < ns; i += KC_CT) cnt[i] = 0;
     __syncthreads();
     const uint64_t* __restrict__ src = pairs + st;
-    for (uint32_t i = tid; i < n; i += KC_CT) atomicAdd(&cnt[(uint32_t)(src[i] >> 32)], 1u);
+    uint64_t pr[KC_PT];   // the bucket is read once: all loads in flight, then the ranks by LDS atomics
+#pragma unroll
+    for (int q = 0; q < KC_PT; ++q) {
+        const uint32_t i = tid + (uint32_t)q * KC_CT;
+        pr[q] = i < n ? src[i] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < KC_PT; ++q)   // the rank inside the sub-bucket joins the high word (sub < 2^12, rank < 2^14)
+        if (tid + (uint32_t)q * KC_CT < n) {
+            const uint32_t sb = (uint32_t)(pr[q] >> 32);
+            pr[q] += (uint64_t)atomicAdd(&cnt[sb], 1u) << 44;
+        }
     __syncthreads();
     {   // exclusive scan of the sub-bucket counts (<= 4096: four a thread); kci_ptr of the bucket's KmerIDs
         uint32_t v[4], sum = 0;
@@ -706,14 +716,14 @@ __global__ void __launch_bounds__(KC_CT) lk_kci_bsort(const uint64_t* __restrict
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += KC_CT) {
-        const uint64_t pr = src[i];
-        sk[atomicAdd(&cnt[(uint32_t)(pr >> 32)], 1u)] = (uint32_t)pr;   // cnt[s] ends at s's end
-    }
+#pragma unroll
+    for (int q = 0; q < KC_PT; ++q)
+        if (tid + (uint32_t)q * KC_CT < n)
+            sk[cnt[(uint32_t)(pr[q] >> 32) & 0xfffu] + (uint32_t)(pr[q] >> 44)] = (uint32_t)pr[q];
     __syncthreads();
     constexpr uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
     for (uint32_t s2 = tid; s2 < ns; s2 += KC_CT) {
-        const uint32_t lo = s2 ? cnt[s2 - 1] : 0u, hi = cnt[s2];
+        const uint32_t lo = cnt[s2], hi = s2 + 1 < ns ? cnt[s2 + 1] : n;
         for (int gi = 0; gi < 8; ++gi) {   // Shell sort (gap 1 = insertion sort of a KmerID's ~11 reads)
             const uint32_t g = gaps[gi];
             if (g >= hi - lo) continue;
@@ -1308,9 +1318,17 @@ void lookup_run(hga_ctx* c) {
     uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(std::max<uint64_t>(H, 1) * 4));
     ++L.kci_epoch;
     // kmer_component_index: the bucketed sort (lk_kci_*) when every bucket fits a workgroup's LDS, else
-    // (or with HGA_KCI_RADIX) a stable radix sort of the read-ordered hits by KmerID + lk_ptr
-    const int kD = kbits > KC_SMAX ? kbits - KC_SMAX : 0, kS = kbits - kD;
-    const bool bucketed = H && kD <= KC_DMAX && !std::getenv("HGA_KCI_RADIX");
+    // (with HGA_KCI_BUCKETED=1) or a stable radix sort of the read-ordered hits by KmerID + lk_ptr
+    // D top KmerID bits pick the bucket: at least kbits - KC_SMAX (sub-buckets = KmerIDs fit the LDS
+    // counters) and enough buckets for ~6 K hits each (KC_CAP = 16 K a bucket), at most KC_DMAX
+    int kD = kbits > KC_SMAX ? kbits - KC_SMAX : 0;
+    while (kD < KC_DMAX && kD < kbits && (H >> kD) > 6000) ++kD;
+    const int kS = kbits - kD;
+    // measured at C3 (round 6): lk_kci_scatter 0.51 ms (8-B runs into 4096 buckets, the write pattern of
+    // profiles/r05_slab_probe.txt), bsort 0.17, hist 0.08: 0.78 ms against the radix path's 0.58 — so the
+    // radix path is the default and the bucketed one is opt-in (HGA_KCI_BUCKETED=1)
+    const char* kb_env = std::getenv("HGA_KCI_BUCKETED");
+    const bool bucketed = H && kD <= KC_DMAX && kb_env && *kb_env == '1';
     auto radix_kci = [&] {
         uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
         radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
@@ -1332,14 +1350,11 @@ void lookup_run(hga_ctx* c) {
         uint64_t* pairs = reinterpret_cast<uint64_t*>(kt + ((64 + rows_b + 2 * (size_t)nbk * 4 + 255) & ~(size_t)255));
         HGA_HIP(hipMemsetAsync(kflag, 0, 64, c->stream));
         c->launch("lk_kci", [&] {
-            hipLaunchKernelGGL(lk_kci_hist, dim3(tiles), dim3(KC_T), 0, c->stream, hk, H, kS, nbk, rows);
-            hipLaunchKernelGGL(lk_kci_colsum, dim3(blocks_for(nbk, 256)), dim3(256), 0, c->stream, (const uint32_t*)rows,
-                               tiles, nbk, tot);
+            hipLaunchKernelGGL(lk_kci_hist, dim3(tiles), dim3(KC_T), 0, c->stream, hk, H, kS, nbk, tiles, rows);
+            hipLaunchKernelGGL(lk_kci_bscan, dim3(blocks_for(nbk, 4)), dim3(256), 0, c->stream, rows, tiles, nbk, tot);
             hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)tot, nbk, bbase, kflag + 1);
-            hipLaunchKernelGGL(lk_kci_colscan, dim3(blocks_for(nbk, 256)), dim3(256), 0, c->stream, rows, tiles, nbk,
-                               (const uint32_t*)bbase);
-            hipLaunchKernelGGL(lk_kci_scatter, dim3(tiles), dim3(KC_T), 0, c->stream, hk, hr, H, kS, nbk,
-                               (const uint32_t*)rows, pairs);
+            hipLaunchKernelGGL(lk_kci_scatter, dim3(tiles), dim3(KC_T), 0, c->stream, hk, hr, H, kS, nbk, tiles,
+                               (const uint32_t*)rows, (const uint32_t*)bbase, pairs);
             hipLaunchKernelGGL(lk_kci_bsort, dim3(nbk), dim3(KC_CT), 0, c->stream, (const uint64_t*)pairs,
                                (const uint32_t*)tot, (const uint32_t*)bbase, kS, (uint64_t)L.n_sdk, H, kptr, kv, kflag);
         });

@@ -172,28 +172,36 @@ def test_lookup_shared_kmer_lists(gpu_ctx, n_share):
 
 
 
-@pytest.mark.parametrize("n_sdk,radix", [(3000, False), (200_000, False), (200_000, True)])
-def test_kmer_component_index_paths(gpu_ctx, monkeypatch, n_sdk, radix):
-    """kmer_component_index (ReadClusteringEngine.cpp:262-267, 282-284) by the bucketed sort (lookup.hip
-    lk_kci_*: an MSD pass on the top KmerID bits, then per bucket a count by KmerID and each KmerID's reads
-    sorted): 3000 SDKs put every hit in ONE bucket of more than its 32 K LDS pairs, so the kernel flags it
-    and the index is rebuilt by the radix path; 200 K SDKs spread the hits over 64 buckets; HGA_KCI_RADIX
-    forces the radix path.  Every CSR output equals the oracle's."""
-    if radix:
-        monkeypatch.setenv("HGA_KCI_RADIX", "1")
+@pytest.mark.parametrize("n_sdk,mode", [(3000, "bucketed"), (3000, "overflow"), (200_000, "bucketed"),
+                                        (200_000, "radix")])
+def test_kmer_component_index_paths(gpu_ctx, monkeypatch, n_sdk, mode):
+    """kmer_component_index (ReadClusteringEngine.cpp:262-267, 282-284) by the default radix path and by
+    the opt-in bucketed sort (HGA_KCI_BUCKETED=1, lookup.hip lk_kci_*: an MSD pass on the top KmerID bits,
+    then per bucket a count by KmerID and each KmerID's reads sorted); "overflow" gives one KmerID more
+    reads than a bucket's 15 K LDS pairs, so the kernel flags it and the index is rebuilt by the radix
+    path.  Every CSR output equals the oracle's."""
+    if mode != "radix":
+        monkeypatch.setenv("HGA_KCI_BUCKETED", "1")
     rng = np.random.default_rng(n_sdk)
     k = 17
     g = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 20_000 if n_sdk < 4096 else 400_000))
-    reads, L = [], 0
-    for _ in range(6000):
+    n_reads = 16_000 if mode == "overflow" else 6000
+    reads = []
+    for _ in range(n_reads):
         s = int(rng.integers(0, len(g) - 200))
         r = g[s:s + int(rng.integers(60, 200))]
-        reads.append(r)
+        reads.append(g[:k] + r if mode == "overflow" else r)   # every read holds the genome's first k-mer
     codes, _ = oracle.kmer_windows(g, k)
     pool = np.unique(codes)
+    if mode == "overflow":
+        pool = pool[pool != codes[0]]
     sdk = rng.choice(pool, n_sdk, replace=False).astype(np.uint64)
+    if mode == "overflow":
+        sdk[0] = codes[0]
     bases = b"".join(reads)
     offsets = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
     exp = oracle.construct_indices(bases, offsets, k, sdk, 1)
     assert len(exp["kci_read"]) > (32768 if n_sdk < 4096 else 200_000)
+    if mode == "overflow":
+        assert int(np.diff(exp["kci_ptr"]).max()) > 15 * 1024
     assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 1), exp)
