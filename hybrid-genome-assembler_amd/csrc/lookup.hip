@@ -567,61 +567,175 @@ __global__ void lk_ptr(const uint32_t* __restrict__ idx, uint64_t H, uint64_t ns
 
 // ---- kmer_component_index without LSD radix passes (ReadClusteringEngine.cpp:262-267, 282-284) ----
 // The hits arrive in read order; kmer_component_index is, per KmerID, its reads ascending (with
-// duplicates).  One MSD pass on the top D KmerID bits (per-tile LDS histograms, a column scan of them:
-// deterministic offsets, no global atomics) scatters (low KmerID bits, read) pairs into <= 4096 buckets;
-// one workgroup per bucket then counts its pairs into 2^S sub-buckets = single KmerIDs (S = kbits - D <=
-// 12), which gives kci_ptr directly, places the reads by sub-bucket in LDS and each thread sorts its
-// KmerIDs' reads (insertion sort of ~11 at C3; Shell sort for a crowded one) — the order a stable sort
-// by KmerID leaves them in.  Replaces three 8-bit LSD passes (upsweep + downsweep each) and lk_ptr.
-constexpr int KC_T = 512, KC_I = 64;
-constexpr uint32_t KC_TILE = KC_T * KC_I;   // hits per histogram / scatter tile (32 K: ~625 tiles at C3)
-constexpr int KC_DMAX = 12, KC_SMAX = 12;
-constexpr int KC_CT = 1024, KC_PT = 15;     // bucket-sort workgroup, pairs a thread holds in registers
-constexpr uint32_t KC_CAP = KC_CT * KC_PT;  // pairs per bucket (60 KB of u32 reads + 16 KB of counters in LDS: two workgroups a CU)
-// per tile: counts of the top D KmerID bits, stored bucket-major (rows[b][tile]) for lk_kci_bscan
-__global__ void __launch_bounds__(KC_T) lk_kci_hist(const uint32_t* __restrict__ hk, uint64_t H, int sh, uint32_t nb,
+// duplicates).  The top D KmerID bits (D <= 14) pick a bucket of ~2.5 K hits: one or two MSD passes of
+// <= 7 bits each move (KmerID, read) pairs there — per tile a 128-way LDS counting sort, so every digit's
+// run leaves the tile as one contiguous write (a single 4096-way pass writes 8-B runs: 0.51 ms at C3,
+// the pattern of profiles/r05_slab_probe.txt); deterministic offsets from per-tile digit counts, no
+// global atomics.  Then one workgroup per bucket counts its pairs into 2^S sub-buckets = single KmerIDs
+// (S = kbits - D <= 10), which gives kci_ptr directly, places the reads by sub-bucket in LDS and each
+// thread sorts its KmerIDs' reads (insertion sort of ~10 at C3; Shell sort for a crowded one) — the
+// order a stable sort by KmerID leaves them in.  Replaces three 8-bit LSD passes and lk_ptr.
+constexpr int KC_T = 512, KC_I = 16;
+constexpr uint32_t KC_TILE = KC_T * KC_I;   // pairs per MSD tile (64 KB of LDS stage)
+constexpr int KC_DMAX = 14, KC_SMAX = 10, KC_PASS_BITS = 7;
+constexpr int KC_CT = 256, KC_PT = 16;      // bucket-sort workgroup, pairs a thread holds in registers
+constexpr uint32_t KC_CAP = KC_CT * KC_PT;  // pairs per bucket (16 KB of u32 reads + 4 KB of counters in LDS: 8 workgroups a CU)
+static_assert((1 << KC_SMAX) <= 4 * KC_CT, "lk_kci_bsort scans four sub-bucket counts a thread");
+
+// An MSD tile: SEG = false, tile t of the hit arrays; SEG = true, tile t - tstart[s] of segment s
+// (the previous pass's digit s at [sbase[s], sbase[s] + stot[s])).  Returns false past the last tile.
+template <bool SEG>
+__device__ __forceinline__ bool msd_tile(uint32_t t, uint64_t H, const uint32_t* tstart, const uint32_t* sbase,
+                                         const uint32_t* stot, uint32_t& seg, uint64_t& lo, uint32_t& n) {
+    if constexpr (!SEG) {
+        seg = 0;
+        lo = (uint64_t)t * KC_TILE;
+        if (lo >= H) return false;
+        n = (uint32_t)min<uint64_t>(H - lo, KC_TILE);
+        return true;
+    } else {
+        if (t >= tstart[1u << KC_PASS_BITS]) return false;
+        uint32_t a = 0, b = 1u << KC_PASS_BITS;   // the last segment with tstart <= t
+        while (b - a > 1) {
+            const uint32_t m = (a + b) / 2;
+            if (tstart[m] <= t) a = m; else b = m;
+        }
+        seg = a;
+        const uint32_t j = t - tstart[a];
+        lo = (uint64_t)sbase[a] + (uint64_t)j * KC_TILE;
+        n = min(stot[a] - j * KC_TILE, KC_TILE);
+        return true;
+    }
+}
+template <bool SEG>
+__device__ __forceinline__ uint64_t msd_item(const uint32_t* hk, const uint32_t* hr, const uint64_t* pin, uint64_t i) {
+    if constexpr (SEG) return pin[i];
+    else return ((uint64_t)hk[i] << 32) | hr[i];
+}
+// per tile: counts of its digits (KmerID >> sh, nd of them), stored digit-major (rows[d][tile])
+template <bool SEG>
+__global__ void __launch_bounds__(KC_T) lk_msd_hist(const uint32_t* __restrict__ hk, const uint64_t* __restrict__ pin,
+                                                    uint64_t H, int sh, uint32_t nd, const uint32_t* __restrict__ tstart,
+                                                    const uint32_t* __restrict__ sbase, const uint32_t* __restrict__ stot,
                                                     uint32_t tiles, uint32_t* __restrict__ rows) {
-    __shared__ uint32_t h[1 << KC_DMAX];
-    for (uint32_t i = threadIdx.x; i < nb; i += KC_T) h[i] = 0;
+    __shared__ uint32_t h[1 << KC_PASS_BITS];
+    uint32_t seg, n;
+    uint64_t lo;
+    if (!msd_tile<SEG>(blockIdx.x, H, tstart, sbase, stot, seg, lo, n)) return;
+    if (threadIdx.x < nd) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * KC_TILE;
-#pragma unroll 8
-    for (int j = 0; j < KC_I; ++j) {
-        const uint64_t i = base + (uint64_t)j * KC_T + threadIdx.x;
-        if (i < H) atomicAdd(&h[hk[i] >> sh], 1u);
+    const uint32_t dm = nd - 1;
+#pragma unroll
+    for (int q = 0; q < KC_I; ++q) {
+        const uint32_t i = threadIdx.x + (uint32_t)q * KC_T;
+        if (i < n) {
+            const uint32_t k = SEG ? (uint32_t)(pin[lo + i] >> 32) : hk[lo + i];
+            atomicAdd(&h[(k >> sh) & dm], 1u);
+        }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nb; i += KC_T) rows[(uint64_t)i * tiles + blockIdx.x] = h[i];
+    if (threadIdx.x < nd) rows[(uint64_t)threadIdx.x * tiles + blockIdx.x] = h[threadIdx.x];
 }
-// One wave per bucket: its tiles' counts -> exclusive offsets inside the bucket (in place, coalesced over
-// the bucket's row), tot[b] = the bucket's size
-__global__ void __launch_bounds__(256) lk_kci_bscan(uint32_t* __restrict__ rows, uint32_t tiles, uint32_t nb,
+// One wave per (segment s, digit d): the tiles tstart[s] .. tstart[s+1] of row d -> exclusive offsets
+// inside (s, d) (in place), tot[s * nd + d] = its size.  tstart == nullptr: one segment of all tiles.
+__global__ void __launch_bounds__(256) lk_msd_bscan(uint32_t* __restrict__ rows, uint32_t tiles, uint32_t nd,
+                                                    uint32_t nseg, const uint32_t* __restrict__ tstart,
                                                     uint32_t* __restrict__ tot) {
-    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (b >= nb) return;
-    uint32_t* __restrict__ r = rows + (uint64_t)b * tiles;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= nseg * nd) return;
+    const uint32_t sg = w / nd, d = w % nd;
+    const uint32_t t0 = tstart ? tstart[sg] : 0u, t1 = tstart ? tstart[sg + 1] : tiles;
+    uint32_t* __restrict__ r = rows + (uint64_t)d * tiles;
     uint32_t run = 0;
-    for (uint32_t t0 = 0; t0 < tiles; t0 += 64) {
-        const uint32_t t = t0 + lane;
-        const uint32_t c = t < tiles ? r[t] : 0u;
+    for (uint32_t tb = t0; tb < t1; tb += 64) {
+        const uint32_t t = tb + lane;
+        const uint32_t c = t < t1 ? r[t] : 0u;
         const uint32_t inc = wave_incl_scan(c, (int)lane);
-        if (t < tiles) r[t] = run + inc - c;
+        if (t < t1) r[t] = run + inc - c;
         run += __shfl(inc, 63, 64);
     }
-    if (lane == 0) tot[b] = run;
+    if (lane == 0) tot[w] = run;
 }
-// bbase[b] = exclusive scan of tot (nb <= 4096: one 1024-thread workgroup, four a thread); stat[0] = the
-// largest bucket
+// Tiles of the second pass: tstart[s] = sum of ceil(tot[s'] / KC_TILE) over s' < s (<= 128 segments;
+// past nseg the total)
+__global__ void lk_msd_tiles(const uint32_t* __restrict__ tot, uint32_t nseg, uint32_t* __restrict__ tstart) {
+    if (threadIdx.x != 0) return;
+    uint32_t o = 0;
+    for (uint32_t sg = 0; sg <= (1u << KC_PASS_BITS); ++sg) {
+        tstart[sg] = o;
+        if (sg < nseg) o += (tot[sg] + KC_TILE - 1) / KC_TILE;
+    }
+}
+// Per tile: a 64-way counting sort of its pairs in LDS by digit, then each digit's run written
+// contiguously at obase[seg * nd + d] + the tile's offset inside (seg, d) (lk_msd_bscan)
+template <bool SEG>
+__global__ void __launch_bounds__(KC_T) lk_msd_scatter(const uint32_t* __restrict__ hk, const uint32_t* __restrict__ hr,
+                                                       const uint64_t* __restrict__ pin, uint64_t H, int sh, uint32_t nd,
+                                                       const uint32_t* __restrict__ tstart, const uint32_t* __restrict__ sbase,
+                                                       const uint32_t* __restrict__ stot, uint32_t tiles,
+                                                       const uint32_t* __restrict__ rows, const uint32_t* __restrict__ obase,
+                                                       uint64_t* __restrict__ out) {
+    __shared__ uint64_t st[KC_TILE];
+    __shared__ uint32_t cnt[1 << KC_PASS_BITS], lst[1 << KC_PASS_BITS];
+    __shared__ unsigned long long gof[1 << KC_PASS_BITS];
+    uint32_t seg, n;
+    uint64_t lo;
+    if (!msd_tile<SEG>(blockIdx.x, H, tstart, sbase, stot, seg, lo, n)) return;
+    const uint32_t tid = threadIdx.x, dm = nd - 1;
+    if (tid < nd) cnt[tid] = 0;   // (nd <= 128 < KC_T)
+    __syncthreads();
+    uint64_t it[KC_I];
+    uint32_t rk[KC_I];
+#pragma unroll
+    for (int q = 0; q < KC_I; ++q) {
+        const uint32_t i = tid + (uint32_t)q * KC_T;
+        it[q] = i < n ? msd_item<SEG>(hk, hr, pin, lo + i) : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < KC_I; ++q)
+        if (tid + (uint32_t)q * KC_T < n) rk[q] = atomicAdd(&cnt[((uint32_t)(it[q] >> 32) >> sh) & dm], 1u);
+    __syncthreads();
+    if (tid < 64) {   // one wave scans the <= 128 digit counts, two a lane
+        const uint32_t c0 = 2 * tid < nd ? cnt[2 * tid] : 0u, c1 = 2 * tid + 1 < nd ? cnt[2 * tid + 1] : 0u;
+        const uint32_t inc = wave_incl_scan(c0 + c1, (int)tid);
+        if (2 * tid < nd) {
+            lst[2 * tid] = inc - c0 - c1;
+            gof[2 * tid] = (unsigned long long)obase[seg * nd + 2 * tid] + rows[(uint64_t)(2 * tid) * tiles + blockIdx.x];
+        }
+        if (2 * tid + 1 < nd) {
+            lst[2 * tid + 1] = inc - c1;
+            gof[2 * tid + 1] = (unsigned long long)obase[seg * nd + 2 * tid + 1] +
+                               rows[(uint64_t)(2 * tid + 1) * tiles + blockIdx.x];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KC_I; ++q)
+        if (tid + (uint32_t)q * KC_T < n) st[lst[((uint32_t)(it[q] >> 32) >> sh) & dm] + rk[q]] = it[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KC_I; ++q) {
+        const uint32_t i = tid + (uint32_t)q * KC_T;
+        if (i < n) {
+            const uint64_t v = st[i];
+            const uint32_t d = ((uint32_t)(v >> 32) >> sh) & dm;
+            out[gof[d] + (i - lst[d])] = v;
+        }
+    }
+}
+// bbase[b] = exclusive scan of tot (nb <= 16384: one 1024-thread workgroup, sixteen a thread); stat[0] =
+// the largest bucket
 __global__ void __launch_bounds__(1024) lk_kci_scan(const uint32_t* __restrict__ tot, uint32_t nb,
                                                     uint32_t* __restrict__ bbase, unsigned long long* __restrict__ stat) {
+    constexpr int V = (1 << KC_DMAX) / 1024;
     __shared__ uint32_t ws[1024 / 64 + 1];
     __shared__ uint32_t mx;
     const uint32_t t = threadIdx.x;
     if (t == 0) mx = 0;
-    uint32_t v[4], sum = 0, m = 0;
+    uint32_t v[V], sum = 0, m = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t i = 4 * t + (uint32_t)q;
+    for (int q = 0; q < V; ++q) {
+        const uint32_t i = V * t + (uint32_t)q;
         v[q] = i < nb ? tot[i] : 0u;
         sum += v[q];
         m = max(m, v[q]);
@@ -629,8 +743,8 @@ __global__ void __launch_bounds__(1024) lk_kci_scan(const uint32_t* __restrict__
     uint32_t total;
     uint32_t o = block_excl_scan<1024>(sum, ws, &total);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t i = 4 * t + (uint32_t)q;
+    for (int q = 0; q < V; ++q) {
+        const uint32_t i = V * t + (uint32_t)q;
         if (i < nb) bbase[i] = o;
         o += v[q];
     }
@@ -638,32 +752,10 @@ __global__ void __launch_bounds__(1024) lk_kci_scan(const uint32_t* __restrict__
     __syncthreads();
     if (t == 0) stat[0] = mx;
 }
-// Per tile: its pairs to their buckets at bbase[b] + the tile's offset inside b (lk_kci_bscan), ranks
-// inside the tile by LDS atomics (the order inside a bucket is re-sorted by lk_kci_bsort)
-__global__ void __launch_bounds__(KC_T) lk_kci_scatter(const uint32_t* __restrict__ hk, const uint32_t* __restrict__ hr,
-                                                       uint64_t H, int sh, uint32_t nb, uint32_t tiles,
-                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ bbase,
-                                                       uint64_t* __restrict__ pairs) {
-    __shared__ uint32_t cur[1 << KC_DMAX];
-    const uint32_t t = blockIdx.x;
-    for (uint32_t b = threadIdx.x; b < nb; b += KC_T) cur[b] = bbase[b] + off[(uint64_t)b * tiles + t];
-    __syncthreads();
-    const uint64_t base = (uint64_t)t * KC_TILE;
-    const uint32_t smask = (1u << sh) - 1u;
-#pragma unroll 8
-    for (int j = 0; j < KC_I; ++j) {
-        const uint64_t i = base + (uint64_t)j * KC_T + threadIdx.x;
-        if (i < H) {
-            const uint32_t k = hk[i];
-            const uint32_t pos = atomicAdd(&cur[k >> sh], 1u);
-            pairs[pos] = ((uint64_t)(k & smask) << 32) | hr[i];
-        }
-    }
-}
 // One workgroup per bucket: sub-bucket counts -> kci_ptr of its KmerIDs, reads placed by KmerID in LDS,
 // each KmerID's reads sorted ascending, written to kci_val.  A bucket past KC_CAP sets *flag (the host
 // redoes the index by the radix path).
-__global__ void __launch_bounds__(KC_CT, 8) lk_kci_bsort(const uint64_t* __restrict__ pairs, const uint32_t* __restrict__ tot,
+__global__ void __launch_bounds__(KC_CT) lk_kci_bsort(const uint64_t* __restrict__ pairs, const uint32_t* __restrict__ tot,
                                                       const uint32_t* __restrict__ bbase, int S, uint64_t n_sdk,
                                                       uint64_t H, uint64_t* __restrict__ kptr, uint32_t* __restrict__ kv,
                                                       unsigned long long* __restrict__ flag) {
@@ -682,10 +774,12 @@ __global__ void __launch_bounds__(KC_CT, 8) lk_kci_bsort(const uint64_t* __restr
     __syncthreads();
     const uint64_t* __restrict__ src = pairs + st;
     uint64_t pr[KC_PT];   // the bucket is read once: all loads in flight, then the ranks by LDS atomics
+    const uint64_t smask = ((1ull << S) - 1ull) << 32;
 #pragma unroll
-    for (int q = 0; q < KC_PT; ++q) {
+    for (int q = 0; q < KC_PT; ++q) {   // (KmerID, read) -> (its low S bits, read)
         const uint32_t i = tid + (uint32_t)q * KC_CT;
-        pr[q] = i < n ? src[i] : 0ull;
+        const uint64_t v = i < n ? src[i] : 0ull;
+        pr[q] = (v & smask) | (uint32_t)v;
     }
 #pragma unroll
     for (int q = 0; q < KC_PT; ++q)   // the rank inside the sub-bucket joins the high word (sub < 2^12, rank < 2^14)
@@ -1317,18 +1411,14 @@ void lookup_run(hga_ctx* c) {
     uint64_t* kptr = static_cast<uint64_t*>(L.kci_ptr.ensure(((uint64_t)L.n_sdk + 1) * 8));
     uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(std::max<uint64_t>(H, 1) * 4));
     ++L.kci_epoch;
-    // kmer_component_index: the bucketed sort (lk_kci_*) when every bucket fits a workgroup's LDS, else
-    // (with HGA_KCI_BUCKETED=1) or a stable radix sort of the read-ordered hits by KmerID + lk_ptr
+    // kmer_component_index: the bucketed sort (lk_msd_* + lk_kci_*) when every bucket fits a workgroup's
+    // LDS, else (or with HGA_KCI_RADIX) a stable radix sort of the read-ordered hits by KmerID + lk_ptr
     // D top KmerID bits pick the bucket: at least kbits - KC_SMAX (sub-buckets = KmerIDs fit the LDS
-    // counters) and enough buckets for ~6 K hits each (KC_CAP = 16 K a bucket), at most KC_DMAX
+    // counters) and enough buckets for ~2.5 K hits each (KC_CAP = 4 K a bucket), at most KC_DMAX
     int kD = kbits > KC_SMAX ? kbits - KC_SMAX : 0;
-    while (kD < KC_DMAX && kD < kbits && (H >> kD) > 6000) ++kD;
+    while (kD < KC_DMAX && kD < kbits && (H >> kD) > 2500) ++kD;
     const int kS = kbits - kD;
-    // measured at C3 (round 6): lk_kci_scatter 0.51 ms (8-B runs into 4096 buckets, the write pattern of
-    // profiles/r05_slab_probe.txt), bsort 0.17, hist 0.08: 0.78 ms against the radix path's 0.58 — so the
-    // radix path is the default and the bucketed one is opt-in (HGA_KCI_BUCKETED=1)
-    const char* kb_env = std::getenv("HGA_KCI_BUCKETED");
-    const bool bucketed = H && kD <= KC_DMAX && kb_env && *kb_env == '1';
+    const bool bucketed = H && kD <= KC_DMAX && !std::getenv("HGA_KCI_RADIX");
     auto radix_kci = [&] {
         uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
         radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
@@ -1340,23 +1430,54 @@ void lookup_run(hga_ctx* c) {
     };
     unsigned long long* kflag = nullptr;
     if (bucketed) {
-        const uint32_t nbk = 1u << kD, tiles = (uint32_t)((H + KC_TILE - 1) / KC_TILE);
-        const size_t rows_b = (size_t)tiles * nbk * 4;
-        char* kt = static_cast<char*>(L.kci_tmp.ensure(64 + rows_b + 2 * (size_t)nbk * 4 + H * 8 + 256));
+        // pass A on the top D1 bucket bits, pass B (if D2 > 0) on the next D2 inside each A digit
+        const int D1 = kD > KC_PASS_BITS ? kD - KC_PASS_BITS : kD, D2 = kD - D1;
+        const uint32_t ndA = 1u << D1, ndB = 1u << D2, nbk = 1u << kD;
+        const uint32_t tilesA = (uint32_t)((H + KC_TILE - 1) / KC_TILE), tilesB = D2 ? tilesA + ndA : 0u;
+        const size_t rowsA_b = (size_t)tilesA * ndA * 4, rowsB_b = (size_t)tilesB * ndB * 4;
+        const size_t small_b = 64 + rowsA_b + rowsB_b + (128 + 128 + 256) * 4 + 2 * (size_t)nbk * 4;
+        const size_t pairs_off = (small_b + 255) & ~(size_t)255;
+        char* kt = static_cast<char*>(L.kci_tmp.ensure(pairs_off + 2 * H * 8));
         kflag = reinterpret_cast<unsigned long long*>(kt);
-        uint32_t* rows = reinterpret_cast<uint32_t*>(kt + 64);
-        uint32_t* tot = reinterpret_cast<uint32_t*>(kt + 64 + rows_b);
+        uint32_t* rowsA = reinterpret_cast<uint32_t*>(kt + 64);
+        uint32_t* rowsB = reinterpret_cast<uint32_t*>(kt + 64 + rowsA_b);
+        uint32_t* totA = reinterpret_cast<uint32_t*>(kt + 64 + rowsA_b + rowsB_b);
+        uint32_t* baseA = totA + 128;
+        uint32_t* tstart = baseA + 128;
+        uint32_t* tot = tstart + 256;
         uint32_t* bbase = tot + nbk;
-        uint64_t* pairs = reinterpret_cast<uint64_t*>(kt + ((64 + rows_b + 2 * (size_t)nbk * 4 + 255) & ~(size_t)255));
+        uint64_t* pairsA = reinterpret_cast<uint64_t*>(kt + pairs_off);
+        uint64_t* pairsB = pairsA + H;
+        const int shA = kS + D2, shB = kS;
         HGA_HIP(hipMemsetAsync(kflag, 0, 64, c->stream));
         c->launch("lk_kci", [&] {
-            hipLaunchKernelGGL(lk_kci_hist, dim3(tiles), dim3(KC_T), 0, c->stream, hk, H, kS, nbk, tiles, rows);
-            hipLaunchKernelGGL(lk_kci_bscan, dim3(blocks_for(nbk, 4)), dim3(256), 0, c->stream, rows, tiles, nbk, tot);
-            hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)tot, nbk, bbase, kflag + 1);
-            hipLaunchKernelGGL(lk_kci_scatter, dim3(tiles), dim3(KC_T), 0, c->stream, hk, hr, H, kS, nbk, tiles,
-                               (const uint32_t*)rows, (const uint32_t*)bbase, pairs);
-            hipLaunchKernelGGL(lk_kci_bsort, dim3(nbk), dim3(KC_CT), 0, c->stream, (const uint64_t*)pairs,
-                               (const uint32_t*)tot, (const uint32_t*)bbase, kS, (uint64_t)L.n_sdk, H, kptr, kv, kflag);
+            hipLaunchKernelGGL(lk_msd_hist<false>, dim3(tilesA), dim3(KC_T), 0, c->stream, hk, (const uint64_t*)nullptr, H,
+                               shA, ndA, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                               tilesA, rowsA);
+            hipLaunchKernelGGL(lk_msd_bscan, dim3(blocks_for(ndA, 4)), dim3(256), 0, c->stream, rowsA, tilesA, ndA, 1u,
+                               (const uint32_t*)nullptr, totA);
+            hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)totA, ndA, baseA, kflag + 1);
+            hipLaunchKernelGGL(lk_msd_scatter<false>, dim3(tilesA), dim3(KC_T), 0, c->stream, hk, hr,
+                               (const uint64_t*)nullptr, H, shA, ndA, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr, tilesA, (const uint32_t*)rowsA, (const uint32_t*)baseA,
+                               D2 ? pairsA : pairsB);
+            if (D2) {
+                hipLaunchKernelGGL(lk_msd_tiles, dim3(1), dim3(64), 0, c->stream, (const uint32_t*)totA, ndA, tstart);
+                hipLaunchKernelGGL(lk_msd_hist<true>, dim3(tilesB), dim3(KC_T), 0, c->stream, (const uint32_t*)nullptr,
+                                   (const uint64_t*)pairsA, H, shB, ndB, (const uint32_t*)tstart, (const uint32_t*)baseA,
+                                   (const uint32_t*)totA, tilesB, rowsB);
+                hipLaunchKernelGGL(lk_msd_bscan, dim3(blocks_for(nbk, 4)), dim3(256), 0, c->stream, rowsB, tilesB, ndB,
+                                   ndA, (const uint32_t*)tstart, tot);
+                hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)tot, nbk, bbase,
+                                   kflag + 1);
+                hipLaunchKernelGGL(lk_msd_scatter<true>, dim3(tilesB), dim3(KC_T), 0, c->stream, (const uint32_t*)nullptr,
+                                   (const uint32_t*)nullptr, (const uint64_t*)pairsA, H, shB, ndB, (const uint32_t*)tstart,
+                                   (const uint32_t*)baseA, (const uint32_t*)totA, tilesB, (const uint32_t*)rowsB,
+                                   (const uint32_t*)bbase, pairsB);
+            }
+            hipLaunchKernelGGL(lk_kci_bsort, dim3(nbk), dim3(KC_CT), 0, c->stream, (const uint64_t*)pairsB,
+                               (const uint32_t*)(D2 ? tot : totA), (const uint32_t*)(D2 ? bbase : baseA), kS,
+                               (uint64_t)L.n_sdk, H, kptr, kv, kflag);
         });
         c->check_launch("lk_kci");
     } else if (H) {

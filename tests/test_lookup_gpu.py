@@ -173,19 +173,20 @@ def test_lookup_shared_kmer_lists(gpu_ctx, n_share):
 
 
 @pytest.mark.parametrize("n_sdk,mode", [(3000, "bucketed"), (3000, "overflow"), (200_000, "bucketed"),
-                                        (200_000, "radix")])
+                                        (200_000, "two_pass"), (200_000, "radix")])
 def test_kmer_component_index_paths(gpu_ctx, monkeypatch, n_sdk, mode):
-    """kmer_component_index (ReadClusteringEngine.cpp:262-267, 282-284) by the default radix path and by
-    the opt-in bucketed sort (HGA_KCI_BUCKETED=1, lookup.hip lk_kci_*: an MSD pass on the top KmerID bits,
-    then per bucket a count by KmerID and each KmerID's reads sorted); "overflow" gives one KmerID more
-    reads than a bucket's 15 K LDS pairs, so the kernel flags it and the index is rebuilt by the radix
-    path.  Every CSR output equals the oracle's."""
-    if mode != "radix":
-        monkeypatch.setenv("HGA_KCI_BUCKETED", "1")
+    """kmer_component_index (ReadClusteringEngine.cpp:262-267, 282-284) by the bucketed sort (lookup.hip
+    lk_msd_* + lk_kci_*: one or two <= 128-way MSD passes on the top KmerID bits, then per bucket a count
+    by KmerID and each KmerID's reads sorted) and by the radix path (HGA_KCI_RADIX=1).  3000 SDKs: one MSD
+    pass; 200 K SDKs: two passes (256 buckets; "two_pass": 40 K reads, ~2 M hits, 1024 buckets); "overflow"
+    gives one KmerID more reads than a bucket's 4 K LDS pairs, so the kernel flags it and the index is
+    rebuilt by the radix path.  Every CSR output equals the oracle's."""
+    if mode == "radix":
+        monkeypatch.setenv("HGA_KCI_RADIX", "1")
     rng = np.random.default_rng(n_sdk)
     k = 17
     g = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 20_000 if n_sdk < 4096 else 400_000))
-    n_reads = 16_000 if mode == "overflow" else 6000
+    n_reads = {"overflow": 16_000, "two_pass": 40_000}.get(mode, 6000)
     reads = []
     for _ in range(n_reads):
         s = int(rng.integers(0, len(g) - 200))
@@ -201,7 +202,7 @@ def test_kmer_component_index_paths(gpu_ctx, monkeypatch, n_sdk, mode):
     bases = b"".join(reads)
     offsets = np.cumsum([0] + [len(r) for r in reads]).astype(np.uint64)
     exp = oracle.construct_indices(bases, offsets, k, sdk, 1)
-    assert len(exp["kci_read"]) > (32768 if n_sdk < 4096 else 200_000)
+    assert len(exp["kci_read"]) > (32768 if n_sdk < 4096 else 1_000_000 if mode == "two_pass" else 200_000)
     if mode == "overflow":
         assert int(np.diff(exp["kci_ptr"]).max()) > 15 * 1024
     assert_same(run_gpu(gpu_ctx, bases, offsets, k, sdk, 1), exp)
