@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 for so in "$@"; do
   n=$(basename $so .so)
-  HGA_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/bv_$n.json 2> gpurun_out/bv_$n.err || { echo "$n failed"; tail -3 gpurun_out/bv_$n.err; exit 1; }
+  HGA_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu --no-scale --no-ingest > gpurun_out/bv_$n.json 2> gpurun_out/bv_$n.err || { echo "$n failed"; tail -3 gpurun_out/bv_$n.err; exit 1; }
   python3 - "$n" <<'PY'
 import json, sys
 n = sys.argv[1]
