@@ -359,11 +359,17 @@ __device__ bool cn_block_pivot(const CnIn& in, const CnOut& out, uint32_t p, uin
             __syncthreads();
             cn_owner_scan(L.own, L.sh + 2);
             uint32_t cand[CN_U];
+            uint32_t ob[CN_U];
+#pragma unroll
+            for (int u = 0; u < CN_U; ++u) ob[u] = L.own[t + CN_T * u];   // (j - w0 < CN_W) all LDS reads first
+            decltype(+L.lo[0]) lb[CN_U];
+#pragma unroll
+            for (int u = 0; u < CN_U; ++u) lb[u] = L.lo[ob[u]];
 #pragma unroll
             for (int u = 0; u < CN_U; ++u) {
                 const uint32_t j = w0 + t + CN_T * u;
                 cand[u] = CN_EMPTY;
-                if (j < T) cand[u] = in.kci[L.lo[L.own[j - w0]] + j];
+                if (j < T) cand[u] = in.kci[lb[u] + j];
             }
 #pragma unroll
             for (int u = 0; u < CN_U; ++u)
@@ -584,12 +590,23 @@ __global__ void __launch_bounds__(64 * CNW_WAVES, HGA_CNW_MINW) cn_wave(CnIn in,
                 wave_lds_sync();
                 W.own[lane] = nv;
                 wave_lds_sync();
+                // the owners and their list bases read for all eight pairs first (unpredicated: j - w0 <
+                // CNW_W, an owner < 64), so the LDS reads wait twice per window instead of twice per pair
+                // before its candidate load can issue
                 uint32_t cand[CNW_U];
+                uint32_t ob[CNW_U];
+                uint64_t cb[CNW_U];
+#pragma unroll
+                for (int u = 0; u < CNW_U; ++u) ob[u] = own8[lane + 64 * u];
+#pragma unroll
+                for (int u = 0; u < CNW_U; ++u) cb[u] = W.base[ob[u]];
 #pragma unroll
                 for (int u = 0; u < CNW_U; ++u) {
                     const uint32_t j = w0 + lane + 64 * u;
                     cand[u] = CN_EMPTY;
-                    if (j < T) cand[u] = *reinterpret_cast<const uint32_t*>(W.base[own8[j - w0]] + 4ull * j);
+                    // a global (not flat) load: flat loads count in lgkmcnt with the LDS reads, so each
+                    // LDS wait would also wait for the candidate loads issued before it
+                    if (j < T) cand[u] = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(cb[u] + 4ull * j);
                 }
                 // a candidate already at its home slot (most walks repeat a candidate) is one count add;
                 // the rest go through the wave's queue and are inserted with every lane busy (a lane's own

@@ -885,7 +885,9 @@ __global__ void __launch_bounds__(MG_NT) kx_xb_merge(const uint64_t* __restrict_
             const uint32_t mid = (lo + hi) >> 1;
             if (rpre[mid] <= i) lo = mid; else hi = mid;
         }
-        return reinterpret_cast<const uint64_t*>(rst[lo])[i - rpre[lo]];
+        // a global (not flat) load: flat loads count in lgkmcnt, so the next piece's binary search in
+        // LDS would wait for this load
+        return reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(rst[lo])[i - rpre[lo]];
     };
     const uint64_t hbase = sizeof(KT) == 4 ? (u_first + u) << lowbits : 0ull;
     merge_bucket<T, FMAX, true>(L, ld, m, ubase[u], u, pf, mx, sizeof(KT) == 4 ? (1ull << lowbits) - 1 : kmask, hbase,

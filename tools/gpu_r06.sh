@@ -37,9 +37,9 @@ if has sq; then
            "SQ_BUSY_CU_CYCLES SQ_CYCLES SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC SQ_WAIT_INST_ANY SQ_INSTS_SMEM"; do
     n=$(echo $p | cut -d" " -f1)_$(echo $p | cut -d" " -f2)
     (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $p --output-format csv -d $R/gpurun_out/sq_${TAG}_$n -o run -- \
-      python3 $R/tools/kprof.py --reps 2 --lookup > $R/gpurun_out/sq_${TAG}_$n.log 2>&1) || { echo "pmc $n failed"; tail -3 gpurun_out/sq_${TAG}_$n.log; exit 1; }
+      python3 $R/tools/kprof.py --reps 2 --connections > $R/gpurun_out/sq_${TAG}_$n.log 2>&1) || { echo "pmc $n failed"; tail -3 gpurun_out/sq_${TAG}_$n.log; exit 1; }
   done
-  python3 tools/pmc_raw.py "gpurun_out/sq_${TAG}_*" kc_bin1 kc_rebin kc_count_s lk_scan > gpurun_out/sq_${TAG}.txt
+  python3 tools/pmc_raw.py "gpurun_out/sq_${TAG}_*" kc_bin1 kc_rebin kc_count_s lk_scan cn_wave > gpurun_out/sq_${TAG}.txt
   head -80 gpurun_out/sq_${TAG}.txt
 fi
 if has var; then
