@@ -719,10 +719,25 @@ int ClusteringEngine::approximate_read_overlap(ComponentID x, ComponentID y) con
 std::pair<std::vector<ComponentID>, std::vector<ComponentID>> ClusteringEngine::spanning_tree_tails(
     const SpanningTree& tree) const {
     std::map<ComponentID, std::map<ComponentID, int>> adjacency;
-    for (auto& edge : tree) {
-        const int dist = approximate_read_overlap(edge.first, edge.second);
-        adjacency[edge.first].emplace(edge.second, dist);
-        adjacency[edge.second].emplace(edge.first, dist);
+    // the edges' overlaps (an intersection of two merged components' KmerID lists each: the stage's
+    // cost) on the host threads, then the adjacency built in tree order as before
+    std::vector<int> ov(tree.size());
+    {
+        const int T = std::max(1, std::min<int>(host_threads(), (int)(tree.size() / 8) + 1));
+        std::atomic<size_t> next{0};
+        auto work = [&] {
+            size_t q;
+            while ((q = next.fetch_add(1)) < tree.size()) ov[q] = approximate_read_overlap(tree[q].first, tree[q].second);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t) th.emplace_back(work);
+        work();
+        for (auto& x : th) x.join();
+    }
+    for (size_t q = 0; q < tree.size(); ++q) {
+        const auto& edge = tree[q];
+        adjacency[edge.first].emplace(edge.second, ov[q]);
+        adjacency[edge.second].emplace(edge.first, ov[q]);
     }
     if (adjacency.empty()) return {};
     auto distance_bfs = [&](ComponentID start) {
@@ -780,12 +795,23 @@ std::vector<ComponentID> ClusteringEngine::amplify_component(const std::vector<C
 std::vector<Connection> ClusteringEngine::core_component_connections(
     const std::vector<std::pair<ComponentList, SpanningTree>>& comps_and_trees) {
     std::map<ComponentID, std::pair<std::vector<KmerID>, std::vector<KmerID>>> tails_map;
+    // HGA_TIMING=1: the stage's parts summed over the scaffold components ("hga-timing tails.<part> <ms>")
+    using clk = std::chrono::steady_clock;
+    double t_tree = 0, t_amp = 0, t_acc = 0;
+    auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     for (auto& ct : comps_and_trees) {
+        auto t0 = clk::now();
         const auto tails = spanning_tree_tails(ct.second);
+        t_tree += since(t0);
+        t0 = clk::now();
         const auto lv = amplify_component(tails.first, (Score)(int)cfg_.tail_amplification_min_score);
         const auto rv = amplify_component(tails.second, (Score)(int)cfg_.tail_amplification_min_score);
+        t_amp += since(t0);
+        t0 = clk::now();
         tails_map.emplace(ct.first[0], std::make_pair(accumulate_kmer_ids(lv), accumulate_kmer_ids(rv)));
+        t_acc += since(t0);
     }
+    const auto t_int0 = clk::now();
     std::vector<Connection> edges;
     for (auto& a : tails_map)
         for (auto& b : tails_map)
@@ -797,6 +823,10 @@ std::vector<Connection> ClusteringEngine::core_component_connections(
                 edges.push_back({a.first, b.first, *std::max_element(s, s + 4), is_good(a.first, b.first)});
             }
     sort_connections(edges);
+    if (const char* te = std::getenv("HGA_TIMING"); te && std::string(te) == "1")
+        std::fprintf(stderr, "hga-timing tails.spanning_tree_tails %.2f\nhga-timing tails.amplify %.2f\n"
+                             "hga-timing tails.accumulate %.2f\nhga-timing tails.intersections %.2f\n",
+                     t_tree, t_amp, t_acc, since(t_int0));
     return filter_connections(edges, [](const Connection& c) { return c.score > 0; });
 }
 
