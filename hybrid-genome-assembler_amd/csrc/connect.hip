@@ -538,12 +538,16 @@ __global__ void __launch_bounds__(64 * CNW_WAVES, HGA_CNW_MINW) cn_wave(CnIn in,
         }
         wave_lds_sync();
         bool ok = true;
+        // the chunk's KmerIDs were requested one chunk ahead (their latency behind the previous chunk's walk)
+        uint32_t nkid = b + lane < e ? in.skid[b + lane] : 0u;
         for (uint64_t cb = b; cb < e && ok; cb += 64) {
             const uint64_t i = cb + lane;
             uint32_t len = 0;
             uint64_t first = 0;   // byte address of the hit's first read index
+            const uint32_t ckid = nkid;
+            if (cb + 64 < e) nkid = cb + 64 + lane < e ? in.skid[cb + 64 + lane] : 0u;
             if (i < e) {
-                const uint32_t kid = in.skid[i];
+                const uint32_t kid = ckid;
                 if (in.slots) {   // one 128-B slot: header and (short) list in the same line
                     const uint32_t* sl = in.slots + (uint64_t)kid * SLOT_W;
                     const uint4 h = *reinterpret_cast<const uint4*>(sl);
