@@ -1606,16 +1606,24 @@ __device__ __forceinline__ uint32_t spec_index(uint32_t prev, uint32_t total, co
 // SG_S groups in flight per thread; one workgroup per CU, whose LDS histogram is flushed with
 // one global atomic per nonzero bin.  Totals in [TL, TD) (rare) go to the dense global
 // histogram directly (ctrl[3] counts them), >= TD to an overflow list.
+// bnd (n_thr <= 8, else null): per total t < TL the eight u16 boundaries b_i = the smallest prev with
+// thr[i] <= spec(prev, t) (spec_index's expression, evaluated on the host; 0xFFFF: none, and for the
+// unused entries) — spec is monotone in prev, so spec_index(prev, t) = #{i : prev >= b_i}: eight integer
+// compares instead of a double division per row (C4 shard: 1.47 -> 0.8 ms)
 __global__ void __launch_bounds__(NT_S) kc_spec_hist(const uint32_t* __restrict__ cnt, uint64_t rows,
                                                      const unsigned long long* __restrict__ rows_dev,
                                                      uint64_t cap, uint32_t F,
                                                      const double* __restrict__ thr, uint32_t n_thr,
+                                                     const uint4* __restrict__ bnd,
                                                      unsigned long long* __restrict__ hist,
                                                      unsigned long long* __restrict__ over,
                                                      unsigned long long* __restrict__ ctrl,
                                                      uint64_t over_cap) {
     extern __shared__ uint32_t lh[];   // n_thr * TL counters (sized at launch)
+    __shared__ uint4 sb[TL];
     for (uint32_t i = threadIdx.x; i < n_thr * TL; i += NT_S) lh[i] = 0;
+    if (bnd)
+        for (uint32_t i = threadIdx.x; i < TL; i += NT_S) sb[i] = bnd[i];
     if (rows_dev) {   // count_run not settled yet: the row cursor it left on the device (<= cap)
         const uint64_t r = *rows_dev;
         rows = r < cap ? r : cap;
@@ -1659,7 +1667,18 @@ __global__ void __launch_bounds__(NT_S) kc_spec_hist(const uint32_t* __restrict_
             for (int j = 0; j < 4; ++j) {
                 if (g * 4 + j >= rows) continue;
                 const uint32_t total = tot[u][j];
-                const uint32_t ti = spec_index(prv[u][j], total, thr, n_thr);
+                uint32_t ti;
+                if (bnd && total < TL) {
+                    const uint4 b = sb[total];
+                    const uint32_t pv = prv[u][j];
+                    const uint32_t w[4] = {b.x, b.y, b.z, b.w};
+                    ti = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        ti += (pv >= (w[q] & 0xFFFFu) ? 1u : 0u) + (pv >= (w[q] >> 16) ? 1u : 0u);
+                } else {
+                    ti = spec_index(prv[u][j], total, thr, n_thr);
+                }
                 if (ti >= n_thr) { atomicOr(&ctrl[1], 1ull); continue; }
                 if (total < TL) {
                     atomicAdd(&lh[ti * TL + total], 1u);
@@ -2708,7 +2727,7 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     const uint64_t over_cap = 1u << 20;
     const size_t hbytes = (size_t)MAX_THR * TD * 8;
     const bool fresh = s.hist_dense.cap == 0;
-    char* base = static_cast<char*>(s.hist_dense.ensure(hbytes + over_cap * 8 + 256 + 64));
+    char* base = static_cast<char*>(s.hist_dense.ensure(hbytes + over_cap * 8 + 256 + 64 + (size_t)TL * 16));
     auto* hist = reinterpret_cast<unsigned long long*>(base);
     auto* over = reinterpret_cast<unsigned long long*>(base + hbytes);
     auto* ctrl = reinterpret_cast<unsigned long long*>(base + hbytes + over_cap * 8);
@@ -2725,8 +2744,24 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
     std::memcpy(hthr, thr.data(), n_thr * 8);
     // hist is kept clear by kc_hist_compact, ctrl by kc_spec_publish
     if (fresh) HGA_HIP(hipMemsetAsync(base, 0, hbytes + over_cap * 8 + 256, c->stream));
+    auto* dbnd = reinterpret_cast<uint4*>(base + hbytes + over_cap * 8 + 256 + 64);
+    const bool use_bnd = n_thr <= 8 && !std::getenv("HGA_SPEC_FP64");
     if (fresh || s.thr_dev != thr) {   // the same thresholds as last time are already there
         HGA_HIP(hipMemcpyAsync(dthr, hthr, n_thr * 8, hipMemcpyHostToDevice, c->stream));
+        if (n_thr <= 8) {   // the per-total boundaries of kc_spec_hist (its comment), same IEEE expression
+            std::vector<uint16_t> b((size_t)TL * 8, 0xFFFF);
+            for (uint32_t t = 1; t < TL; ++t)
+                for (uint32_t i = 0; i < n_thr; ++i) {
+                    uint32_t lo = 0, hi = t + 1;   // smallest prev in [0, t] passing, t + 1 = none
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) / 2;
+                        const volatile double x = (double)mid / (double)t;
+                        if (thr[i] <= x * 100.0) hi = mid; else lo = mid + 1;
+                    }
+                    b[(size_t)t * 8 + i] = lo > t ? 0xFFFF : (uint16_t)lo;
+                }
+            HGA_HIP(hipMemcpy(dbnd, b.data(), b.size() * 2, hipMemcpyHostToDevice));
+        }
         s.thr_dev = thr;
     }
     // an unsettled count_run: rows come from its device cursor, the counters ride in this readback
@@ -2738,7 +2773,7 @@ void count_spec_hist(hga_ctx* c, const double* thr_in, uint32_t n_thr_in, std::v
         hipLaunchKernelGGL(kc_spec_hist, dim3(grid), dim3(NT_S), (size_t)n_thr * TL * 4, c->stream,
                            s.rows_cnt.as<uint32_t>(), rows_hint,
                            pend ? static_cast<const unsigned long long*>(s.cursor.p) : nullptr, s.rows_cap, s.n_files,
-                           dthr, n_thr,
+                           dthr, n_thr, use_bnd ? (const uint4*)dbnd : nullptr,
                            hist, over, ctrl, over_cap);
     });
     c->check_launch("kc_spec_hist");

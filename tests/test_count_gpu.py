@@ -78,6 +78,29 @@ def test_count_random_vs_oracle(gpu_ctx, k):
     assert_same(run_gpu(gpu_ctx, streams, k, 2, 6), o)
 
 
+@pytest.mark.parametrize("thr", [(100.01,), (50.0, 75.0, 100.01), (33.333333333333336, 50.0, 60.0, 66.66666666666667,
+                                                                    75.0, 80.0, 100.0, 100.01),
+                                 tuple(range(10, 101, 10)) + (100.01, 200.0)])
+def test_spec_hist_thresholds(gpu_ctx, thr):
+    """kc_spec_hist's per-total boundary table (n_thr <= 8: integer compares against boundaries computed on
+    the host with the same IEEE expression) and its double path (more thresholds, totals >= 1024): the
+    histogram equals the oracle's for thresholds that ratios hit exactly (1/2, 3/4, 2/3 ...), three files,
+    and a few k-mers repeated past 1024 instances."""
+    rng = random.Random(11)
+    reads = [[], [], []]
+    for _ in range(400):   # a distinct 25-base read repeated (a, b, c) times: ratios like 1/2, 2/3, 3/4
+        r = "".join(rng.choice("ACGT") for _ in range(25)).encode()
+        for f in range(3):
+            reads[f] += [r] * rng.choice([0, 0, 1, 2, 3, 4, 6, 8, 9, 12])
+    reads[0] += [b"ACGTTGCAACGTAGGCTAACG"] * 1500
+    reads[1] += [b"ACGTTGCAACGTAGGCTAACG"] * 700
+    streams = [b"\n".join(x) for x in reads]
+    o = oracle.count_pipeline(streams, 19, 2, 9, thresholds=list(thr))
+    r = run_gpu(gpu_ctx, streams, 19, 2, 9, thr=list(thr))
+    assert int(o["counts"].sum(1).max()) >= 1024
+    assert np.array_equal(r["hist"], o["hist"])
+
+
 @pytest.mark.parametrize("n_files", [1, 3, 5])
 @pytest.mark.parametrize("min_count", [1, 2, 3])
 def test_count_files_and_min(gpu_ctx, n_files, min_count):
