@@ -98,9 +98,16 @@ hga_status hga_ctx_destroy(hga_ctx* c) {
     return guard([&] {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
-        hipStream_t s = c->stream;
+        if (c->side) (void)hipStreamSynchronize(c->side);
+        hipStream_t s = c->stream, s2 = c->side;
+        hipEvent_t e1 = c->ev_fork, e2 = c->ev_join;
         delete c;
         (void)hipStreamDestroy(s);
+        if (s2) {
+            (void)hipEventDestroy(e1);
+            (void)hipEventDestroy(e2);
+            (void)hipStreamDestroy(s2);
+        }
     });
 }
 

@@ -232,6 +232,18 @@ struct Comm {
 struct hga_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // a second stream for work that overlaps the main stream's (lookup.hip: kmer_component_index beside
+    // the per-read sorts), forked and joined with these two events; created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t side_stream() {
+        if (!side) {
+            HGA_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+            HGA_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+            HGA_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+        }
+        return side;
+    }
     int num_cu = 256;
     hga::Profiler prof;
     hga::CountState count;
@@ -258,6 +270,21 @@ struct hga_ctx {
         HGA_HIP(hipEventRecord(a, stream));
         f();
         HGA_HIP(hipEventRecord(b, stream));
+        prof.pending.push_back({name, a, b});
+        if (prof.pending.size() > 4096) prof.drain();
+    }
+    // the same on another stream (events recorded on that stream)
+    template <class F>
+    void launch_on(const char* name, hipStream_t s, F&& f) {
+        if (!prof.on || (!prof.only.empty() &&
+                         std::find(prof.only.begin(), prof.only.end(), name) == prof.only.end())) {
+            f();
+            return;
+        }
+        hipEvent_t a = prof.get(), b = prof.get();
+        HGA_HIP(hipEventRecord(a, s));
+        f();
+        HGA_HIP(hipEventRecord(b, s));
         prof.pending.push_back({name, a, b});
         if (prof.pending.size() > 4096) prof.drain();
     }

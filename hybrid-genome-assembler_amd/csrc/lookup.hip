@@ -1365,6 +1365,90 @@ void lookup_run(hga_ctx* c) {
         });
         c->check_launch("lk_emit");
     }
+    // kmer_component_index (ReadClusteringEngine.cpp:262-267, 282-284), from the read-ordered hits
+    bool kjoin = false;
+    uint64_t* kptr = static_cast<uint64_t*>(L.kci_ptr.ensure(((uint64_t)L.n_sdk + 1) * 8));
+    uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(std::max<uint64_t>(H, 1) * 4));
+    ++L.kci_epoch;
+    // kmer_component_index: the bucketed sort (lk_msd_* + lk_kci_*) when every bucket fits a workgroup's
+    // LDS, else (or with HGA_KCI_RADIX) a stable radix sort of the read-ordered hits by KmerID + lk_ptr
+    // D top KmerID bits pick the bucket: at least kbits - KC_SMAX (sub-buckets = KmerIDs fit the LDS
+    // counters) and enough buckets for ~2.5 K hits each (KC_CAP = 4 K a bucket), at most KC_DMAX
+    int kD = kbits > KC_SMAX ? kbits - KC_SMAX : 0;
+    while (kD < KC_DMAX && kD < kbits && (H >> kD) > 2500) ++kD;
+    const int kS = kbits - kD;
+    const bool bucketed = H && kD <= KC_DMAX && !std::getenv("HGA_KCI_RADIX");
+    auto radix_kci = [&] {
+        uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
+        radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
+        c->launch("lk_post", [&] {
+            hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(H + 1, 256)), dim3(256), 0, c->stream, (const uint32_t*)kk, H,
+                               (uint64_t)L.n_sdk, kptr);
+        });
+        c->check_launch("lk_ptr");
+    };
+    unsigned long long* kflag = nullptr;
+    if (bucketed) {
+        // pass A on the top D1 bucket bits, pass B (if D2 > 0) on the next D2 inside each A digit
+        const int D1 = kD > KC_PASS_BITS ? kD - KC_PASS_BITS : kD, D2 = kD - D1;
+        const uint32_t ndA = 1u << D1, ndB = 1u << D2, nbk = 1u << kD;
+        const uint32_t tilesA = (uint32_t)((H + KC_TILE - 1) / KC_TILE), tilesB = D2 ? tilesA + ndA : 0u;
+        const size_t rowsA_b = (size_t)tilesA * ndA * 4, rowsB_b = (size_t)tilesB * ndB * 4;
+        const size_t small_b = 64 + rowsA_b + rowsB_b + (128 + 128 + 256) * 4 + 2 * (size_t)nbk * 4;
+        const size_t pairs_off = (small_b + 255) & ~(size_t)255;
+        char* kt = static_cast<char*>(L.kci_tmp.ensure(pairs_off + 2 * H * 8));
+        kflag = reinterpret_cast<unsigned long long*>(kt);
+        uint32_t* rowsA = reinterpret_cast<uint32_t*>(kt + 64);
+        uint32_t* rowsB = reinterpret_cast<uint32_t*>(kt + 64 + rowsA_b);
+        uint32_t* totA = reinterpret_cast<uint32_t*>(kt + 64 + rowsA_b + rowsB_b);
+        uint32_t* baseA = totA + 128;
+        uint32_t* tstart = baseA + 128;
+        uint32_t* tot = tstart + 256;
+        uint32_t* bbase = tot + nbk;
+        uint64_t* pairsA = reinterpret_cast<uint64_t*>(kt + pairs_off);
+        uint64_t* pairsB = pairsA + H;
+        const int shA = kS + D2, shB = kS;
+        // on the ctx's side stream, forked here: it overlaps the per-read sort and first-occurrence
+        // kernels below (independent: they read sk / sv, this reads hk / hr); joined before the read-back
+        hipStream_t ks = c->side_stream();
+        HGA_HIP(hipEventRecord(c->ev_fork, c->stream));
+        HGA_HIP(hipStreamWaitEvent(ks, c->ev_fork, 0));
+        HGA_HIP(hipMemsetAsync(kflag, 0, 64, ks));
+        c->launch_on("lk_kci", ks, [&] {
+            hipLaunchKernelGGL(lk_msd_hist<false>, dim3(tilesA), dim3(KC_T), 0, ks, hk, (const uint64_t*)nullptr, H,
+                               shA, ndA, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                               tilesA, rowsA);
+            hipLaunchKernelGGL(lk_msd_bscan, dim3(blocks_for(ndA, 4)), dim3(256), 0, ks, rowsA, tilesA, ndA, 1u,
+                               (const uint32_t*)nullptr, totA);
+            hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, ks, (const uint32_t*)totA, ndA, baseA, kflag + 1);
+            hipLaunchKernelGGL(lk_msd_scatter<false>, dim3(tilesA), dim3(KC_T), 0, ks, hk, hr,
+                               (const uint64_t*)nullptr, H, shA, ndA, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr, tilesA, (const uint32_t*)rowsA, (const uint32_t*)baseA,
+                               D2 ? pairsA : pairsB);
+            if (D2) {
+                hipLaunchKernelGGL(lk_msd_tiles, dim3(1), dim3(64), 0, ks, (const uint32_t*)totA, ndA, tstart);
+                hipLaunchKernelGGL(lk_msd_hist<true>, dim3(tilesB), dim3(KC_T), 0, ks, (const uint32_t*)nullptr,
+                                   (const uint64_t*)pairsA, H, shB, ndB, (const uint32_t*)tstart, (const uint32_t*)baseA,
+                                   (const uint32_t*)totA, tilesB, rowsB);
+                hipLaunchKernelGGL(lk_msd_bscan, dim3(blocks_for(nbk, 4)), dim3(256), 0, ks, rowsB, tilesB, ndB,
+                                   ndA, (const uint32_t*)tstart, tot);
+                hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, ks, (const uint32_t*)tot, nbk, bbase,
+                                   kflag + 1);
+                hipLaunchKernelGGL(lk_msd_scatter<true>, dim3(tilesB), dim3(KC_T), 0, ks, (const uint32_t*)nullptr,
+                                   (const uint32_t*)nullptr, (const uint64_t*)pairsA, H, shB, ndB, (const uint32_t*)tstart,
+                                   (const uint32_t*)baseA, (const uint32_t*)totA, tilesB, (const uint32_t*)rowsB,
+                                   (const uint32_t*)bbase, pairsB);
+            }
+            hipLaunchKernelGGL(lk_kci_bsort, dim3(nbk), dim3(KC_CT), 0, ks, (const uint64_t*)pairsB,
+                               (const uint32_t*)(D2 ? tot : totA), (const uint32_t*)(D2 ? bbase : baseA), kS,
+                               (uint64_t)L.n_sdk, H, kptr, kv, kflag);
+        });
+        c->check_launch("lk_kci");
+        HGA_HIP(hipEventRecord(c->ev_join, ks));
+        kjoin = true;
+    } else if (H) {
+        radix_kci();
+    }
     // hit_ptr over reads
     auto* ctr = static_cast<unsigned long long*>(L.first_flag.ensure(64));
     HGA_HIP(hipMemsetAsync(ctr, 0, 32, c->stream));
@@ -1408,81 +1492,6 @@ void lookup_run(hga_ctx* c) {
         c->check_launch("lk_first_write");
     }
     uint64_t* fptr = static_cast<uint64_t*>(L.first_ptr.ensure((n + 1) * 8));
-    uint64_t* kptr = static_cast<uint64_t*>(L.kci_ptr.ensure(((uint64_t)L.n_sdk + 1) * 8));
-    uint32_t* kv = static_cast<uint32_t*>(L.kci_val.ensure(std::max<uint64_t>(H, 1) * 4));
-    ++L.kci_epoch;
-    // kmer_component_index: the bucketed sort (lk_msd_* + lk_kci_*) when every bucket fits a workgroup's
-    // LDS, else (or with HGA_KCI_RADIX) a stable radix sort of the read-ordered hits by KmerID + lk_ptr
-    // D top KmerID bits pick the bucket: at least kbits - KC_SMAX (sub-buckets = KmerIDs fit the LDS
-    // counters) and enough buckets for ~2.5 K hits each (KC_CAP = 4 K a bucket), at most KC_DMAX
-    int kD = kbits > KC_SMAX ? kbits - KC_SMAX : 0;
-    while (kD < KC_DMAX && kD < kbits && (H >> kD) > 2500) ++kD;
-    const int kS = kbits - kD;
-    const bool bucketed = H && kD <= KC_DMAX && !std::getenv("HGA_KCI_RADIX");
-    auto radix_kci = [&] {
-        uint32_t* kk = static_cast<uint32_t*>(L.kci_key.ensure(H * 4));
-        radix_sort_u32_from(c, hk, hr, kk, kv, H, kbits, L.scratch2);
-        c->launch("lk_post", [&] {
-            hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(H + 1, 256)), dim3(256), 0, c->stream, (const uint32_t*)kk, H,
-                               (uint64_t)L.n_sdk, kptr);
-        });
-        c->check_launch("lk_ptr");
-    };
-    unsigned long long* kflag = nullptr;
-    if (bucketed) {
-        // pass A on the top D1 bucket bits, pass B (if D2 > 0) on the next D2 inside each A digit
-        const int D1 = kD > KC_PASS_BITS ? kD - KC_PASS_BITS : kD, D2 = kD - D1;
-        const uint32_t ndA = 1u << D1, ndB = 1u << D2, nbk = 1u << kD;
-        const uint32_t tilesA = (uint32_t)((H + KC_TILE - 1) / KC_TILE), tilesB = D2 ? tilesA + ndA : 0u;
-        const size_t rowsA_b = (size_t)tilesA * ndA * 4, rowsB_b = (size_t)tilesB * ndB * 4;
-        const size_t small_b = 64 + rowsA_b + rowsB_b + (128 + 128 + 256) * 4 + 2 * (size_t)nbk * 4;
-        const size_t pairs_off = (small_b + 255) & ~(size_t)255;
-        char* kt = static_cast<char*>(L.kci_tmp.ensure(pairs_off + 2 * H * 8));
-        kflag = reinterpret_cast<unsigned long long*>(kt);
-        uint32_t* rowsA = reinterpret_cast<uint32_t*>(kt + 64);
-        uint32_t* rowsB = reinterpret_cast<uint32_t*>(kt + 64 + rowsA_b);
-        uint32_t* totA = reinterpret_cast<uint32_t*>(kt + 64 + rowsA_b + rowsB_b);
-        uint32_t* baseA = totA + 128;
-        uint32_t* tstart = baseA + 128;
-        uint32_t* tot = tstart + 256;
-        uint32_t* bbase = tot + nbk;
-        uint64_t* pairsA = reinterpret_cast<uint64_t*>(kt + pairs_off);
-        uint64_t* pairsB = pairsA + H;
-        const int shA = kS + D2, shB = kS;
-        HGA_HIP(hipMemsetAsync(kflag, 0, 64, c->stream));
-        c->launch("lk_kci", [&] {
-            hipLaunchKernelGGL(lk_msd_hist<false>, dim3(tilesA), dim3(KC_T), 0, c->stream, hk, (const uint64_t*)nullptr, H,
-                               shA, ndA, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
-                               tilesA, rowsA);
-            hipLaunchKernelGGL(lk_msd_bscan, dim3(blocks_for(ndA, 4)), dim3(256), 0, c->stream, rowsA, tilesA, ndA, 1u,
-                               (const uint32_t*)nullptr, totA);
-            hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)totA, ndA, baseA, kflag + 1);
-            hipLaunchKernelGGL(lk_msd_scatter<false>, dim3(tilesA), dim3(KC_T), 0, c->stream, hk, hr,
-                               (const uint64_t*)nullptr, H, shA, ndA, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
-                               (const uint32_t*)nullptr, tilesA, (const uint32_t*)rowsA, (const uint32_t*)baseA,
-                               D2 ? pairsA : pairsB);
-            if (D2) {
-                hipLaunchKernelGGL(lk_msd_tiles, dim3(1), dim3(64), 0, c->stream, (const uint32_t*)totA, ndA, tstart);
-                hipLaunchKernelGGL(lk_msd_hist<true>, dim3(tilesB), dim3(KC_T), 0, c->stream, (const uint32_t*)nullptr,
-                                   (const uint64_t*)pairsA, H, shB, ndB, (const uint32_t*)tstart, (const uint32_t*)baseA,
-                                   (const uint32_t*)totA, tilesB, rowsB);
-                hipLaunchKernelGGL(lk_msd_bscan, dim3(blocks_for(nbk, 4)), dim3(256), 0, c->stream, rowsB, tilesB, ndB,
-                                   ndA, (const uint32_t*)tstart, tot);
-                hipLaunchKernelGGL(lk_kci_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)tot, nbk, bbase,
-                                   kflag + 1);
-                hipLaunchKernelGGL(lk_msd_scatter<true>, dim3(tilesB), dim3(KC_T), 0, c->stream, (const uint32_t*)nullptr,
-                                   (const uint32_t*)nullptr, (const uint64_t*)pairsA, H, shB, ndB, (const uint32_t*)tstart,
-                                   (const uint32_t*)baseA, (const uint32_t*)totA, tilesB, (const uint32_t*)rowsB,
-                                   (const uint32_t*)bbase, pairsB);
-            }
-            hipLaunchKernelGGL(lk_kci_bsort, dim3(nbk), dim3(KC_CT), 0, c->stream, (const uint64_t*)pairsB,
-                               (const uint32_t*)(D2 ? tot : totA), (const uint32_t*)(D2 ? bbase : baseA), kS,
-                               (uint64_t)L.n_sdk, H, kptr, kv, kflag);
-        });
-        c->check_launch("lk_kci");
-    } else if (H) {
-        radix_kci();
-    }
     c->launch("lk_post", [&] {
         if (!H)   // with hits the first-occurrence scan above already left the CSR pointers in fptr
             hipLaunchKernelGGL(lk_ptr, dim3(blocks_for(U + 1, 256)), dim3(256), 0, c->stream,
@@ -1492,6 +1501,7 @@ void lookup_run(hga_ctx* c) {
                                H, (uint64_t)L.n_sdk, kptr);
     });
     c->check_launch("lk_ptr");
+    if (kjoin) HGA_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     unsigned long long hc[4], kf = 0;
     HGA_HIP(hipMemcpyAsync(hc, ctr, 32, hipMemcpyDeviceToHost, c->stream));
     if (H) HGA_HIP(hipMemcpyAsync(&U, fptr + n, 8, hipMemcpyDeviceToHost, c->stream));
