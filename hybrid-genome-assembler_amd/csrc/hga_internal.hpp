@@ -366,7 +366,7 @@ void lookup_load(hga_ctx* c, int k, const uint64_t* keys, uint32_t n);
 void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, uint64_t n,
                       uint32_t first_id);
 void lookup_run(hga_ctx* c);
-void lookup_pack(hga_ctx* c);   // per-base encode of the resident reads (lookup_run, hll_registers)
+void lookup_pack(hga_ctx* c, bool skip_codes = false);   // per-base encode of the resident reads (lookup_run, hll_registers)
 void lookup_sizes(hga_ctx* c, hga_lookup_sizes* out);
 void lookup_fetch(hga_ctx* c, const hga_lookup_result* out);
 void hll_registers(hga_ctx* c, int k, int b, uint8_t* regs);

@@ -1,8 +1,9 @@
 // lookup.hip — MI355X replacement for the per-read SDK lookup loop of
 // ReadClusteringEngine::construct_indices (src/clustering/ReadClusteringEngine.cpp:234-299).
 //
-//   lk_pack (pack_kernel<REF>)  reads -> 2-bit codes with KmerIterator semantics (non-ACGT
-//                 contributes 0 to both strands, KmerIterator.cpp:7-19,54-63) + valid bits.
+//   lk_pack       the read-start bitmap and word -> read map (the 2-bit codes with KmerIterator
+//                 semantics — non-ACGT contributes 0 to both strands, KmerIterator.cpp:7-19,54-63 — are
+//                 packed by lk_scan from the ASCII reads; pack_kernel<REF> only for hll_scan).
 //   lk_starts     read-start bitmap (1 bit per base): a window is in one read iff no read
 //                 starts inside (start, end].
 //   lk_build      read-only table {canonical code -> KmerID}, 5 keys + 5 ids per 64-B bucket,
@@ -35,6 +36,15 @@ namespace {
 #endif
 #ifndef HGA_LK_T
 #define HGA_LK_T 256
+#endif
+#ifndef HGA_LK_MINW
+#define HGA_LK_MINW 6   // lk_scan's count pass (compile-time k): 6 waves per SIMD, i.e. <= 80 VGPRs
+#endif
+#ifndef HGA_LK_ASCII
+// lk_scan packs its frames from the ASCII reads itself (four 16-B loads + the SWAR packer per thread),
+// so lookup_run has no codes pass: C3 lk_pack 0.23 -> 0.03 ms (the read-start bits and word -> read map
+// stay), lk_count 1.59 -> 1.72 ms, lookup 2.98 -> 2.92 ms (round 6); hll_scan packs for itself
+#define HGA_LK_ASCII 1
 #endif
 constexpr int LK_T = HGA_LK_T;   // lookup scan workgroup
 constexpr int LK_P = 32;                  // window ends per thread (frame of 4 words)
@@ -290,6 +300,7 @@ struct LkTab {
     const uint32_t* filt;
     uint64_t nbk, fmask;
     uint32_t idb;           // packed layout: KmerID bits of an entry (0: the 64-B layout)
+    const uint8_t* asc;     // the ASCII reads when lk_scan packs its frames itself (HGA_LK_ASCII), else null
 };
 
 // Canonical code of the window ending at p0+j (j compile-time after unrolling).
@@ -323,7 +334,7 @@ __device__ __forceinline__ uint64_t lk_canon_rt(const Frame<LK_P>& f, int j, uin
 // K > 0: k known at compile time (masks and the m-mer / k-mer widths fold, narrowing the 64-bit
 // hash multiplies); K == 0: any k.
 template <bool EMIT, int KM, int K = 0, bool PK = false>
-__global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk, const uint16_t* __restrict__ vd,
+__global__ void __launch_bounds__(LK_T, (!EMIT && K != 0) ? HGA_LK_MINW : 1) lk_scan(const uint32_t* __restrict__ pk, const uint16_t* __restrict__ vd,
                                                 const unsigned int* __restrict__ sb, uint64_t nbases,
                                                 const uint64_t* __restrict__ offs, uint64_t nreads, int k_rt,
                                                 const uint32_t* __restrict__ word_read,
@@ -350,7 +361,16 @@ __global__ void __launch_bounds__(LK_T) lk_scan(const uint32_t* __restrict__ pk,
         uint32_t hits = 0, ovf = 0;
         Frame<LK_P> f;
         if (p0 < nbases) {
-            const uint64_t v64 = load_frame<LK_P, true>(pk, vd, PAD_WORDS + p0 / 16 - 2, k, f);
+            uint64_t v64;
+            if (HGA_LK_ASCII && tab.asc) {   // the frame's four 16-base words packed from the ASCII reads
+                FrameRaw<LK_P> raw;
+#pragma unroll
+                for (int i = 0; i < FrameRaw<LK_P>::NW; ++i)
+                    pack_bytes<true>(load16(tab.asc, (int64_t)p0 - 32 + 16 * i, nbases), raw.x[i], raw.v[i]);
+                v64 = build_frame<LK_P, true>(raw, k, f);
+            } else {
+                v64 = load_frame<LK_P, true>(pk, vd, PAD_WORDS + p0 / 16 - 2, k, f);
+            }
             const uint32_t acgt = (uint32_t)(runs_of(v64, k) >> 32);   // window has only ACGT
             const uint64_t s64 = (uint64_t)sb[SB_PAD + p0 / 32 - 1] | ((uint64_t)sb[SB_PAD + p0 / 32] << 32);
             uint32_t wm = (uint32_t)(runs_of(~s64, k - 1) >> 32);   // no read start in (s, e]
@@ -1263,7 +1283,7 @@ void lookup_set_reads(hga_ctx* c, const char* bases, const uint64_t* offsets, ui
 // packed 2-bit codes + valid bits (pack_kernel<REF>), the read-start bitmap and the per-word read
 // index.  Part of every hga_lookup_run (the reference encodes inside construct_indices,
 // ReadClusteringEngine.cpp:248-254); hga_hll_registers packs when the reads changed since.
-void lookup_pack(hga_ctx* c) {
+void lookup_pack(hga_ctx* c, bool skip_codes) {
     auto& L = c->lookup;
     const uint64_t n = L.n_reads, nb = L.n_bases;
     const uint64_t nw = (nb + 15) / 16, tail = 64;
@@ -1281,7 +1301,7 @@ void lookup_pack(hga_ctx* c) {
     const uint64_t nwr = (nb + 31) / 32;
     uint32_t* wr = static_cast<uint32_t*>(L.word_read.ensure(std::max<uint64_t>(nwr, 1) * 4));
     c->launch("lk_pack", [&] {
-        if (nw)
+        if (nw && !skip_codes)
             hipLaunchKernelGGL(pack_kernel<true>, dim3(blocks_for(nw, 256)), dim3(256), 0, c->stream,
                                L.bases.as<uint8_t>(), nb, pk, vd, nw);
         if (n)
@@ -1289,7 +1309,7 @@ void lookup_pack(hga_ctx* c) {
                                n, nb, sb, wr);
     });
     c->check_launch("lk_pack");
-    L.packed_ok = true;
+    L.packed_ok = !skip_codes;
 }
 
 void lookup_run(hga_ctx* c) {
@@ -1302,7 +1322,7 @@ void lookup_run(hga_ctx* c) {
     HGA_REQUIRE(L.loaded, HGA_ERR_STATE, "hga_lookup_load not called");
     HGA_REQUIRE(L.have_reads, HGA_ERR_STATE, "hga_lookup_set_reads not called");
     c->conn.ready = false;
-    lookup_pack(c);
+    lookup_pack(c, HGA_LK_ASCII != 0);
     const uint64_t n = L.n_reads, nb = L.n_bases;
     const int k = L.k;
     uint64_t w = 0;
@@ -1321,7 +1341,8 @@ void lookup_run(hga_ctx* c) {
     const uint16_t* vd = L.valid.as<uint16_t>();
     const unsigned int* sb = L.starts.as<unsigned int>();
     const uint64_t* offs = L.offsets.as<uint64_t>();
-    LkTab tab{L.tab_key.p, L.filter.as<uint32_t>(), L.slots, L.fwords - 1, L.idb};
+    LkTab tab{L.tab_key.p, L.filter.as<uint32_t>(), L.slots, L.fwords - 1, L.idb,
+              HGA_LK_ASCII ? L.bases.as<uint8_t>() : nullptr};
     uint64_t H = 0;
     if (n_tiles) {
         c->launch("lk_count", [&] {
