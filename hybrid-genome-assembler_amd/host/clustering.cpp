@@ -9,6 +9,7 @@
 #include <cmath>
 #include <filesystem>
 #include <fstream>
+#include <functional>
 #include <limits>
 #include <memory>
 #include <mutex>
@@ -79,6 +80,62 @@ std::vector<std::pair<ComponentList, SpanningTree>> union_find(const std::vector
                                                                const std::set<ComponentID>& restricted,
                                                                int min_component_size, int max_component_size) {
     if (max_component_size == -1) max_component_size = INT_MAX;
+    // ids are read ids from one dense range: the same statements over flat arrays indexed by id - lo
+    // (hash maps cost ~90 ns an edge on C3's 2 M scaffold-forming connections); the result is in
+    // ascending root id, the std::map order of the general version below
+    ComponentID lo = UINT32_MAX, hi = 0;
+    for (const Connection& c : connections) {
+        lo = std::min({lo, c.x, c.y});
+        hi = std::max({hi, c.x, c.y});
+    }
+    if (!connections.empty() && (uint64_t)hi - lo < (1ull << 26)) {
+        const size_t N = (size_t)(hi - lo) + 1;
+        std::vector<ComponentID> parent(N, UINT32_MAX);   // UINT32_MAX: not a vertex
+        std::vector<ComponentList> comp(N);
+        std::vector<SpanningTree> tree(N);
+        std::vector<uint8_t> restr(N, 0);
+        for (const Connection& c : connections)
+            for (ComponentID v : {c.x, c.y})
+                if (parent[v - lo] == UINT32_MAX) {
+                    parent[v - lo] = v;
+                    comp[v - lo] = {v};
+                    restr[v - lo] = restricted.count(v) != 0;
+                }
+        auto root = [&](ComponentID v) {
+            ComponentID r = v;
+            while (parent[r - lo] != r) r = parent[r - lo];
+            while (parent[v - lo] != r) {
+                const ComponentID n = parent[v - lo];
+                parent[v - lo] = r;
+                v = n;
+            }
+            return r;
+        };
+        for (const Connection& c : connections) {
+            const ComponentID px = root(c.x), py = root(c.y);
+            if (px == py) continue;
+            if (restr[px - lo] && restr[py - lo]) continue;
+            if (comp[px - lo].size() + comp[py - lo].size() > (size_t)max_component_size) continue;
+            const bool xb = comp[px - lo].size() > comp[py - lo].size();
+            const ComponentID bigger = xb ? px : py, smaller = xb ? py : px;
+            auto& cb = comp[bigger - lo];
+            auto& cs = comp[smaller - lo];
+            for (ComponentID id : cs) parent[id - lo] = bigger;
+            cb.insert(cb.end(), cs.begin(), cs.end());
+            ComponentList().swap(cs);
+            auto& tb = tree[bigger - lo];
+            tb.emplace_back(c.x, c.y);
+            auto& ts = tree[smaller - lo];
+            tb.insert(tb.end(), ts.begin(), ts.end());
+            SpanningTree().swap(ts);
+            restr[bigger - lo] = restr[bigger - lo] || restr[smaller - lo];
+        }
+        std::vector<std::pair<ComponentList, SpanningTree>> result;
+        for (size_t i = 0; i < N; ++i)
+            if (parent[i] == lo + (ComponentID)i && comp[i].size() >= (size_t)(int64_t)min_component_size)
+                result.emplace_back(std::move(comp[i]), std::move(tree[i]));
+        return result;
+    }
     std::unordered_map<ComponentID, ComponentID> parents;
     std::map<ComponentID, ComponentList> components;
     std::unordered_map<ComponentID, SpanningTree> trees;
@@ -590,9 +647,26 @@ std::vector<KmerID> ClusteringEngine::accumulate_kmer_ids(const std::vector<Comp
 // by KmerID instead of an ordered map of vectors — on C3, where one component absorbs most reads
 // (~20 M pairs), the map took 17.8 s.  The kmer_component_index update runs over the host threads.
 std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<ComponentList>& components) {
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
     std::vector<ComponentID> merged_ids;
     const size_t nk = kci_.size();
-    std::vector<uint64_t> pairs;   // KmerID << 32 | component, in the reference's insertion order
+    const int HT = std::max(1, host_threads());
+    // ranges [0, n) split over up to HT threads (the calling thread takes the last one)
+    auto par = [&](size_t n, size_t grain, const std::function<void(int, size_t, size_t)>& f) {
+        const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)HT, n / std::max<size_t>(grain, 1)));
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) {
+            const size_t a = n * (size_t)t / (size_t)T, b = n * (size_t)(t + 1) / (size_t)T;
+            if (t + 1 == T) f(t, a, b);
+            else th.emplace_back(f, t, a, b);
+        }
+        for (auto& x : th) x.join();
+        return T;
+    };
+    // (KmerID << 32 | component) pairs, per thread; their order is irrelevant: each KmerID's removal
+    // list is sorted before use
+    std::vector<std::vector<uint64_t>> pairs((size_t)HT);
     std::vector<uint8_t> mark;
     for (const ComponentList& ids : components) {
         if (ids.empty()) continue;   // (an empty spectral cluster would dereference ids[0] there)
@@ -603,23 +677,31 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
         std::set<int32_t> cats;
         std::vector<uint32_t> contained;
         size_t total = 0;
-        for (ComponentID id : ids) {
-            Component& c = index_.at(id);
+        std::vector<const std::vector<KmerID>*> km(ids.size());
+        for (size_t i = 0; i < ids.size(); ++i) {
+            Component& c = index_.at(ids[i]);
             contained.insert(contained.end(), c.reads.begin(), c.reads.end());
             c.reads.clear();
             cats.insert(c.categories.begin(), c.categories.end());
             total += c.kmers.size();
+            km[i] = &c.kmers;
         }
         std::vector<KmerID> acc;
-        if (total > nk / 16 + 64) {   // accumulate_kmer_ids as a mark pass (ids < nk)
+        if (total > nk / 16 + 64) {   // accumulate_kmer_ids as a mark pass (ids < nk), both halves threaded
             if (mark.empty()) mark.assign(nk, 0);
-            for (ComponentID id : ids)
-                for (KmerID kid : index_.at(id).kmers) mark[kid] = 1;
-            for (size_t kid = 0; kid < nk; ++kid)
-                if (mark[kid]) {
-                    acc.push_back((KmerID)kid);
-                    mark[kid] = 0;
-                }
+            par(ids.size(), 64, [&](int, size_t a, size_t b) {
+                for (size_t i = a; i < b; ++i)
+                    for (KmerID kid : *km[i]) std::atomic_ref<uint8_t>(mark[kid]).store(1, std::memory_order_relaxed);
+            });
+            std::vector<std::vector<KmerID>> part((size_t)HT);
+            const int T = par(nk, 1 << 16, [&](int t, size_t a, size_t b) {
+                for (size_t kid = a; kid < b; ++kid)
+                    if (mark[kid]) {
+                        part[(size_t)t].push_back((KmerID)kid);
+                        mark[kid] = 0;
+                    }
+            });
+            for (int t = 0; t < T; ++t) acc.insert(acc.end(), part[(size_t)t].begin(), part[(size_t)t].end());
         } else {
             acc = accumulate_kmer_ids(ids);
         }
@@ -628,19 +710,66 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
         survivor.categories = cats;
         survivor.reads = contained;
         merged_ids.push_back(ids[0]);
-        for (ComponentID id : ids)
-            for (KmerID kid : index_.at(id).kmers) pairs.push_back((uint64_t)kid << 32 | id);
+        km[0] = &survivor.kmers;
+        par(ids.size(), 64, [&](int t, size_t a, size_t b) {
+            auto& pv = pairs[(size_t)t];
+            for (size_t i = a; i < b; ++i)
+                for (KmerID kid : *km[i]) pv.push_back((uint64_t)kid << 32 | ids[i]);
+        });
         pristine_ = false;
     }
-    if (pairs.empty()) return merged_ids;
-    // removal lists: counting sort of the pairs by KmerID
+    size_t npairs = 0;
+    for (auto& pv : pairs) npairs += pv.size();
+    if (npairs == 0) return merged_ids;
+    const auto t_groups = clk::now();
+    // removal lists: a counting sort of the pairs by KmerID over the threads without atomics — a count
+    // row per pair vector, per-KmerID totals and their prefix, then each vector's cursors per KmerID
+    // (its rows become cursors) and its own scatter
+    const size_t nv = pairs.size();
+    if (npairs >= UINT32_MAX) {   // (u32 cursors) one vector of everything, counted serially
+        for (size_t v = 1; v < nv; ++v) {
+            pairs[0].insert(pairs[0].end(), pairs[v].begin(), pairs[v].end());
+            std::vector<uint64_t>().swap(pairs[v]);
+        }
+    }
+    std::vector<std::vector<uint32_t>> cnt(nv);
+    par(nv, 1, [&](int, size_t a, size_t b) {
+        for (size_t v = a; v < b; ++v) {
+            if (pairs[v].empty()) continue;
+            cnt[v].assign(nk, 0);
+            for (uint64_t pr : pairs[v]) ++cnt[v][pr >> 32];
+        }
+    });
     std::vector<uint64_t> start(nk + 1, 0);
-    for (uint64_t p : pairs) ++start[(p >> 32) + 1];
+    par(nk, 1 << 14, [&](int, size_t a, size_t b) {
+        for (size_t k = a; k < b; ++k) {
+            uint64_t t = 0;
+            for (size_t v = 0; v < nv; ++v)
+                if (!cnt[v].empty()) t += cnt[v][k];
+            start[k + 1] = t;
+        }
+    });
     for (size_t k = 0; k < nk; ++k) start[k + 1] += start[k];
-    std::vector<ComponentID> rem(pairs.size());
-    {
+    if (npairs < UINT32_MAX) par(nk, 1 << 14, [&](int, size_t a, size_t b) {   // counts -> each vector's first slot per KmerID
+        for (size_t k = a; k < b; ++k) {
+            uint64_t o = start[k];
+            for (size_t v = 0; v < nv; ++v)
+                if (!cnt[v].empty()) {
+                    const uint32_t c = cnt[v][k];
+                    cnt[v][k] = (uint32_t)o;
+                    o += c;
+                }
+        }
+    });
+    std::vector<ComponentID> rem(npairs);
+    if (npairs >= UINT32_MAX) {
         std::vector<uint64_t> cur(start.begin(), start.end() - 1);
-        for (uint64_t p : pairs) rem[cur[p >> 32]++] = (ComponentID)p;
+        for (uint64_t pr : pairs[0]) rem[cur[pr >> 32]++] = (ComponentID)pr;
+    } else {
+        par(nv, 1, [&](int, size_t a, size_t b) {
+            for (size_t v = a; v < b; ++v)
+                for (uint64_t pr : pairs[v]) rem[cnt[v][pr >> 32]++] = (ComponentID)pr;
+        });
     }
     pairs.clear();
     pairs.shrink_to_fit();
@@ -682,6 +811,11 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
         k0 = e;
     }
     for (auto& x : th) x.join();
+    if (const char* te = std::getenv("HGA_TIMING"); te && std::string(te) == "1") {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "hga-timing merge.groups %.2f\nhga-timing merge.kci_update %.2f\n", ms(t_start, t_groups),
+                     ms(t_groups, clk::now()));
+    }
     return merged_ids;
 }
 
