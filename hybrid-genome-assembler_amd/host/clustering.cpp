@@ -1108,26 +1108,45 @@ void ClusteringEngine::export_components(const std::vector<ComponentID>& ids, co
                                          std::ostream& out) const {
     std::filesystem::remove_all(dir);
     std::filesystem::create_directories(dir);
-    std::map<ComponentID, std::ofstream> files;
-    std::unordered_map<uint32_t, ComponentID> read_to_component;
+    // one buffered file per component, every read written straight from the record set in read order
+    // (the same bytes as building each record's strings: no per-read copies)
+    std::map<ComponentID, std::FILE*> files;
+    std::vector<ComponentID> owner(reads_.size(), 0);   // 0: in no exported component (ids start at 1)
+    std::vector<std::unique_ptr<char[]>> bufs;
     for (ComponentID id : ids) {
-        files[id] = std::ofstream(dir + "/#" + std::to_string(id) + ".fa");
+        const std::string path = dir + "/#" + std::to_string(id) + ".fa";
+        std::FILE* f = std::fopen(path.c_str(), "wb");
+        if (!f) throw std::runtime_error("cannot write " + path);
+        bufs.emplace_back(new char[1 << 20]);
+        std::setvbuf(f, bufs.back().get(), _IOFBF, 1 << 20);
+        files[id] = f;
         const auto it = index_.find(id);
         if (it != index_.end())
-            for (uint32_t r : it->second.reads) read_to_component[r] = id;
+            for (uint32_t r : it->second.reads)
+                if (r >= first_id_ && r - first_id_ < reads_.size()) owner[r - first_id_] = id;
     }
     const bool text = reads_.headers.size() == reads_.size();
     for (uint64_t i = 0; i < reads_.size(); ++i) {
-        const auto it = read_to_component.find(first_id_ + (uint32_t)i);
-        if (it == read_to_component.end()) continue;
-        std::ofstream& f = files[it->second];
-        const std::string seq(reads_.bases.data() + reads_.offsets[i], reads_.offsets[i + 1] - reads_.offsets[i]);
-        const std::string hdr = text ? reads_.headers[i] : std::string();
-        const std::string qual = text ? reads_.qualities[i] : std::string();
-        if (qual.empty()) f << '>' << hdr << '\n' << seq << '\n';
-        else f << '@' << hdr << '\n' << seq << "\n+\n" << qual << '\n';
+        if (!owner[i]) continue;
+        std::FILE* f = files[owner[i]];
+        const char* seq = reads_.bases.data() + reads_.offsets[i];
+        const size_t len = reads_.offsets[i + 1] - reads_.offsets[i];
+        const std::string empty;
+        const std::string& hdr = text ? reads_.headers[i] : empty;
+        const std::string& qual = text ? reads_.qualities[i] : empty;
+        std::fputc(qual.empty() ? '>' : '@', f);
+        std::fwrite(hdr.data(), 1, hdr.size(), f);
+        std::fputc('\n', f);
+        std::fwrite(seq, 1, len, f);
+        if (qual.empty()) {
+            std::fputc('\n', f);
+        } else {
+            std::fwrite("\n+\n", 1, 3, f);
+            std::fwrite(qual.data(), 1, qual.size(), f);
+            std::fputc('\n', f);
+        }
     }
-    for (auto& kv : files) kv.second.close();
+    for (auto& kv : files) std::fclose(kv.second);
     out << "Exported " << ids.size() << " components\n";
 }
 
