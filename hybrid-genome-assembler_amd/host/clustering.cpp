@@ -528,36 +528,19 @@ ClusteringEngine::ClusteringEngine(const ClusteringConfig& cfg, bool debug, cons
     const uint64_t n = reads.size();
     if (hit_ptr_.size() != n + 1 || first_ptr_.size() != n + 1)
         throw std::invalid_argument("index arrays do not match the reads");
-    // the per-read components and the per-KmerID lists built on the host threads (1.9 M small vectors
-    // at C3), the components then inserted in id order (ascending keys: end hints)
-    const int T = std::max(1, host_threads());
-    auto par = [&](uint64_t m, const std::function<void(uint64_t, uint64_t)>& f) {
-        const int TT = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)T, m / 4096));
-        std::vector<std::thread> th;
-        for (int t = 0; t < TT; ++t) {
-            const uint64_t a = m * (uint64_t)t / (uint64_t)TT, b = m * (uint64_t)(t + 1) / (uint64_t)TT;
-            if (t + 1 == TT) f(a, b);
-            else th.emplace_back(f, a, b);
-        }
-        for (auto& x : th) x.join();
-    };
-    std::vector<Component> comp(n);
-    par(n, [&](uint64_t a, uint64_t b) {
-        for (uint64_t i = a; i < b; ++i) {   // construct_indices :256-276
-            if (hit_ptr_[i + 1] == hit_ptr_[i]) continue;
-            Component& c = comp[i];
-            c.reads = {first_id_ + (uint32_t)i};
-            c.kmers.assign(sorted_kid.begin() + (int64_t)hit_ptr_[i], sorted_kid.begin() + (int64_t)hit_ptr_[i + 1]);
-            c.categories = {reads.category[i]};
-        }
-    });
-    for (uint64_t i = 0; i < n; ++i)
-        if (hit_ptr_[i + 1] != hit_ptr_[i]) index_.emplace_hint(index_.end(), first_id_ + (uint32_t)i, std::move(comp[i]));
+    for (uint64_t i = 0; i < n; ++i) {   // construct_indices :256-276
+        if (hit_ptr_[i + 1] == hit_ptr_[i]) continue;
+        Component c;
+        c.reads = {first_id_ + (uint32_t)i};
+        c.kmers.assign(sorted_kid.begin() + (int64_t)hit_ptr_[i], sorted_kid.begin() + (int64_t)hit_ptr_[i + 1]);
+        c.categories = {reads.category[i]};
+        index_.emplace_hint(index_.end(), first_id_ + (uint32_t)i, std::move(c));
+    }
+    // (built serially: the same construction on the host threads measured slower, 100 -> 155 ms at C3 —
+    // 1.9 M small allocations contend in the allocator)
     kci_.resize(kci_ptr.empty() ? 0 : kci_ptr.size() - 1);
-    par(kci_.size(), [&](uint64_t a, uint64_t b) {
-        for (uint64_t k = a; k < b; ++k)
-            kci_[k].assign(kci_read.begin() + (int64_t)kci_ptr[k], kci_read.begin() + (int64_t)kci_ptr[k + 1]);
-    });
+    for (size_t k = 0; k + 1 < kci_ptr.size(); ++k)
+        kci_[k].assign(kci_read.begin() + (int64_t)kci_ptr[k], kci_read.begin() + (int64_t)kci_ptr[k + 1]);
 }
 
 uint32_t ClusteringEngine::read_length(ComponentID r) const {   // ReadMetaData::length
