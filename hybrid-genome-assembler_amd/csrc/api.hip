@@ -135,6 +135,11 @@ hga_status hga_connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t*
     HGA_CTX_GUARD(c, hga::connections_fetch(c, x, y, score, is_good));
 }
 
+hga_status hga_connections_fetch_range(hga_ctx* c, uint64_t first, uint64_t count, uint32_t* x, uint32_t* y,
+                                       uint64_t* score, uint8_t* is_good) {
+    HGA_CTX_GUARD(c, hga::connections_fetch(c, x, y, score, is_good, first, count));
+}
+
 hga_status hga_count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts,
                               uint64_t n) {
     HGA_CTX_GUARD(c, hga::count_add_rows(c, file, keys, counts, n));

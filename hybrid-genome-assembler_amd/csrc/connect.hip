@@ -1248,15 +1248,18 @@ void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_
     *n_out = n;
 }
 
-void connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good) {
+void connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good, uint64_t first,
+                       uint64_t count) {
     auto& S = c->conn;
     HGA_REQUIRE(S.ready, HGA_ERR_STATE, "hga_connections_run not called");
-    const uint64_t n = S.n;
+    const uint64_t a = std::min<uint64_t>(first, S.n), n = std::min<uint64_t>(count, S.n - a);
     if (n) {
-        if (x) HGA_HIP(hipMemcpyAsync(x, S.ox.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-        if (y) HGA_HIP(hipMemcpyAsync(y, S.oy.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-        if (score) HGA_HIP(hipMemcpyAsync(score, S.os.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-        if (is_good) HGA_HIP(hipMemcpyAsync(is_good, S.og.p, n, hipMemcpyDeviceToHost, c->stream));
+        if (x) HGA_HIP(hipMemcpyAsync(x, static_cast<const uint32_t*>(S.ox.p) + a, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (y) HGA_HIP(hipMemcpyAsync(y, static_cast<const uint32_t*>(S.oy.p) + a, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (score)
+            HGA_HIP(hipMemcpyAsync(score, static_cast<const uint64_t*>(S.os.p) + a, n * 8, hipMemcpyDeviceToHost, c->stream));
+        if (is_good)
+            HGA_HIP(hipMemcpyAsync(is_good, static_cast<const uint8_t*>(S.og.p) + a, n, hipMemcpyDeviceToHost, c->stream));
     }
     c->sync();
 }

@@ -318,7 +318,8 @@ void count_partition(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint
 void count_merge(hga_ctx* c, const uint64_t* keys, const uint32_t* counts, uint64_t n, uint32_t min_c);
 void connections_run(hga_ctx* c, const uint32_t* pivots, uint64_t n_piv, uint32_t min_kmers, uint64_t min_score,
                      const int32_t* categories, uint64_t* n_out);
-void connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good);
+void connections_fetch(hga_ctx* c, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good, uint64_t first = 0,
+                       uint64_t count = ~0ull);
 void count_add_rows(hga_ctx* c, uint32_t file, const uint64_t* keys, const uint32_t* counts, uint64_t n);
 int count_pack_bits(hga_ctx* c);
 uint64_t count_partition_packed(hga_ctx* c, const uint64_t* splitters, uint32_t n_own, uint64_t* out,

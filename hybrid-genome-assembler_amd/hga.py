@@ -90,6 +90,7 @@ HGA_SYMBOLS = {
     "hga_lookup_fetch": (C.c_int, [_vp, C.POINTER(LookupResult)]),
     "hga_connections_run": (C.c_int, [_vp, _u32p, C.c_uint64, C.c_uint32, C.c_uint64, _i32p, _u64p]),
     "hga_connections_fetch": (C.c_int, [_vp, _u32p, _u32p, _u64p, _u8p]),
+    "hga_connections_fetch_range": (C.c_int, [_vp, C.c_uint64, C.c_uint64, _u32p, _u32p, _u64p, _u8p]),
     "hga_hll_registers": (C.c_int, [_vp, C.c_int, C.c_uint32, _u8p]),
     "hga_profile_enable": (C.c_int, [_vp, C.c_int]),
     "hga_profile_select": (C.c_int, [_vp, C.c_char_p]),
@@ -419,6 +420,7 @@ class Ctx:
         _ck(lib().hga_connections_run(self._h, None if pv is None else _p(pv, C.c_uint32),
                                       0 if pv is None else len(pv), min_kmers, min_score,
                                       None if cat is None else _p(cat, C.c_int32), C.byref(n)))
+        self._conn_n = n.value
         return n.value
 
     def connections(self, pivots=None, min_kmers: int = 1, min_score: int = 1, categories=None):
@@ -428,6 +430,15 @@ class Ctx:
         sc, g = np.zeros(m, np.uint64), np.zeros(m, np.uint8)
         _ck(lib().hga_connections_fetch(self._h, _p(x, C.c_uint32), _p(y, C.c_uint32), _p(sc, C.c_uint64),
                                         _p(g, C.c_uint8)))
+        return x, y, sc, g
+
+    def connections_range(self, first: int, count: int):
+        """Entries [first, first + count) (clipped) of the last connections_run result."""
+        m = max(0, min(count, self._conn_n - min(first, self._conn_n)))
+        x, y = np.zeros(m, np.uint32), np.zeros(m, np.uint32)
+        sc, g = np.zeros(m, np.uint64), np.zeros(m, np.uint8)
+        _ck(lib().hga_connections_fetch_range(self._h, first, count, _p(x, C.c_uint32), _p(y, C.c_uint32),
+                                              _p(sc, C.c_uint64), _p(g, C.c_uint8)))
         return x, y, sc, g
 
     # ---- HyperLogLog auto-k (KmerAnalysis.cpp:15-56) on the reads of lookup_set_reads

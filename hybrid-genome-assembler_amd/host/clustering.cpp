@@ -598,12 +598,16 @@ std::vector<Connection> ClusteringEngine::host_connections(const std::vector<Com
 }
 
 std::vector<Connection> ClusteringEngine::get_connections(const std::vector<ComponentID>& pivots, Score min_score,
-                                                          uint32_t min_kmers) {
-    if (!(pristine_ && (gpu_ || dev_conn_))) return host_connections(pivots, min_score);
+                                                          uint32_t min_kmers, double keep_fraction) {
+    const auto prefix = [keep_fraction](std::vector<Connection> v) {
+        if (keep_fraction >= 0) v.resize(std::min(v.size(), (size_t)((double)v.size() * keep_fraction)));
+        return v;
+    };
+    if (!(pristine_ && (gpu_ || dev_conn_))) return prefix(host_connections(pivots, min_score));
     if (min_kmers == 0 && pivots.empty()) return {};   // (a null pivot list means "every read" there)
     if (dev_conn_) {
         ++gpu_calls_;
-        return dev_conn_(pivots, min_score, min_kmers);
+        return prefix(dev_conn_(pivots, min_score, min_kmers));
     }
     // construct_indices' state is on the device: hga_connections_run (connect.hip)
     std::vector<int32_t> cats;
@@ -613,22 +617,23 @@ std::vector<Connection> ClusteringEngine::get_connections(const std::vector<Comp
     if (hga_connections_run(gpu_, all ? nullptr : pivots.data(), all ? 0 : pivots.size(), all ? min_kmers : 1,
                             min_score, debug_ ? cats.data() : nullptr, &n) != HGA_OK)
         throw std::runtime_error(std::string("hga_connections_run: ") + hga_last_error());
+    if (keep_fraction >= 0) n = std::min<uint64_t>(n, (uint64_t)(size_t)((double)n * keep_fraction));
     std::vector<uint32_t> x(n), y(n);
     std::vector<uint64_t> s(n);
     std::vector<uint8_t> g(n);
-    if (hga_connections_fetch(gpu_, x.data(), y.data(), s.data(), g.data()) != HGA_OK)
-        throw std::runtime_error(std::string("hga_connections_fetch: ") + hga_last_error());
+    if (hga_connections_fetch_range(gpu_, 0, n, x.data(), y.data(), s.data(), g.data()) != HGA_OK)
+        throw std::runtime_error(std::string("hga_connections_fetch_range: ") + hga_last_error());
     ++gpu_calls_;
     std::vector<Connection> out(n);
     for (uint64_t i = 0; i < n; ++i) out[i] = {x[i], y[i], s[i], g[i] != 0};
     return out;
 }
 
-std::vector<Connection> ClusteringEngine::get_all_connections(Score min_score) {   // :335-339
-    if (pristine_ && (gpu_ || dev_conn_)) return get_connections({}, min_score, 1);
+std::vector<Connection> ClusteringEngine::get_all_connections(Score min_score, double keep_fraction) {   // :335-339
+    if (pristine_ && (gpu_ || dev_conn_)) return get_connections({}, min_score, 1, keep_fraction);
     std::vector<ComponentID> ids;
     for (auto& kv : index_) ids.push_back(kv.first);
-    return host_connections(ids, min_score);
+    return get_connections(ids, min_score, 0, keep_fraction);
 }
 
 // accumulate_kmer_ids (:341-347): merge_n_vectors(..., unique = true), a sorted set union.
@@ -1048,9 +1053,9 @@ std::vector<ComponentID> ClusteringEngine::run(std::ostream& out) {
         });
         scaffold_forming = filter_connections(conns, [&](const Connection& c) { return c.score > s; });
     } else {
-        conns = timed(out, "Calculation of connections between reads", [&] { return get_all_connections(1); });
-        const size_t keep = (size_t)((double)conns.size() * cfg_.scaffold_forming_fraction);
-        scaffold_forming.assign(conns.begin(), conns.begin() + (int64_t)std::min(keep, conns.size()));
+        // only the first size * fraction entries are used (:754-755): fetch just that prefix
+        scaffold_forming = timed(out, "Calculation of connections between reads",
+                                 [&] { return get_all_connections(1, cfg_.scaffold_forming_fraction); });
     }
     std::set<ComponentID> restricted;
     auto comps_and_trees = timed(out, "Union-find", [&] {

@@ -99,9 +99,11 @@ class ClusteringEngine {
     void export_components(const std::vector<ComponentID>& ids, const std::string& dir, std::ostream& out) const;
 
     // Stages, public for the tests.
+    // keep_fraction >= 0: return only the first (size_t)(n * keep_fraction) entries of the sorted list
+    // (the device path fetches just that prefix, hga_connections_fetch_range).
     std::vector<Connection> get_connections(const std::vector<ComponentID>& pivots, Score min_score,
-                                            uint32_t min_kmers = 0);
-    std::vector<Connection> get_all_connections(Score min_score);
+                                            uint32_t min_kmers = 0, double keep_fraction = -1.0);
+    std::vector<Connection> get_all_connections(Score min_score, double keep_fraction = -1.0);
     std::vector<ComponentID> merge_components(const std::vector<ComponentList>& components);
     void remove_merged_components();
     std::vector<ComponentID> component_ids(uint64_t threshold_size) const;

@@ -313,6 +313,11 @@ hga_status hga_connections_run(hga_ctx* ctx, const uint32_t* pivots, uint64_t n_
  * {component_x_id = x, component_y_id = y, score, is_good}
  * (src/clustering/ReadClusteringEngine.h:127-136). */
 hga_status hga_connections_fetch(hga_ctx* ctx, uint32_t* x, uint32_t* y, uint64_t* score, uint8_t* is_good);
+/* The same for entries [first, first + count) of the result (clipped to n): run_clustering keeps only the
+ * first scaffold_forming_fraction of get_all_connections' sorted list (src/clustering/ReadClusteringEngine.cpp:754-755),
+ * so the caller fetches just that prefix. */
+hga_status hga_connections_fetch_range(hga_ctx* ctx, uint64_t first, uint64_t count, uint32_t* x, uint32_t* y,
+                                       uint64_t* score, uint8_t* is_good);
 
 /* ------------------------------------------------------------------------------
  * Measurement: per-kernel device time, recorded with HIP events on the ctx stream.

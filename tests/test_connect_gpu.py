@@ -59,6 +59,19 @@ def test_connections_filters_and_pivots(gpu_ctx, golden_case):
     same(gpu_ctx.connections(pivots=dup), oracle.connections(idx, pivots=dup))
 
 
+def test_connections_fetch_range(gpu_ctx, golden_case):
+    """hga_connections_fetch_range: the prefix run_clustering keeps (:754-755) and arbitrary clipped slices."""
+    rec, g = golden_case
+    idx = lookup(gpu_ctx, rec["bases"], rec["offsets"], 19, g["sdk_keys_id_order"])
+    exp = oracle.connections(idx, min_score=1)
+    n = gpu_ctx.connections_run(min_score=1)
+    assert n == len(exp[0]) > 10
+    for first, count in ((0, int(n * 0.15)), (0, n), (3, 7), (n - 2, 100), (n, 5), (n + 9, 1), (0, 0)):
+        a = min(first, n)
+        b = min(n, a + count)
+        same(gpu_ctx.connections_range(first, count), tuple(e[a:b] for e in exp))
+
+
 @pytest.mark.parametrize("env", [None, "HGA_CN_FORCE_BLOCK", "HGA_CN_FORCE_GLOBAL", "HGA_CN_TWO_STAGE", "HGA_CN_RCAP",
                                  "HGA_CN_FULL_SORT", "HGA_CN_BIG_HITS=0", "HGA_CN_BIG_HITS=60",
                                  "HGA_CN_SEGSORT", "HGA_CN_KEY64"])
