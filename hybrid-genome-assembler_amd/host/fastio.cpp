@@ -409,82 +409,118 @@ RecordSet load_records(const std::vector<std::string>& paths, bool annotate, boo
 namespace hgah {
 
 // The iteration order of a std::unordered_set<uint64_t> (libstdc++) after inserting `keys` in order,
-// without building it: the same rehash policy object (std::__detail::_Prime_rehash_policy, whose
-// _M_need_rehash / _M_next_bkt are the library's own), std::hash<uint64_t> = identity and bucket =
-// key % bucket_count, the same node-list moves as _Hashtable::_M_insert_bucket_begin and
-// _M_rehash_aux(unique), on index arrays instead of heap nodes (no allocation per key, one int32 link
-// per key); a present key is found as _M_find_before_node finds it (its bucket's run) and not inserted.  tests/test_host.py
-// checks it against a real std::unordered_set (the oracle's or_load_sdk_text) on random key sets.
-std::vector<uint64_t> unordered_set_order(const uint64_t* keys, size_t n) {
-    constexpr int32_t NIL = -1, BB = -2;   // BB: _M_before_begin
-    std::vector<uint64_t> val;             // node i's key (nodes in insertion order)
-    val.reserve(n);
-    std::vector<int32_t> nxt;
-    nxt.reserve(n);
-    int32_t bb_next = NIL;
+// without building it.  std::hash<uint64_t> is the identity, bucket = key % bucket_count, and the node
+// list only ever changes in two ways, both "a node goes to the front of its bucket's run, a node of an
+// empty bucket to the front of the whole list": _Hashtable::_M_insert_bucket_begin for an insert, and
+// _M_rehash_aux(unique) walking the old list in order for a rehash.  So after a rehash to n buckets
+// followed by inserts, the list is the sequence S = (old list, then the new keys) regrouped: buckets in
+// decreasing order of their first element's position in S, each bucket's keys in decreasing position.
+// Rehash points depend only on the element count (the library's own _Prime_rehash_policy, asked once
+// per new key as the table asks it), so the order is built epoch by epoch with counting passes over
+// flat arrays (no per-key pointer chase), and a key already present changes nothing (insert() of a
+// duplicate).  tests/test_host.py checks it against a real std::unordered_set (the oracle's
+// or_load_sdk_text) on random key sets with and without duplicates.
+namespace {
+// a % d for any 64-bit a and d >= 1 (M = 2^128 / d rounded up; 128 fraction bits are exact for 64-bit
+// operands), a multiply-only replacement for the library's 64-bit division
+inline uint64_t fastmod_u64(uint64_t a, unsigned __int128 M, uint64_t d) {
+    const unsigned __int128 low = M * a;
+    const unsigned __int128 bot = ((unsigned __int128)(uint64_t)low * d) >> 64;
+    const unsigned __int128 top = (unsigned __int128)(uint64_t)(low >> 64) * d;
+    return (uint64_t)((bot + top) >> 64);
+}
+
+// the list order after inserting the distinct keys u in order; *nb_out = the final bucket count
+std::vector<uint64_t> order_of_distinct(const std::vector<uint64_t>& u, size_t* nb_out) {
+    const size_t U = u.size();
     std::__detail::_Prime_rehash_policy pol;
-    size_t nb = 1;                          // _M_single_bucket
-    std::vector<int32_t> bkt(1, NIL);       // NIL: empty; BB or a node: the node before the bucket's first
-    auto next_of = [&](int32_t p) { return p == BB ? bb_next : nxt[(size_t)p]; };
-    auto set_next = [&](int32_t p, int32_t v) {
-        if (p == BB) bb_next = v;
-        else nxt[(size_t)p] = v;
-    };
-    for (size_t i = 0; i < n; ++i) {
-        const uint64_t key = keys[i];
-        size_t b = (size_t)(key % nb);
-        if (bkt[b] != NIL) {   // _M_find_before_node: the bucket's run, until the bucket changes
-            bool dup = false;
-            for (int32_t p = next_of(bkt[b]); p != NIL; p = nxt[(size_t)p]) {
-                const uint64_t v = val[(size_t)p];
-                if (v == key) { dup = true; break; }
-                if ((size_t)(v % nb) != b) break;
-            }
-            if (dup) continue;   // insert() of a present key: no change
-        }
-        const size_t m = val.size();
+    std::vector<size_t> start, nbs;   // epoch e: keys [start[e], start[e+1]) inserted with nbs[e] buckets
+    size_t nb = 1;                    // _M_single_bucket
+    for (size_t m = 0; m < U; ++m) {
         const auto r = pol._M_need_rehash(nb, m, 1);
-        if (r.first) {   // _M_rehash_aux(n, true_type)
-            const size_t nn = r.second;
-            std::vector<int32_t> nbk(nn, NIL);
-            int32_t p = bb_next;
-            bb_next = NIL;
-            size_t bbegin = 0;
-            while (p != NIL) {
-                const int32_t next = nxt[(size_t)p];
-                const size_t pb = (size_t)(val[(size_t)p] % nn);
-                if (nbk[pb] == NIL) {
-                    nxt[(size_t)p] = bb_next;
-                    bb_next = p;
-                    nbk[pb] = BB;
-                    if (nxt[(size_t)p] != NIL) nbk[bbegin] = p;
-                    bbegin = pb;
-                } else {
-                    nxt[(size_t)p] = next_of(nbk[pb]);
-                    set_next(nbk[pb], p);
-                }
-                p = next;
-            }
-            bkt.swap(nbk);
-            nb = nn;
-            b = (size_t)(key % nb);
-        }
-        const int32_t node = (int32_t)m;   // _M_insert_bucket_begin
-        val.push_back(key);
-        if (bkt[b] != NIL) {
-            nxt.push_back(next_of(bkt[b]));
-            set_next(bkt[b], node);
-        } else {
-            nxt.push_back(bb_next);
-            bb_next = node;
-            if (nxt[m] != NIL) bkt[(size_t)(val[(size_t)nxt[m]] % nb)] = node;
-            bkt[b] = BB;
+        if (r.first) {
+            nb = r.second;
+            start.push_back(m);
+            nbs.push_back(nb);
         }
     }
-    std::vector<uint64_t> out;
-    out.reserve(val.size());
-    for (int32_t p = bb_next; p != NIL; p = nxt[(size_t)p]) out.push_back(val[(size_t)p]);
-    return out;
+    if (U && (start.empty() || start[0] != 0)) {
+        start.insert(start.begin(), 0);
+        nbs.insert(nbs.begin(), 1);
+    }
+    *nb_out = nb;
+    std::vector<uint64_t> cur, seq;
+    std::vector<uint32_t> bk, cnt, firsts;
+    for (size_t e = 0; e < start.size(); ++e) {
+        const size_t a = start[e], b = e + 1 < start.size() ? start[e + 1] : U, nbe = nbs[e];
+        seq.assign(cur.begin(), cur.end());
+        seq.insert(seq.end(), u.begin() + (int64_t)a, u.begin() + (int64_t)b);
+        const size_t L = seq.size();
+        const unsigned __int128 M = ~(unsigned __int128)0 / nbe + 1;
+        bk.resize(L);
+        cnt.assign(nbe, 0);
+        firsts.clear();
+        for (size_t j = 0; j < L; ++j) {
+            const uint32_t bj = (uint32_t)fastmod_u64(seq[j], M, nbe);
+            bk[j] = bj;
+            if (cnt[bj]++ == 0) firsts.push_back(bj);
+        }
+        uint32_t pos = 0;   // buckets by decreasing first position: cnt becomes each bucket's cursor
+        for (size_t t = firsts.size(); t-- > 0;) {
+            const uint32_t c = cnt[firsts[t]];
+            cnt[firsts[t]] = pos;
+            pos += c;
+        }
+        cur.resize(L);
+        for (size_t j = L; j-- > 0;) cur[cnt[bk[j]]++] = seq[j];   // decreasing position inside a bucket
+    }
+    return cur;
+}
+}  // namespace
+
+std::vector<uint64_t> unordered_set_order(const uint64_t* keys, size_t n) {
+    if (n >= (1ull << 32)) throw std::invalid_argument("too many k-mers");
+    size_t nb = 1;
+    // SDK lines are almost always distinct: order them as such, then look for a repeat inside the final
+    // bucket runs (equal keys share a bucket); only then take the distinct keys in first-occurrence order
+    std::vector<uint64_t> u(keys, keys + n);
+    std::vector<uint64_t> out = order_of_distinct(u, &nb);
+    bool dup = false;
+    {
+        const unsigned __int128 M = ~(unsigned __int128)0 / nb + 1;
+        size_t r0 = 0;
+        uint64_t b0 = n ? fastmod_u64(out[0], M, nb) : 0;
+        std::vector<uint64_t> run;
+        for (size_t j = 1; j <= n && !dup; ++j) {
+            const uint64_t bj = j < n ? fastmod_u64(out[j], M, nb) : ~0ull;
+            if (bj == b0) continue;
+            if (j - r0 > 1) {   // the bucket run [r0, j)
+                run.assign(out.begin() + (int64_t)r0, out.begin() + (int64_t)j);
+                std::sort(run.begin(), run.end());
+                dup = std::adjacent_find(run.begin(), run.end()) != run.end();
+            }
+            r0 = j;
+            b0 = bj;
+        }
+    }
+    if (!dup) return out;
+    u.clear();
+    int lg = 4;
+    while ((1ull << lg) < 2 * n) ++lg;
+    const size_t cap = 1ull << lg, msk = cap - 1;
+    std::vector<uint64_t> slot(cap);
+    std::vector<uint8_t> used(cap, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t key = keys[i];
+        size_t h = (size_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - lg));
+        while (used[h] && slot[h] != key) h = (h + 1) & msk;
+        if (!used[h]) {
+            used[h] = 1;
+            slot[h] = key;
+            u.push_back(key);
+        }
+    }
+    return order_of_distinct(u, &nb);
 }
 
 // load_text_file_kmers (src/read_clustering.cpp:18-33) without its per-line cost: the file mapped, its

@@ -179,7 +179,7 @@ def test_kmer_text_loader_matches_unordered_set(tmp_path, n, dup_frac, eol):
 
 @pytest.mark.parametrize("n", [0, 1, 2, 11, 12, 13, 24, 100, 5000, 200_000])
 def test_unordered_set_order_matches_libstdcxx(n):
-    """unordered_set_order (an array simulation of libstdc++'s node list and rehashes) against a real
+    """unordered_set_order (libstdc++'s node list regrouped epoch by epoch between its rehashes) against a real
     std::unordered_set<uint64_t>: the oracle's load_text_file_kmers fills one from lines written so that
     each line's canonical code is the key itself (31-mers, the smaller strand), duplicates included."""
     import hga as hga_mod
