@@ -675,12 +675,14 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
     // list is sorted before use
     std::vector<std::vector<uint64_t>> pairs((size_t)HT);
     std::vector<uint8_t> mark;
+    double t_members = 0, t_union = 0, t_pairs = 0;   // (HGA_TIMING parts of merge.groups)
     for (const ComponentList& ids : components) {
         if (ids.empty()) continue;   // (an empty spectral cluster would dereference ids[0] there)
         if (ids.size() == 1) {
             merged_ids.push_back(ids[0]);
             continue;
         }
+        const auto q0 = clk::now();
         std::set<int32_t> cats;
         std::vector<uint32_t> contained;
         size_t total = 0;
@@ -693,6 +695,7 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
             total += c.kmers.size();
             km[i] = &c.kmers;
         }
+        const auto q1 = clk::now();
         std::vector<KmerID> acc;
         if (total > nk / 16 + 64) {   // accumulate_kmer_ids as a mark pass (ids < nk), both halves threaded
             if (mark.empty()) mark.assign(nk, 0);
@@ -718,12 +721,20 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
         survivor.reads = contained;
         merged_ids.push_back(ids[0]);
         km[0] = &survivor.kmers;
+        const auto q2 = clk::now();
         par(ids.size(), 64, [&](int t, size_t a, size_t b) {
             auto& pv = pairs[(size_t)t];
+            size_t add = 0;
+            for (size_t i = a; i < b; ++i) add += km[i]->size();
+            if (pv.capacity() < pv.size() + add) pv.reserve(std::max(pv.size() + add, 2 * pv.capacity()));
             for (size_t i = a; i < b; ++i)
                 for (KmerID kid : *km[i]) pv.push_back((uint64_t)kid << 32 | ids[i]);
         });
         pristine_ = false;
+        const auto q3 = clk::now();
+        t_members += std::chrono::duration<double, std::milli>(q1 - q0).count();
+        t_union += std::chrono::duration<double, std::milli>(q2 - q1).count();
+        t_pairs += std::chrono::duration<double, std::milli>(q3 - q2).count();
     }
     size_t npairs = 0;
     for (auto& pv : pairs) npairs += pv.size();
@@ -788,7 +799,9 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
             if (start[kid] == start[kid + 1]) continue;
             ComponentID* rb = rem.data() + start[kid];
             ComponentID* re = rem.data() + start[kid + 1];
-            std::sort(rb, re);
+            // (the scatter keeps each pair vector's member order, so with ascending member lists the
+            // removal list usually arrives sorted)
+            if (!std::is_sorted(rb, re)) std::sort(rb, re);
             std::vector<ComponentID>& list = kci_[kid];
             updated.clear();
             size_t j = 0;
@@ -820,7 +833,12 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
     for (auto& x : th) x.join();
     if (const char* te = std::getenv("HGA_TIMING"); te && std::string(te) == "1") {
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "hga-timing merge.groups %.2f\nhga-timing merge.kci_update %.2f\n", ms(t_start, t_groups),
+        static int call = 0;   // one set of lines per call: merge<call>.*
+        ++call;
+        std::fprintf(stderr,
+                     "hga-timing merge%d.groups %.2f\nhga-timing merge%d.members %.2f\nhga-timing merge%d.union %.2f\n"
+                     "hga-timing merge%d.pairs %.2f\nhga-timing merge%d.kci_update %.2f\n",
+                     call, ms(t_start, t_groups), call, t_members, call, t_union, call, t_pairs, call,
                      ms(t_groups, clk::now()));
     }
     return merged_ids;
