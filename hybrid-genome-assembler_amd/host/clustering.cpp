@@ -794,7 +794,6 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
     // kmer_component_index update (:395-419), including its early stop: once the removal list
     // is exhausted the rest of the kmer's list is not copied
     auto update = [&](size_t k0, size_t k1) {
-        std::vector<ComponentID> updated;
         for (size_t kid = k0; kid < k1; ++kid) {
             if (start[kid] == start[kid + 1]) continue;
             ComponentID* rb = rem.data() + start[kid];
@@ -803,20 +802,18 @@ std::vector<ComponentID> ClusteringEngine::merge_components(const std::vector<Co
             // removal list usually arrives sorted)
             if (!std::is_sorted(rb, re)) std::sort(rb, re);
             std::vector<ComponentID>& list = kci_[kid];
-            updated.clear();
-            size_t j = 0;
+            size_t j = 0, w = 0;   // kept entries compacted in place (w <= j): the reference's `updated`
             for (ComponentID* r = rb; r < re && j < list.size();) {
                 if (*r < list[j]) {
                     ++r;
                 } else if (list[j] < *r) {
-                    updated.push_back(list[j]);
-                    ++j;
+                    list[w++] = list[j++];
                 } else {
                     ++r;
                     ++j;
                 }
             }
-            list.assign(updated.begin(), updated.end());
+            list.resize(w);
         }
     };
     const int T = std::max(1, std::min<int>(host_threads(), (int)(rem.size() >> 16) + 1));
